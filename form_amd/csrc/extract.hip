@@ -1,0 +1,586 @@
+// extract.hip — stage 1: per-scan feature extraction on gfx950.
+//
+// Restates form::FeatureExtractor::extract (form/feature/extraction.tpp:29-132) as
+//   k_extract_rows : one workgroup per scan line.  The row is staged in LDS;
+//                    validity masks (:136-222), LOAM curvature (:226-261), the
+//                    per-sector greedy planar selection (:44-68, :332-358) and the
+//                    point selection (:70-96, :360-399).
+//   k_closest      : one wave per selected planar point; wave-wide argmin over
+//                    the adjacent scan lines (find_closest, :402-420).
+//   k_fit          : one lane per selected planar point; neighbour gather
+//                    (find_neighbors, :422-448), A^T A covariance and the smallest
+//                    eigenvector (compute_normal, :263-329).
+//   k_row_scan / k_write_features : ordered compaction into the query arrays.
+//
+// Greedy planar selection.  The reference sorts each sector by curvature and
+// accepts, in that order, every still-unused point under the threshold, clearing
+// +-(k-1) columns around it, until planar_feats_per_sector+1 are accepted.  With a
+// strict total order on (curvature, column) that greedy result equals the greedy
+// maximal independent set computed in parallel rounds (a candidate that is the
+// minimum of its undecided +-(k-1) neighbourhood is accepted, its neighbours are
+// removed), truncated to the P+1 smallest keys.  Sectors stay sequential: the
+// suppression of sector s spills into sector s+1 (parity hazard 5).
+#include "fmx_device.hpp"
+#include "fmx_internal.hpp"
+
+#include <cfloat>
+
+namespace fmx {
+namespace {
+
+constexpr int kRowThreads = 256;
+
+struct ExArgs {
+  int R, C, k, S, P, Ppt;
+  int cap_pl, cap_pt;  // per-row slot capacities
+  double thr, min2, max2, radius2;
+  int min_points;
+};
+
+// key order for the greedy: (curvature, column)
+__device__ __forceinline__ bool key_less(const float* curv, int a, int b) {
+  const float ca = curv[a], cb = curv[b];
+  return ca < cb || (ca == cb && a < b);
+}
+
+// Ordered (stable) block compaction of flag(c) for c in [b, e) into list[0..n).
+// Returns n (uniform).  Uses ws[kRowThreads/64 + 1].
+template <class F>
+__device__ int block_compact(int b, int e, F flag, int* list, int* ws) {
+  const int tid = threadIdx.x, w = tid / kWave;
+  int base = 0;
+  for (int t0 = b; t0 < e; t0 += kRowThreads) {
+    const int c = t0 + tid;
+    const bool f = c < e && flag(c);
+    const uint64_t m = __ballot(f);
+    if (lane_id() == 0) ws[w] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int i = 0; i < w; ++i) off += ws[i];
+    int tot = 0;
+    for (int i = 0; i < kRowThreads / kWave; ++i) tot += ws[i];
+    if (f) list[off + __popcll(m & lanemask_lt())] = c;
+    __syncthreads();
+    base += tot;
+  }
+  return base;
+}
+
+__global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __restrict__ scan, ExArgs a,
+                                                              uint8_t* __restrict__ planar_mask,
+                                                              uint32_t* __restrict__ sel_slots,
+                                                              uint32_t* __restrict__ pt_slots,
+                                                              uint32_t* __restrict__ row_counts) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int C = a.C, r = blockIdx.x, tid = threadIdx.x, k = a.k;
+  float4* pts = reinterpret_cast<float4*>(smem);
+  float* curv = reinterpret_cast<float*>(pts + C);
+  int* list = reinterpret_cast<int*>(curv + C);
+  uint8_t* flg = reinterpret_cast<uint8_t*>(list + C);  // bit0 point-valid, bit1 out-of-range, bit2 planar-valid
+  uint8_t* used = flg + C;                               // used_points (planar) then point mask
+  uint8_t* state = used + C;
+  uint8_t* win = state + C;
+  __shared__ int ws[kRowThreads / kWave + 1];
+  __shared__ int s_cnt;
+
+  const float4* row = scan + (size_t)r * C;
+  for (int c = tid; c < C; c += kRowThreads) pts[c] = row[c];
+  __syncthreads();
+
+  // compute_valid_points / compute_point_valid_points (extraction.tpp:136-222)
+  for (int c = tid; c < C; c += kRowThreads) {
+    uint8_t f = 0;
+    if (c >= k && c < C - k) {
+      const float4 p = pts[c];
+      const double r2 = (double)sqnorm4f(p.x, p.y, p.z);
+      const bool oor = r2 < a.min2 || r2 > a.max2;
+      f = oor ? 2 : 1;
+    }
+    flg[c] = f;
+  }
+  __syncthreads();
+  // planar validity: neighbour invalidation of +-k around out-of-range points
+  // (scatter at :170-173, evaluated here as a gather), then the curvature (:226-261).
+  for (int c = tid; c < C; c += kRowThreads) {
+    bool plv = (flg[c] & 1) != 0;
+    if (plv) {
+      for (int d = 1; d <= k; ++d) {
+        if (c - d >= 0 && (flg[c - d] & 2)) plv = false;
+        if (c + d < C && (flg[c + d] & 2)) plv = false;
+      }
+    }
+    float cv = FLT_MAX;
+    if (plv) {
+      const float4 p = pts[c];
+      double dx = -(2.0 * k) * (double)p.x;
+      double dy = -(2.0 * k) * (double)p.y;
+      double dz = -(2.0 * k) * (double)p.z;
+      for (int n = 1; n <= k; ++n) {
+        const float4 qm = pts[c - n], qp = pts[c + n];
+        dx = dx + (double)qm.x + (double)qp.x;
+        dy = dy + (double)qm.y + (double)qp.y;
+        dz = dz + (double)qm.z + (double)qp.z;
+      }
+      cv = (float)(dx * dx + dy * dy + dz * dz);
+    }
+    curv[c] = cv;
+    win[c] = plv ? 1 : 0;
+    planar_mask[(size_t)r * C + c] = plv ? 1 : 0;
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kRowThreads) {
+    if (win[c]) flg[c] |= 4;
+    used[c] = win[c];
+  }
+  __syncthreads();
+
+  // ---------------- planar features: sectors in order (extraction.tpp:44-68)
+  const int pps = C / a.S;
+  int pl_count = 0;  // uniform
+  for (int s = 0; s < a.S; ++s) {
+    const int b = s * pps;
+    const int e = (s == a.S - 1) ? C : b + pps;
+    for (int c = b + tid; c < e; c += kRowThreads) {
+      state[c] = (used[c] && (double)curv[c] < a.thr) ? 1 : 0;  // 1 = undecided candidate
+      win[c] = 0;
+    }
+    __syncthreads();
+    // parallel greedy MIS in (curvature, column) order, conflict radius k-1
+    for (;;) {
+      for (int c = b + tid; c < e; c += kRowThreads) {
+        if (state[c] != 1) continue;
+        bool w = true;
+        for (int d = 1; d < k && w; ++d) {
+          const int cl = c - d, cr = c + d;
+          if (cl >= b && state[cl] == 1 && key_less(curv, cl, c)) w = false;
+          if (cr < e && state[cr] == 1 && key_less(curv, cr, c)) w = false;
+        }
+        win[c] = w ? 1 : 0;
+      }
+      __syncthreads();
+      int undecided = 0;
+      for (int c = b + tid; c < e; c += kRowThreads) {
+        if (state[c] != 1) continue;
+        if (win[c]) {
+          state[c] = 2;  // accepted
+        } else {
+          bool rm = false;
+          for (int d = 1; d < k && !rm; ++d) {
+            if (c - d >= b && win[c - d]) rm = true;
+            if (c + d < e && win[c + d]) rm = true;
+          }
+          if (rm) state[c] = 3;
+          else undecided = 1;
+        }
+      }
+      if (!__syncthreads_or(undecided)) break;
+      for (int c = b + tid; c < e; c += kRowThreads) win[c] = 0;
+      __syncthreads();
+    }
+    // accepted set -> ranks in key order; keep the P+1 smallest (break at :354)
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    for (int c = b + tid; c < e; c += kRowThreads)
+      if (state[c] == 2) list[atomicAdd(&s_cnt, 1)] = c;
+    __syncthreads();
+    const int n_acc = s_cnt;
+    const int keep = n_acc < a.P + 1 ? n_acc : a.P + 1;
+    for (int i = tid; i < n_acc; i += kRowThreads) {
+      const int c = list[i];
+      int rank = 0;
+      for (int j = 0; j < n_acc; ++j) rank += key_less(curv, list[j], c) ? 1 : 0;
+      if (rank < keep) {
+        sel_slots[(size_t)r * a.cap_pl + pl_count + rank] = (uint32_t)c;
+        state[c] = 4;
+      }
+    }
+    __syncthreads();
+    // suppression used[c +- n], n in [0, k) (:347-350)
+    for (int c = b + tid; c < e; c += kRowThreads) {
+      if (state[c] != 4) continue;
+      for (int n = 0; n < k; ++n) {
+        used[c + n] = 0;
+        used[c - n] = 0;
+      }
+    }
+    pl_count += keep;
+    __syncthreads();
+  }
+
+  // ---------------- point features (extraction.tpp:70-96)
+  // eligible = (used == planar_valid) && point_valid  (:77-79)
+  for (int c = tid; c < C; c += kRowThreads) {
+    const uint8_t f = flg[c];
+    win[c] = ((f & 1) && (used[c] == ((f >> 2) & 1))) ? 1 : 0;
+  }
+  __syncthreads();
+  int pt_count = 0;  // uniform (broadcast through s_cnt)
+  for (int s = 0; s < a.S; ++s) {
+    const int b = s * pps;
+    const int e = (s == a.S - 1) ? C : b + pps;
+    const int nu = block_compact(b, e, [&](int c) { return win[c] != 0; }, list, ws);
+    if (tid == 0) {
+      // extract_point (:360-399), literal: factor passes with the per-offset break
+      int nf = 0;
+      if (a.Ppt > 0) {
+        const int factor = 1 + nu / a.Ppt;
+        for (int off = 0; off < factor; ++off) {
+          for (int ui = off; ui < nu; ui += factor) {
+            const int c = list[ui];
+            if (win[c]) {
+              pt_slots[(size_t)r * a.cap_pt + pt_count + nf] = (uint32_t)c;
+              for (int n = 0; n < k; ++n) {
+                win[c + n] = 0;
+                win[c - n] = 0;
+              }
+              nf++;
+            }
+            if (nf > a.Ppt) break;
+          }
+        }
+      }
+      s_cnt = pt_count + nf;
+    }
+    __syncthreads();
+    pt_count = s_cnt;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    row_counts[2 * r] = (uint32_t)pl_count;
+    row_counts[2 * r + 1] = (uint32_t)pt_count;
+  }
+}
+
+// find_closest (extraction.tpp:402-420) over rows r-1 and r+1: one wave per slot.
+__global__ __launch_bounds__(256) void k_closest(const float4* __restrict__ scan,
+                                                 const uint8_t* __restrict__ mask,
+                                                 const uint32_t* __restrict__ sel_slots,
+                                                 const uint32_t* __restrict__ row_counts, int R, int C,
+                                                 int cap, int2* __restrict__ closest) {
+  const int wv = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
+  const int r = wv / cap, slot = wv % cap;
+  if (r >= R) return;
+  if ((uint32_t)slot >= row_counts[2 * r]) return;
+  const int lane = lane_id();
+  const int c = (int)sel_slots[(size_t)r * cap + slot];
+  const float4 p = scan[(size_t)r * C + c];
+  int res[2];
+  for (int dir = 0; dir < 2; ++dir) {
+    const int rr = dir == 0 ? r - 1 : r + 1;
+    res[dir] = -1;
+    if (rr < 0 || rr >= R) continue;
+    const float4* row = scan + (size_t)rr * C;
+    const uint8_t* mrow = mask + (size_t)rr * C;
+    float best = 0.f;
+    int bj = -1;
+    for (int j = lane; j < C; j += kWave) {
+      if (!mrow[j]) continue;
+      const float d = dist2f(row[j], p);
+      // reference: double(d) < min_dist2 (init DBL_MAX), so only finite d qualify
+      if (d <= FLT_MAX && (bj < 0 || d < best)) {
+        best = d;
+        bj = j;
+      }
+    }
+    // lexicographic (found, d, j) wave argmin
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oj = __shfl_xor(bj, o, 64);
+      if (oj >= 0 && (bj < 0 || ob < best || (ob == best && oj < bj))) {
+        best = ob;
+        bj = oj;
+      }
+    }
+    res[dir] = bj < 0 ? -1 : rr * C + bj;
+  }
+  if (lane == 0) closest[(size_t)r * cap + slot] = make_int2(res[0], res[1]);
+}
+
+// Cyclic Jacobi on the symmetric 3x3 covariance in double; returns the unit
+// eigenvector of the smallest eigenvalue (Eigen::SelfAdjointEigenSolver col(0)).
+__device__ void smallest_eigvec(const float cov[3][3], double n[3]) {
+  double A[3][3], V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) A[i][j] = (double)cov[i][j];
+  for (int sweep = 0; sweep < 64; ++sweep) {
+    const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
+    const double dia = A[0][0] * A[0][0] + A[1][1] * A[1][1] + A[2][2] * A[2][2];
+    if (off <= 1e-36 * dia || off == 0.0) break;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+#pragma unroll
+      for (int qq = pp + 1; qq < 3; ++qq) {
+        const double apq = A[pp][qq];
+        if (apq == 0.0) continue;
+        const double theta = (A[qq][qq] - A[pp][pp]) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double cc = 1.0 / sqrt(t * t + 1.0), ss = t * cc;
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          const double amp = A[m][pp], amq = A[m][qq];
+          A[m][pp] = cc * amp - ss * amq;
+          A[m][qq] = ss * amp + cc * amq;
+        }
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          const double apm = A[pp][m], aqm = A[qq][m];
+          A[pp][m] = cc * apm - ss * aqm;
+          A[qq][m] = ss * apm + cc * aqm;
+        }
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          const double vmp = V[m][pp], vmq = V[m][qq];
+          V[m][pp] = cc * vmp - ss * vmq;
+          V[m][qq] = ss * vmp + cc * vmq;
+        }
+      }
+    }
+  }
+  int mi = 0;
+  if (A[1][1] < A[mi][mi]) mi = 1;
+  if (A[2][2] < A[mi][mi]) mi = 2;
+  double v0 = mi == 0 ? V[0][0] : (mi == 1 ? V[0][1] : V[0][2]);
+  double v1 = mi == 0 ? V[1][0] : (mi == 1 ? V[1][1] : V[1][2]);
+  double v2 = mi == 0 ? V[2][0] : (mi == 1 ? V[2][1] : V[2][2]);
+  const double nn = sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+  n[0] = v0 / nn;
+  n[1] = v1 / nn;
+  n[2] = v2 / nn;
+}
+
+// compute_normal (extraction.tpp:263-329): one lane per selected planar point.
+__global__ __launch_bounds__(256) void k_fit(const float4* __restrict__ scan,
+                                             const uint32_t* __restrict__ sel_slots,
+                                             const uint32_t* __restrict__ row_counts,
+                                             const int2* __restrict__ closest, ExArgs a,
+                                             float4* __restrict__ nrm_slots,
+                                             uint32_t* __restrict__ row_ok) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = g / a.cap_pl, slot = g % a.cap_pl;
+  if (r >= a.R) return;
+  if ((uint32_t)slot >= row_counts[2 * r]) return;
+  const int C = a.C, k = a.k;
+  const size_t idx = (size_t)r * C + sel_slots[(size_t)r * a.cap_pl + slot];
+  const float4 p = scan[idx];
+  const int2 cl = closest[(size_t)r * a.cap_pl + slot];
+  const double r2 = a.radius2;
+  // visit(q): the neighbour sequence of the reference, in push order
+  auto walk = [&](auto&& visit) {
+    auto nbrs = [&](size_t j) {  // find_neighbors(j) (:422-448)
+      const float4 pj = scan[j];
+      for (int i = 1; i <= k; ++i) {
+        const float4 q = scan[j + i];
+        if ((double)dist2f(q, pj) < r2) visit(q);
+        else break;
+      }
+      for (int i = 1; i <= k; ++i) {
+        const float4 q = scan[j - i];
+        if ((double)dist2f(q, pj) < r2) visit(q);
+        else break;
+      }
+    };
+    nbrs(idx);
+    if (cl.x >= 0) {
+      visit(scan[cl.x]);
+      nbrs((size_t)cl.x);
+    }
+    if (cl.y >= 0) {
+      visit(scan[cl.y]);
+      nbrs((size_t)cl.y);
+    }
+  };
+  int cnt = 0;
+  walk([&](float4) { ++cnt; });
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((cl.x >= 0 || cl.y >= 0) && cnt >= a.min_points) {
+    const float nf = (float)cnt;
+    float cov[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    walk([&](float4 q) {
+      const float ax = (q.x - p.x) / nf, ay = (q.y - p.y) / nf, az = (q.z - p.z) / nf;
+      const float av[3] = {ax, ay, az};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) cov[i][j] = cov[i][j] + av[i] * av[j];
+    });
+    double n[3];
+    smallest_eigvec(cov, n);
+    const double dp = (n[0] * (double)p.x + n[1] * (double)p.y) + n[2] * (double)p.z;
+    if (dp > 0) {
+      n[0] = -n[0];
+      n[1] = -n[1];
+      n[2] = -n[2];
+    }
+    out = make_float4((float)n[0], (float)n[1], (float)n[2], 1.0f);  // w = 1: normal found
+    atomicAdd(&row_ok[r], 1u);
+  }
+  nrm_slots[(size_t)r * a.cap_pl + slot] = out;
+}
+
+// per-row offsets of {planar with normal, points, planar selected}: one block
+__global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, const uint32_t* row_ok, int R,
+                                                   uint32_t* row_off /* [3][R+1] */) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry[3];
+  if (threadIdx.x < 3) carry[threadIdx.x] = 0;
+  __syncthreads();
+  for (int r0 = 0; r0 < R; r0 += 1024) {
+    const int r = r0 + threadIdx.x;
+    for (int t = 0; t < 3; ++t) {
+      uint32_t v = 0;
+      if (r < R) v = t == 0 ? row_ok[r] : (t == 1 ? row_counts[2 * r + 1] : row_counts[2 * r]);
+      const uint32_t incl = wave_incl_scan(v);
+      const int w = threadIdx.x / kWave;
+      if (lane_id() == 63) ws[w] = incl;
+      __syncthreads();
+      uint32_t off = 0, tot = 0;
+      for (int i = 0; i < 16; ++i) {
+        if (i < w) off += ws[i];
+        tot += ws[i];
+      }
+      if (r < R) row_off[t * (R + 1) + r] = carry[t] + off + incl - v;
+      __syncthreads();
+      if (threadIdx.x == 0) carry[t] += tot;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x < 3) row_off[threadIdx.x * (R + 1) + R] = carry[threadIdx.x];
+}
+
+// ordered compaction of row slots into the query arrays (block per row)
+__global__ __launch_bounds__(256) void k_write_features(const float4* __restrict__ scan, ExArgs a,
+                                                        const uint32_t* __restrict__ row_counts,
+                                                        const uint32_t* __restrict__ row_off,
+                                                        const uint32_t* __restrict__ sel_slots,
+                                                        const uint32_t* __restrict__ pt_slots,
+                                                        const float4* __restrict__ nrm_slots,
+                                                        float4* __restrict__ pl_pos, float4* __restrict__ pl_nrm,
+                                                        uint32_t* __restrict__ pl_idx,
+                                                        float4* __restrict__ pt_pos, uint32_t* __restrict__ pt_idx) {
+  __shared__ int ws[4];
+  const int r = blockIdx.x, tid = threadIdx.x, w = tid / kWave;
+  const int R = a.R, C = a.C;
+  const uint32_t nsel = row_counts[2 * r], npt = row_counts[2 * r + 1];
+  uint32_t base = row_off[r];
+  for (uint32_t s0 = 0; s0 < nsel; s0 += 256) {
+    const uint32_t s = s0 + tid;
+    const bool ok = s < nsel && nrm_slots[(size_t)r * a.cap_pl + s].w != 0.f;
+    const uint64_t m = __ballot(ok);
+    if (lane_id() == 0) ws[w] = __popcll(m);
+    __syncthreads();
+    uint32_t off = base, tot = 0;
+    for (int i = 0; i < 4; ++i) {
+      if (i < w) off += ws[i];
+      tot += ws[i];
+    }
+    if (ok) {
+      const uint32_t o = off + __popcll(m & lanemask_lt());
+      const uint32_t idx = (uint32_t)r * C + sel_slots[(size_t)r * a.cap_pl + s];
+      const float4 p = scan[idx];
+      const float4 n = nrm_slots[(size_t)r * a.cap_pl + s];
+      pl_pos[o] = make_float4(p.x, p.y, p.z, 0.f);
+      pl_nrm[o] = make_float4(n.x, n.y, n.z, 0.f);
+      pl_idx[o] = idx;
+    }
+    __syncthreads();
+    base += tot;
+  }
+  const uint32_t pbase = row_off[(R + 1) + r];
+  for (uint32_t s = tid; s < npt; s += 256) {
+    const uint32_t idx = (uint32_t)r * C + pt_slots[(size_t)r * a.cap_pt + s];
+    const float4 p = scan[idx];
+    pt_pos[pbase + s] = make_float4(p.x, p.y, p.z, 0.f);
+    pt_idx[pbase + s] = idx;
+  }
+}
+
+}  // namespace
+
+void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out) {
+  const auto& E = c->P.extraction;
+  ExArgs a;
+  a.R = R;
+  a.C = C;
+  a.k = (int)E.neighbor_points;
+  a.S = (int)E.num_sectors;
+  a.P = (int)E.planar_feats_per_sector;
+  a.Ppt = (int)E.point_feats_per_sector;
+  a.cap_pl = a.S * (a.P + 1);
+  a.cap_pt = a.k > 0 ? C / a.k + 1 : C;
+  a.thr = E.planar_threshold;
+  a.min2 = E.min_norm_squared;
+  a.max2 = E.max_norm_squared;
+  a.radius2 = E.radius * E.radius;
+  a.min_points = (int)E.min_points;
+  hipStream_t st = c->stream;
+  const size_t N = (size_t)R * C;
+  c->planar_mask.ensure(N);
+  c->sel_slots.ensure((size_t)R * a.cap_pl);
+  c->pt_slots.ensure((size_t)R * a.cap_pt);
+  c->row_counts.ensure(2 * (size_t)R);
+  c->row_ok.ensure(R);
+  c->row_off.ensure(3 * ((size_t)R + 1));
+  c->closest.ensure((size_t)R * a.cap_pl);
+  c->nrm_slots.ensure((size_t)R * a.cap_pl);
+  c->h_u32.ensure(8);
+  c->rows = R;
+  c->cols = C;
+  const size_t lds = (size_t)C * (16 + 4 + 4 + 4);
+  if (!c->lds_attr_set) {
+    FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extract_rows),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * (16 + 4 + 4 + 4)));
+    c->lds_attr_set = true;
+  }
+  {
+    ProfScope ps(c->prof, PROF_EXTRACT_ROWS, 16.0 * N + N, st);
+    hipLaunchKernelGGL(k_extract_rows, dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                       c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+  }
+  FMX_HIP(hipGetLastError());
+  FMX_HIP(hipMemsetAsync(c->row_ok.p, 0, R * sizeof(uint32_t), st));
+  const int nslots = R * a.cap_pl;
+  {
+    ProfScope ps(c->prof, PROF_CLOSEST, 0.0, st);
+    hipLaunchKernelGGL(k_closest, dim3((nslots + 3) / 4), dim3(256), 0, st, d_scan, c->planar_mask.p,
+                       c->sel_slots.p, c->row_counts.p, R, C, a.cap_pl, c->closest.p);
+  }
+  {
+    ProfScope ps(c->prof, PROF_FIT, 0.0, st);
+    hipLaunchKernelGGL(k_fit, dim3((nslots + 255) / 256), dim3(256), 0, st, d_scan, c->sel_slots.p,
+                       c->row_counts.p, c->closest.p, a, c->nrm_slots.p, c->row_ok.p);
+  }
+  {
+    ProfScope ps(c->prof, PROF_COMPACT, 0.0, st);
+    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, st, c->row_counts.p, c->row_ok.p, R, c->row_off.p);
+  }
+  FMX_HIP(hipGetLastError());
+  // totals: planar-with-normal, points, selected
+  FMX_HIP(hipMemcpyAsync(c->h_u32.p + 0, c->row_off.p + R, 4, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(c->h_u32.p + 1, c->row_off.p + (R + 1) + R, 4, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(c->h_u32.p + 2, c->row_off.p + 2 * (R + 1) + R, 4, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
+  c->q_pl_pos.ensure(npl + 1);
+  c->q_pl_nrm.ensure(npl + 1);
+  c->q_pl_idx.ensure(npl + 1);
+  c->q_pt_pos.ensure(npt + 1);
+  c->q_pt_idx.ensure(npt + 1);
+  {
+    ProfScope ps(c->prof, PROF_COMPACT, 32.0 * npl + 16.0 * npt, st);
+    hipLaunchKernelGGL(k_write_features, dim3(R), dim3(256), 0, st, d_scan, a, c->row_counts.p, c->row_off.p,
+                       c->sel_slots.p, c->pt_slots.p, c->nrm_slots.p, c->q_pl_pos.p, c->q_pl_nrm.p,
+                       c->q_pl_idx.p, c->q_pt_pos.p, c->q_pt_idx.p);
+  }
+  FMX_HIP(hipGetLastError());
+  c->n_qpl = npl;
+  c->n_qpt = npt;
+  c->n_sel = nsel;
+  if (out) {
+    out->planar = npl;
+    out->point = npt;
+    out->planar_selected = nsel;
+  }
+}
+
+}  // namespace fmx

@@ -1,0 +1,925 @@
+// fmx_api.cpp — C-ABI entry points (include/fmx/fmx.h) and the host adapter that
+// mirrors form::Estimator::register_scan (form/form.cpp:40-114) on top of the
+// device stages.  Host code only; built with hipcc -ffp-contract=off so the pose
+// algebra rounds like the reference's SSE2 Eigen/GTSAM code.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <new>
+#include <set>
+#include <vector>
+
+#include "fmx_internal.hpp"
+
+using namespace fmx;
+
+// ============================================================================ profiling
+namespace fmx {
+static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest", "fit",      "compact",   "map_build",
+                                             "match",        "pair_sort", "linearize", "error_eval", "insert"};
+
+ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), bytes(by), st(s) {
+  if (!pr.on) return;
+  auto get = [&]() {
+    hipEvent_t e;
+    if (!pr.free_events.empty()) {
+      e = pr.free_events.back();
+      pr.free_events.pop_back();
+    } else {
+      FMX_HIP(hipEventCreate(&e));
+    }
+    return e;
+  };
+  a = get();
+  b = get();
+  FMX_HIP(hipEventRecord(a, st));
+}
+ProfScope::~ProfScope() {
+  if (!a) return;
+  (void)hipEventRecord(b, st);
+  pr.pending.push_back({id, {a, b}});
+  pr.pending_bytes.push_back(bytes);
+}
+static void prof_collect(fmx_ctx* c) {
+  Prof& pr = c->prof;
+  if (pr.pending.empty()) return;
+  FMX_HIP(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < pr.pending.size(); ++i) {
+    auto& [id, ev] = pr.pending[i];
+    float ms = 0.f;
+    FMX_HIP(hipEventElapsedTime(&ms, ev.first, ev.second));
+    pr.ms[id] += ms;
+    pr.launches[id] += 1;
+    pr.bytes[id] += pr.pending_bytes[i];
+    pr.free_events.push_back(ev.first);
+    pr.free_events.push_back(ev.second);
+  }
+  pr.pending.clear();
+  pr.pending_bytes.clear();
+}
+}  // namespace fmx
+
+// ============================================================================ pose algebra
+namespace {
+struct Pose {
+  double m[12];  // row-major [R | t]
+};
+Pose identity() {
+  Pose p{};
+  p.m[0] = p.m[5] = p.m[10] = 1.0;
+  return p;
+}
+Pose compose(const Pose& a, const Pose& b) {  // gtsam Pose3::operator*
+  Pose c;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j)
+      c.m[4 * i + j] = (a.m[4 * i] * b.m[j] + a.m[4 * i + 1] * b.m[4 + j]) + a.m[4 * i + 2] * b.m[8 + j];
+    c.m[4 * i + 3] = ((a.m[4 * i] * b.m[3] + a.m[4 * i + 1] * b.m[7]) + a.m[4 * i + 2] * b.m[11]) + a.m[4 * i + 3];
+  }
+  return c;
+}
+Pose inverse(const Pose& a) {  // (R^T, R^T(-t))
+  Pose c;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) c.m[4 * i + j] = a.m[4 * j + i];
+  const double nt[3] = {-a.m[3], -a.m[7], -a.m[11]};
+  for (int i = 0; i < 3; ++i) c.m[4 * i + 3] = (c.m[4 * i] * nt[0] + c.m[4 * i + 1] * nt[1]) + c.m[4 * i + 2] * nt[2];
+  return c;
+}
+void cross(const double a[3], const double b[3], double o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+Pose expmap(const double xi[6]) {  // gtsam Pose3::Expmap, tangent [w; v]
+  const double* w = xi;
+  const double* v = xi + 3;
+  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  double A, B, a, b;
+  if (th2 <= DBL_EPSILON) {
+    A = 1.0;
+    B = 0.5;
+    a = 0.5;
+    b = 1.0 / 6.0;
+  } else {
+    const double th = std::sqrt(th2);
+    A = std::sin(th) / th;
+    B = (1.0 - std::cos(th)) / th2;
+    a = B;
+    b = (th - std::sin(th)) / (th2 * th);
+  }
+  const double W[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+  Pose T;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      const double w2 = W[i][0] * W[0][j] + W[i][1] * W[1][j] + W[i][2] * W[2][j];
+      T.m[4 * i + j] = (i == j ? 1.0 : 0.0) + A * W[i][j] + B * w2;
+    }
+  double wxv[3], wxwxv[3];
+  cross(w, v, wxv);
+  cross(w, wxv, wxwxv);
+  for (int i = 0; i < 3; ++i) T.m[4 * i + 3] = v[i] + a * wxv[i] + b * wxwxv[i];
+  return T;
+}
+void logmap(const Pose& T, double xi[6]) {  // gtsam Pose3::Logmap
+  const double* m = T.m;
+  const double tr = m[0] + m[5] + m[10];
+  double w[3];
+  if (tr + 1.0 < 1e-10) {
+    if (std::abs(m[10] + 1.0) > 1e-10) {
+      const double s = M_PI / std::sqrt(2.0 + 2.0 * m[10]);
+      w[0] = s * m[2]; w[1] = s * m[6]; w[2] = s * (1.0 + m[10]);
+    } else if (std::abs(m[5] + 1.0) > 1e-10) {
+      const double s = M_PI / std::sqrt(2.0 + 2.0 * m[5]);
+      w[0] = s * m[1]; w[1] = s * (1.0 + m[5]); w[2] = s * m[9];
+    } else {
+      const double s = M_PI / std::sqrt(2.0 + 2.0 * m[0]);
+      w[0] = s * (1.0 + m[0]); w[1] = s * m[4]; w[2] = s * m[8];
+    }
+  } else {
+    const double tr_3 = tr - 3.0;
+    double mag;
+    if (tr_3 < -1e-7) {
+      const double th = std::acos((tr - 1.0) / 2.0);
+      mag = th / (2.0 * std::sin(th));
+    } else {
+      mag = 0.5 - tr_3 * tr_3 / 12.0;
+    }
+    w[0] = mag * (m[9] - m[6]);
+    w[1] = mag * (m[2] - m[8]);
+    w[2] = mag * (m[4] - m[1]);
+  }
+  const double t = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  xi[0] = w[0]; xi[1] = w[1]; xi[2] = w[2];
+  const double tt[3] = {m[3], m[7], m[11]};
+  if (t < 1e-10) {
+    xi[3] = tt[0]; xi[4] = tt[1]; xi[5] = tt[2];
+    return;
+  }
+  const double wn[3] = {w[0] / t, w[1] / t, w[2] / t};
+  double WT[3], WWT[3];
+  cross(wn, tt, WT);
+  cross(wn, WT, WWT);
+  const double Tan = std::tan(0.5 * t);
+  for (int i = 0; i < 3; ++i) xi[3 + i] = tt[i] - (0.5 * t) * WT[i] + (1 - t / (2. * Tan)) * WWT[i];
+}
+void normalize_rot(Pose& P) {  // gtsam Rot3::normalized (constraints.cpp:93-95)
+  double* R = P.m;
+  const double det = R[0] * (R[5] * R[10] - R[6] * R[9]) - R[1] * (R[4] * R[10] - R[6] * R[8]) +
+                     R[2] * (R[4] * R[9] - R[5] * R[8]);
+  if (std::fabs(det - 1) < 1e-12) return;
+  const double x[3] = {R[0], R[1], R[2]}, y[3] = {R[4], R[5], R[6]};
+  const double err = x[0] * y[0] + x[1] * y[1] + x[2] * y[2];
+  double xo[3], yo[3], zo[3];
+  for (int i = 0; i < 3; ++i) {
+    xo[i] = x[i] - (err / 2) * y[i];
+    yo[i] = y[i] - (err / 2) * x[i];
+  }
+  cross(xo, yo, zo);
+  const double sx = 0.5 * (3 - (xo[0] * xo[0] + xo[1] * xo[1] + xo[2] * xo[2]));
+  const double sy = 0.5 * (3 - (yo[0] * yo[0] + yo[1] * yo[1] + yo[2] * yo[2]));
+  const double sz = 0.5 * (3 - (zo[0] * zo[0] + zo[1] * zo[1] + zo[2] * zo[2]));
+  for (int i = 0; i < 3; ++i) {
+    R[i] = sx * xo[i];
+    R[4 + i] = sy * yo[i];
+    R[8 + i] = sz * zo[i];
+  }
+}
+
+bool chol_solve6(const double H[6][6], const double g[6], double x[6]) {
+  double L[6][6] = {};
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = H[i][j];
+      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+      if (i == j) {
+        if (s <= 0) return false;
+        L[i][i] = std::sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  double y[6];
+  for (int i = 0; i < 6; ++i) {
+    double s = g[i];
+    for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+  return true;
+}
+
+// KeyScanner::step (form/mapping/keyscanner.cpp:29-91)
+struct KScan {
+  uint64_t idx;
+  size_t unused = 0, size = 0;
+};
+struct KeyScanner {
+  const fmx_params* P = nullptr;
+  std::deque<KScan> recent, key;
+  uint64_t oldest_rf() const { return recent.empty() ? 0 : recent.front().idx; }
+  std::vector<uint64_t> step(uint64_t idx, size_t size, const std::function<size_t(uint64_t)>& conn) {
+    if (idx == 0) key.push_back({idx, 0, size});
+    else recent.push_back({idx, 0, size});
+    std::vector<uint64_t> marg;
+    if (recent.size() > P->max_num_recent_scans) {
+      KScan rf = recent.front();
+      recent.pop_front();
+      const double ratio = (double)conn(rf.idx) / (double)(rf.size * recent.size());
+      if (ratio > P->keyscan_match_ratio) key.push_back(rf);
+      else marg.push_back(rf.idx);
+    }
+    std::set<uint64_t> fin;
+    for (auto& kf : key) {
+      if (conn(kf.idx) > 0) kf.unused = 0;
+      else ++kf.unused;
+      if ((int64_t)kf.unused > P->max_steps_unused_keyscan) {
+        marg.push_back(kf.idx);
+        fin.insert(kf.idx);
+      }
+    }
+    key.erase(std::remove_if(key.begin(), key.end(), [&](const KScan& f) { return fin.count(f.idx) > 0; }),
+              key.end());
+    if (P->max_num_keyscans > 0 && (int64_t)key.size() > P->max_num_keyscans) {
+      marg.push_back(key.front().idx);
+      key.pop_front();
+    }
+    return marg;
+  }
+};
+
+template <class F>
+fmx_status guard(fmx_ctx* c, F&& f) {
+  if (!c) return FMX_E_INVAL;
+  try {
+    FMX_HIP(hipSetDevice(c->device));
+    f();
+    c->err.clear();
+    return FMX_OK;
+  } catch (const StatusError& e) {
+    c->err = e.what();
+    return e.st;
+  } catch (const HipError& e) {
+    c->err = e.what();
+    return FMX_E_HIP;
+  } catch (const std::bad_alloc&) {
+    c->err = "host allocation failed";
+    return FMX_E_OOM;
+  } catch (const std::exception& e) {
+    c->err = e.what();
+    return FMX_E_INVAL;
+  }
+}
+
+void compact_pool(fmx_ctx* c, int t) {
+  Pool& pool = c->pool[t];
+  DBuf<float4> npos, nnrm;
+  npos.ensure(pool.pos.cap);
+  if (t == 0) nnrm.ensure(pool.nrm.cap);
+  std::vector<std::pair<uint64_t, uint64_t>> order;  // (offset, scan)
+  for (auto& [s, r] : pool.ranges) order.push_back({r.first, s});
+  std::sort(order.begin(), order.end());
+  uint64_t o = 0;
+  for (auto& [off, s] : order) {
+    auto& r = pool.ranges[s];
+    if (r.second) {
+      FMX_HIP(hipMemcpyAsync(npos.p + o, pool.pos.p + off, r.second * sizeof(float4), hipMemcpyDeviceToDevice,
+                             c->stream));
+      if (t == 0)
+        FMX_HIP(hipMemcpyAsync(nnrm.p + o, pool.nrm.p + off, r.second * sizeof(float4), hipMemcpyDeviceToDevice,
+                               c->stream));
+    }
+    r.first = o;
+    o += r.second;
+  }
+  FMX_HIP(hipStreamSynchronize(c->stream));
+  pool.pos.release();
+  pool.pos = npos;
+  if (t == 0) {
+    pool.nrm.release();
+    pool.nrm = nnrm;
+  }
+  pool.used = o;
+}
+
+void ensure_pool_room(fmx_ctx* c, int t, uint64_t need) {
+  Pool& pool = c->pool[t];
+  if (pool.used + need <= pool.pos.cap) return;
+  compact_pool(c, t);
+  if (pool.used + need > pool.pos.cap)
+    throw StatusError(FMX_E_OOM, "keypoint pool capacity exceeded (raise keypoint_pool_capacity)");
+}
+
+// upload host features into the pool under `scan`
+void pool_add(fmx_ctx* c, int t, uint64_t scan, const float* f, uint32_t n) {
+  if (n == 0) return;
+  ensure_pool_room(c, t, n);
+  Pool& pool = c->pool[t];
+  std::vector<float4> pos(n), nrm(t == 0 ? n : 0);
+  const int st = t == 0 ? 6 : 3;
+  for (uint32_t i = 0; i < n; ++i) {
+    pos[i] = make_float4(f[st * i], f[st * i + 1], f[st * i + 2], 0.f);
+    if (t == 0) nrm[i] = make_float4(f[st * i + 3], f[st * i + 4], f[st * i + 5], 0.f);
+  }
+  auto& rg = pool.ranges[scan];
+  if (rg.second == 0) rg.first = pool.used;
+  else if (rg.first + rg.second != pool.used) throw StatusError(FMX_E_STATE, "scan keypoints must be added contiguously");
+  FMX_HIP(hipMemcpy(pool.pos.p + pool.used, pos.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  if (t == 0) FMX_HIP(hipMemcpy(pool.nrm.p + pool.used, nrm.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  rg.second += n;
+  pool.used += n;
+}
+
+void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const float* pt, uint32_t npt) {
+  std::vector<float4> a(npl + 1), b(npl + 1), d(npt + 1);
+  for (uint32_t i = 0; i < npl; ++i) {
+    a[i] = make_float4(pl[6 * i], pl[6 * i + 1], pl[6 * i + 2], 0.f);
+    b[i] = make_float4(pl[6 * i + 3], pl[6 * i + 4], pl[6 * i + 5], 0.f);
+  }
+  for (uint32_t i = 0; i < npt; ++i) d[i] = make_float4(pt[3 * i], pt[3 * i + 1], pt[3 * i + 2], 0.f);
+  c->q_pl_pos.ensure(npl + 1);
+  c->q_pl_nrm.ensure(npl + 1);
+  c->q_pl_idx.ensure(npl + 1);
+  c->q_pt_pos.ensure(npt + 1);
+  c->q_pt_idx.ensure(npt + 1);
+  FMX_HIP(hipMemcpy(c->q_pl_pos.p, a.data(), (npl + 1) * sizeof(float4), hipMemcpyHostToDevice));
+  FMX_HIP(hipMemcpy(c->q_pl_nrm.p, b.data(), (npl + 1) * sizeof(float4), hipMemcpyHostToDevice));
+  FMX_HIP(hipMemcpy(c->q_pt_pos.p, d.data(), (npt + 1) * sizeof(float4), hipMemcpyHostToDevice));
+  FMX_HIP(hipMemsetAsync(c->q_pl_idx.p, 0xFF, (npl + 1) * sizeof(uint32_t), c->stream));
+  FMX_HIP(hipMemsetAsync(c->q_pt_idx.p, 0xFF, (npt + 1) * sizeof(uint32_t), c->stream));
+  c->n_qpl = npl;
+  c->n_qpt = npt;
+  c->n_sel = npl;
+  c->q_scan = scan;
+  c->have_queries = true;
+  c->have_match = false;
+}
+
+void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out) {
+  const auto& E = c->P.extraction;
+  const size_t R = (size_t)E.num_rows, C = (size_t)E.num_columns;
+  if (!xyzw && n) throw StatusError(FMX_E_INVAL, "null scan");
+  if (n != R * C)  // extraction.tpp:141-145
+    throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " + std::to_string(R * C) +
+                                      " != " + std::to_string(n));
+  if (C > 4096 || C < 2 * E.neighbor_points + 2 || E.num_sectors == 0 || E.num_sectors > C)
+    throw StatusError(FMX_E_INVAL, "unsupported scan geometry (columns must be <= 4096)");
+  const float4* d;
+  if (on_dev) {
+    d = reinterpret_cast<const float4*>(xyzw);
+  } else {
+    c->scan.ensure(n);
+    FMX_HIP(hipMemcpyAsync(c->scan.p, xyzw, n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    d = c->scan.p;
+  }
+  run_extract(c, d, (int)R, (int)C, out);
+  c->q_scan = scan;
+  c->have_queries = true;
+  c->have_match = false;
+}
+
+}  // namespace
+
+// ============================================================================ estimator
+struct fmx_ctx::Est {
+  bool init = false;
+  uint64_t scan = 0;
+  std::map<uint64_t, Pose> values;
+  std::map<uint64_t, std::map<uint64_t, std::pair<uint32_t, uint32_t>>> cons;
+  KeyScanner ks;
+  std::vector<double> poses_i, poses_j, G, err;
+};
+
+namespace {
+
+// ConstraintManager::predict_next (constraints.cpp:71-101)
+Pose predict_next(const fmx_ctx::Est& e) {
+  if (!e.init) return identity();
+  const uint64_t s = e.scan + 1;
+  const bool pe = s > 0 && e.values.count(s - 1), ppe = s > 1 && e.values.count(s - 2);
+  if (pe && ppe) {
+    const Pose& prev = e.values.at(s - 1);
+    const Pose& pp = e.values.at(s - 2);
+    Pose pr = compose(prev, compose(inverse(pp), prev));
+    normalize_rot(pr);
+    return pr;
+  }
+  if (pe) return e.values.at(s - 1);
+  return identity();
+}
+
+// Single-pose LM on X(j), map poses fixed (disable_smoothing, constraints.cpp:103-111,
+// 235-250) with GTSAM LevenbergMarquardtOptimizer defaults; the linearization and
+// error evaluations run on the device (fmx stage 3, 7x7 layout).
+struct DeviceLM {
+  fmx_ctx* c;
+  fmx_ctx::Est& e;
+  double sigma;
+  double lambda = 1e-5;
+  int linearizations = 0;
+  void fill(const Pose& Tj) {
+    const uint32_t K = c->K;
+    e.poses_i.resize(12 * (size_t)K);
+    e.poses_j.resize(12 * (size_t)K);
+    for (uint32_t k = 0; k < K; ++k) {
+      std::memcpy(&e.poses_i[12 * k], e.values.at(c->map_scans[k]).m, 12 * sizeof(double));
+      std::memcpy(&e.poses_j[12 * k], Tj.m, 12 * sizeof(double));
+    }
+  }
+  double error_at(const Pose& Tj) {
+    if (c->K == 0) return 0.0;
+    fill(Tj);
+    e.err.resize(c->K);
+    run_linearize(c, e.poses_i.data(), e.poses_j.data(), sigma, 2, nullptr, e.err.data());
+    double s = 0;
+    for (uint32_t k = 0; k < c->K; ++k) s += e.err[k];
+    return s;
+  }
+  void iterate(Pose& T, double& err) {
+    const uint32_t K = c->K;
+    fill(T);
+    e.G.resize(28 * (size_t)K);
+    e.err.resize(K);
+    run_linearize(c, e.poses_i.data(), e.poses_j.data(), sigma, 1, e.G.data(), e.err.data());
+    ++linearizations;
+    double Hs[6][6] = {}, g[6] = {}, cc = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+      const double* Gk = &e.G[28 * (size_t)k];
+      double full[7][7];
+      int o = 0;
+      for (int i = 0; i < 7; ++i)
+        for (int j = i; j < 7; ++j) full[i][j] = full[j][i] = Gk[o++];
+      for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < 6; ++j) Hs[i][j] += full[i][j];
+        g[i] += full[i][6];
+      }
+      cc += full[6][6];
+    }
+    const double oldLin = 0.5 * cc;
+    for (;;) {  // LevenbergMarquardtOptimizer::tryLambda
+      double Hd[6][6];
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) Hd[i][j] = Hs[i][j] + (i == j ? lambda : 0.0);
+      double dx[6];
+      const bool ok = chol_solve6(Hd, g, dx);
+      bool success = false, stop = false;
+      Pose Tn = T;
+      double nerr = err;
+      if (ok) {
+        double dHd = 0, dg = 0;
+        for (int i = 0; i < 6; ++i) {
+          double h = 0;
+          for (int j = 0; j < 6; ++j) h += Hs[i][j] * dx[j];
+          dHd += dx[i] * h;
+          dg += dx[i] * g[i];
+        }
+        const double newLin = 0.5 * (dHd - 2 * dg + cc);
+        const double linChange = oldLin - newLin;
+        if (linChange >= 0) {
+          Tn = compose(T, expmap(dx));
+          nerr = error_at(Tn);
+          const double costChange = err - nerr;
+          if (linChange > DBL_EPSILON * oldLin) success = (costChange / linChange) > 1e-3;
+          else success = true;
+          if (std::abs(costChange) < 1e-5 * err) stop = true;
+        }
+      }
+      if (success) {
+        lambda = std::max(0.0, lambda / 10.0);
+        T = Tn;
+        err = nerr;
+        return;
+      } else if (!stop) {
+        lambda *= 10.0;
+        if (lambda >= 1e5) return;
+      } else {
+        return;
+      }
+    }
+  }
+  Pose optimize(const Pose& T0, int* iters) {  // NonlinearOptimizer::defaultOptimize
+    Pose T = T0;
+    double err = error_at(T);
+    int it = 0;
+    if (err <= 0.0) {
+      *iters = 0;
+      return T;
+    }
+    double cur, newErr = err;
+    bool conv;
+    do {
+      cur = newErr;
+      iterate(T, err);
+      ++it;
+      newErr = err;
+      if (newErr <= 0.0) conv = true;
+      else {
+        const double absDec = cur - newErr, relDec = absDec / cur;
+        conv = (relDec <= 1e-5) || (absDec <= 1e-5);
+      }
+    } while (it < 100 && !conv && std::isfinite(cur));
+    *iters = it;
+    return T;
+  }
+};
+
+size_t num_recent_connections(const fmx_ctx::Est& e, uint64_t s, uint64_t oldest) {  // constraints.cpp:319-336
+  size_t cnt = 0;
+  for (auto& [j, m] : e.cons) {
+    if (j < oldest) continue;
+    auto it = m.find(s);
+    if (it != m.end()) cnt += it->second.first + it->second.second;
+  }
+  return cnt;
+}
+
+void remove_scan(fmx_ctx* c, uint64_t s) {  // KeypointMap::remove (map.tpp:112-126)
+  for (int t = 0; t < 2; ++t) c->pool[t].ranges.erase(s);
+}
+
+void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
+  if (!c->est) {
+    c->est = new fmx_ctx::Est();
+    c->est->ks.P = &c->P;
+  }
+  fmx_ctx::Est& e = *c->est;
+  const fmx_params& P = c->P;
+  // step(prediction) (constraints.cpp:206-223)
+  const Pose pred = predict_next(e);
+  const size_t RC = (size_t)P.extraction.num_rows * (size_t)P.extraction.num_columns;
+  if (n != RC)
+    throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " + std::to_string(RC) +
+                                      " != " + std::to_string(n));
+  if (e.init) ++e.scan;
+  e.init = true;
+  const uint64_t j = e.scan;
+  e.values[j] = pred;
+  auto& cj = e.cons[j];
+  for (auto& [i, T] : e.values)
+    if (i != j) cj[i] = {0, 0};
+  // extract (form.cpp:51)
+  fmx_feature_counts fc{};
+  do_extract(c, xyzw, n, j, on_dev, &fc);
+  // to_voxel_map x2, voxel width = max_dist_matching (form.cpp:61-65)
+  std::set<uint64_t> sset;
+  for (int t = 0; t < 2; ++t)
+    for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
+  std::vector<uint64_t> scans(sset.begin(), sset.end());
+  std::vector<double> poses(12 * scans.size());
+  for (size_t k = 0; k < scans.size(); ++k) std::memcpy(&poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double));
+  run_map_build(c, scans, poses.data(), P.max_dist_matching);
+  // ICP loop (form.cpp:67-89)
+  DeviceLM lm{c, e, P.planar_constraint_sigma};
+  uint64_t icp = 0, lm_it = 0;
+  for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
+    ++icp;
+    const Pose before = e.values.at(j);
+    run_match(c, before.m, P.max_dist_matching, P.min_dist_map);
+    lm.lambda = 1e-5;
+    int li = 0;
+    const Pose after = lm.optimize(before, &li);
+    lm_it += li;
+    double xi[6];
+    logmap(compose(inverse(before), after), xi);
+    double dn = 0;
+    for (double x : xi) dn += x * x;
+    if (std::sqrt(dn) < P.new_pose_threshold) break;
+    e.values[j] = after;  // update_current_pose
+  }
+  {  // optimize(false) + update_values (form.cpp:92-93)
+    lm.lambda = 1e-5;
+    int li = 0;
+    e.values[j] = lm.optimize(e.values.at(j), &li);
+    lm_it += li;
+  }
+  uint64_t mpl = 0, mpt = 0;
+  for (uint32_t k = 0; k < c->K; ++k) {
+    cj[c->map_scans[k]] = {c->cnt_pl[k], c->cnt_pt[k]};
+    mpl += c->cnt_pl[k];
+    mpt += c->cnt_pt[k];
+  }
+  // insert_matches (form.cpp:98-100) from the last match
+  uint32_t nin[2] = {0, 0};
+  ensure_pool_room(c, 0, c->n_qpl);
+  ensure_pool_room(c, 1, c->n_qpt);
+  run_insert(c, j, nin);
+  // keyscan selection + marginalization (form.cpp:104-111)
+  auto marg = e.ks.step(j, fc.planar + fc.point, [&](uint64_t i) {
+    return num_recent_connections(e, i, e.ks.oldest_rf());
+  });
+  for (uint64_t m : marg) {
+    e.values.erase(m);
+    e.cons.erase(m);
+    for (auto& [jj, mm] : e.cons) mm.erase(m);
+    remove_scan(c, m);
+  }
+  c->stats[0] = icp;
+  c->stats[1] = lm_it;
+  c->stats[2] = mpl;
+  c->stats[3] = mpt;
+  c->stats[4] = c->map[0].n;
+  c->stats[5] = c->map[1].n;
+  c->stats[6] = lm.linearizations;
+  c->stats[7] = scans.size();
+  if (out) *out = fc;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int fmx_abi_version(void) { return FMX_ABI_VERSION; }
+
+void fmx_default_params(fmx_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  auto& e = p->extraction;  // extraction.hpp:59-88
+  e.neighbor_points = 5;
+  e.num_sectors = 6;
+  e.planar_threshold = 1.0;
+  e.planar_feats_per_sector = 50;
+  e.point_feats_per_sector = 3;
+  e.radius = 1.0;
+  e.min_points = 5;
+  e.min_norm_squared = 1.0;
+  e.max_norm_squared = 100.0 * 100.0;
+  e.num_columns = 1024;
+  e.num_rows = 64;
+  p->max_dist_matching = 0.8;  // matcher.hpp:32-41
+  p->new_pose_threshold = 1e-4;
+  p->max_num_rematches = 30;
+  p->planar_constraint_sigma = 0.1;  // constraints.hpp:60
+  p->disable_smoothing = 1;
+  p->max_num_keyscans = 50;  // keyscanner.hpp:55-64
+  p->max_steps_unused_keyscan = 10;
+  p->max_num_recent_scans = 10;
+  p->keyscan_match_ratio = 0.1;
+  p->min_dist_map = 0.1;  // map.hpp:97-100
+  p->keypoint_pool_capacity = 4u << 20;
+  p->max_pairs = 1024;
+}
+
+fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
+  if (!p || !out) return FMX_E_INVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return FMX_E_HIP;
+  if (device < 0 || device >= ndev) return FMX_E_INVAL;
+  fmx_ctx* c = new (std::nothrow) fmx_ctx();
+  if (!c) return FMX_E_OOM;
+  c->P = *p;
+  c->device = device;
+  fmx_status st = guard(c, [&] {
+    FMX_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const uint64_t cap = p->keypoint_pool_capacity ? p->keypoint_pool_capacity : (4u << 20);
+    c->pool[0].planar = true;
+    c->pool[1].planar = false;
+    c->pool[0].pos.ensure(cap);
+    c->pool[0].nrm.ensure(cap);
+    c->pool[1].pos.ensure(cap);
+  });
+  if (st != FMX_OK) {
+    fmx_destroy(c);
+    return st;
+  }
+  *out = c;
+  return FMX_OK;
+}
+
+void fmx_destroy(fmx_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& e : c->prof.free_events) (void)hipEventDestroy(e);
+  for (auto& pe : c->prof.pending) {
+    (void)hipEventDestroy(pe.second.first);
+    (void)hipEventDestroy(pe.second.second);
+  }
+  delete c->est;
+  // DBuf/HBuf members do not free in their destructors: release explicitly.
+  c->scan.release(); c->planar_mask.release(); c->sel_slots.release(); c->pt_slots.release();
+  c->row_counts.release(); c->row_ok.release(); c->row_off.release(); c->closest.release();
+  c->nrm_slots.release(); c->scan_scratch.release(); c->dev_u32.release(); c->h_u32.release();
+  c->q_pl_pos.release(); c->q_pl_nrm.release(); c->q_pt_pos.release(); c->q_pl_idx.release(); c->q_pt_idx.release();
+  for (int t = 0; t < 2; ++t) {
+    c->pool[t].pos.release(); c->pool[t].nrm.release();
+    auto& M = c->map[t];
+    M.table.release(); M.cursor.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
+    M.rseg.release(); M.pos.release(); M.nrm.release(); M.seg.release(); M.rid.release();
+    c->segs[t].release(); c->h_segs[t].release();
+  }
+  c->h_mapposes.release(); c->map_poses.release(); c->map_inv_poses.release(); c->map_err.release();
+  c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();
+  c->hist.release(); c->hist_off.release(); c->c_pl.release(); c->c_pt.release(); c->pair_counts.release();
+  c->chunk_range.release(); c->chunks.release(); c->n_chunks.release(); c->poses_ij.release();
+  c->partials.release(); c->G.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
+  c->h_corr.release(); c->h_meta.release(); c->h_counts.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* fmx_last_error(const fmx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+fmx_status fmx_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out) {
+  return guard(c, [&] { do_extract(c, xyzw, n, scan, on_dev, out); });
+}
+
+fmx_status fmx_extract_download(fmx_ctx* c, float* planar, uint32_t* planar_index, float* point,
+                                uint32_t* point_index, uint8_t* planar_mask) {
+  return guard(c, [&] {
+    if (!c->have_queries) throw StatusError(FMX_E_STATE, "no extraction");
+    FMX_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t npl = c->n_qpl, npt = c->n_qpt;
+    if (planar) {
+      std::vector<float4> a(npl), b(npl);
+      FMX_HIP(hipMemcpy(a.data(), c->q_pl_pos.p, npl * sizeof(float4), hipMemcpyDeviceToHost));
+      FMX_HIP(hipMemcpy(b.data(), c->q_pl_nrm.p, npl * sizeof(float4), hipMemcpyDeviceToHost));
+      for (uint32_t i = 0; i < npl; ++i) {
+        planar[6 * i] = a[i].x; planar[6 * i + 1] = a[i].y; planar[6 * i + 2] = a[i].z;
+        planar[6 * i + 3] = b[i].x; planar[6 * i + 4] = b[i].y; planar[6 * i + 5] = b[i].z;
+      }
+    }
+    if (planar_index) FMX_HIP(hipMemcpy(planar_index, c->q_pl_idx.p, npl * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (point) {
+      std::vector<float4> a(npt);
+      FMX_HIP(hipMemcpy(a.data(), c->q_pt_pos.p, npt * sizeof(float4), hipMemcpyDeviceToHost));
+      for (uint32_t i = 0; i < npt; ++i) {
+        point[3 * i] = a[i].x; point[3 * i + 1] = a[i].y; point[3 * i + 2] = a[i].z;
+      }
+    }
+    if (point_index) FMX_HIP(hipMemcpy(point_index, c->q_pt_idx.p, npt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (planar_mask) {
+      if (!c->rows) throw StatusError(FMX_E_STATE, "no device extraction");
+      FMX_HIP(hipMemcpy(planar_mask, c->planar_mask.p, (size_t)c->rows * c->cols, hipMemcpyDeviceToHost));
+    }
+  });
+}
+
+fmx_status fmx_set_queries(fmx_ctx* c, uint64_t scan, const float* planar, uint32_t npl, const float* point,
+                           uint32_t npt) {
+  return guard(c, [&] {
+    if ((npl && !planar) || (npt && !point)) throw StatusError(FMX_E_INVAL, "null features");
+    set_queries(c, scan, planar, npl, point, npt);
+  });
+}
+
+fmx_status fmx_keypoints_add(fmx_ctx* c, uint64_t scan, const float* planar, uint32_t npl, const float* point,
+                             uint32_t npt) {
+  return guard(c, [&] {
+    if ((npl && !planar) || (npt && !point)) throw StatusError(FMX_E_INVAL, "null features");
+    pool_add(c, 0, scan, planar, npl);
+    pool_add(c, 1, scan, point, npt);
+  });
+}
+
+fmx_status fmx_keypoints_remove(fmx_ctx* c, uint64_t scan) {
+  return guard(c, [&] { remove_scan(c, scan); });
+}
+
+fmx_status fmx_map_build(fmx_ctx* c, const uint64_t* scans, const double* poses, uint32_t n, double w) {
+  return guard(c, [&] {
+    if (n && (!scans || !poses)) throw StatusError(FMX_E_INVAL, "null scans/poses");
+    if (!(w > 0)) throw StatusError(FMX_E_INVAL, "voxel width must be > 0");
+    std::vector<uint64_t> s(scans, scans + n);
+    run_map_build(c, s, poses, w);
+  });
+}
+
+fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint32_t* cpl, uint32_t* cpt) {
+  return guard(c, [&] {
+    if (!c->have_map) throw StatusError(FMX_E_STATE, "fmx_map_build first");
+    if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
+    if (!(max_dist > 0)) throw StatusError(FMX_E_INVAL, "max_dist must be > 0");
+    run_match(c, pose_j, max_dist, c->P.min_dist_map);
+    c->h_u32.ensure(8);
+    FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->map_err.p, 4, hipMemcpyDeviceToHost, c->stream));
+    FMX_HIP(hipStreamSynchronize(c->stream));
+    if (c->h_u32.p[0]) throw StatusError(FMX_E_RANGE, "voxel coordinate outside the packed-key range");
+    if (cpl) std::memcpy(cpl, c->cnt_pl.data(), c->K * sizeof(uint32_t));
+    if (cpt) std::memcpy(cpt, c->cnt_pt.data(), c->K * sizeof(uint32_t));
+  });
+}
+
+fmx_status fmx_match_download(fmx_ctx* c, int32_t* pair, double* d2, double* pi, double* ni) {
+  return guard(c, [&] {
+    if (!c->have_match) throw StatusError(FMX_E_STATE, "no match results");
+    FMX_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t nq = c->n_qpl + c->n_qpt;
+    if (pair) FMX_HIP(hipMemcpy(pair, c->m_pair.p, nq * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (d2) FMX_HIP(hipMemcpy(d2, c->m_d2.p, nq * sizeof(double), hipMemcpyDeviceToHost));
+    if (pi) {
+      std::vector<double4> a(nq);
+      FMX_HIP(hipMemcpy(a.data(), c->m_pi.p, nq * sizeof(double4), hipMemcpyDeviceToHost));
+      for (uint32_t i = 0; i < nq; ++i) {
+        pi[3 * i] = a[i].x; pi[3 * i + 1] = a[i].y; pi[3 * i + 2] = a[i].z;
+      }
+    }
+    if (ni) {
+      std::vector<double4> a(c->n_qpl);
+      FMX_HIP(hipMemcpy(a.data(), c->m_ni.p, c->n_qpl * sizeof(double4), hipMemcpyDeviceToHost));
+      for (uint32_t i = 0; i < c->n_qpl; ++i) {
+        ni[3 * i] = a[i].x; ni[3 * i + 1] = a[i].y; ni[3 * i + 2] = a[i].z;
+      }
+    }
+  });
+}
+
+fmx_status fmx_map_insert(fmx_ctx* c, double min_dist_map, uint32_t* n_inserted) {
+  return guard(c, [&] {
+    if (!c->have_match) throw StatusError(FMX_E_STATE, "no match results");
+    if (min_dist_map != c->P.min_dist_map)
+      throw StatusError(FMX_E_INVAL, "min_dist_map must equal the context's (fixed at match time)");
+    ensure_pool_room(c, 0, c->n_qpl);
+    ensure_pool_room(c, 1, c->n_qpt);
+    uint32_t n[2];
+    run_insert(c, c->q_scan, n);
+    if (n_inserted) {
+      n_inserted[0] = n[0];
+      n_inserted[1] = n[1];
+    }
+  });
+}
+
+fmx_status fmx_corr_set(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
+                        const double* ppj, const uint32_t* nt, const double* tpi, const double* tpj) {
+  return guard(c, [&] {
+    if (K && (!np || !nt)) throw StatusError(FMX_E_INVAL, "null counts");
+    upload_corr(c, K, np, ppi, pni, ppj, nt, tpi, tpj);
+  });
+}
+
+fmx_status fmx_linearize(fmx_ctx* c, const double* pi, const double* pj, double sigma, int single, double* G,
+                         double* err) {
+  return guard(c, [&] {
+    if (!(sigma > 0)) throw StatusError(FMX_E_INVAL, "sigma must be > 0");
+    if (c->K && (!pi || !pj)) throw StatusError(FMX_E_INVAL, "null poses");
+    run_linearize(c, pi, pj, sigma, single ? 1 : 0, G, err);
+  });
+}
+
+fmx_status fmx_error(fmx_ctx* c, const double* pi, const double* pj, double sigma, double* err) {
+  return guard(c, [&] {
+    if (!(sigma > 0)) throw StatusError(FMX_E_INVAL, "sigma must be > 0");
+    if (c->K && (!pi || !pj)) throw StatusError(FMX_E_INVAL, "null poses");
+    run_linearize(c, pi, pj, sigma, 2, nullptr, err);
+  });
+}
+
+fmx_status fmx_register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
+  return guard(c, [&] { register_scan(c, xyzw, n, on_dev, out); });
+}
+
+fmx_status fmx_current_pose(fmx_ctx* c, double pose[12]) {
+  return guard(c, [&] {
+    if (!c->est || !c->est->init) {
+      const Pose I = identity();
+      std::memcpy(pose, I.m, sizeof(I.m));
+      return;
+    }
+    std::memcpy(pose, c->est->values.at(c->est->scan).m, 12 * sizeof(double));
+  });
+}
+
+fmx_status fmx_last_stats(fmx_ctx* c, uint64_t stats[8]) {
+  return guard(c, [&] { std::memcpy(stats, c->stats, sizeof(c->stats)); });
+}
+
+fmx_status fmx_profile_enable(fmx_ctx* c, int on) {
+  return guard(c, [&] { c->prof.on = on != 0; });
+}
+fmx_status fmx_profile_reset(fmx_ctx* c) {
+  return guard(c, [&] {
+    prof_collect(c);
+    for (int i = 0; i < PROF_COUNT; ++i) {
+      c->prof.ms[i] = 0;
+      c->prof.launches[i] = 0;
+      c->prof.bytes[i] = 0;
+    }
+  });
+}
+int fmx_profile_count(void) { return PROF_COUNT; }
+const char* fmx_profile_name(int k) { return (k >= 0 && k < PROF_COUNT) ? kProfNames[k] : ""; }
+fmx_status fmx_profile_read(fmx_ctx* c, double* ms, uint64_t* launches, double* bytes, int n) {
+  return guard(c, [&] {
+    prof_collect(c);
+    for (int i = 0; i < std::min(n, (int)PROF_COUNT); ++i) {
+      if (ms) ms[i] = c->prof.ms[i];
+      if (launches) launches[i] = c->prof.launches[i];
+      if (bytes) bytes[i] = c->prof.bytes[i];
+    }
+  });
+}
+fmx_status fmx_sync(fmx_ctx* c) {
+  return guard(c, [&] { FMX_HIP(hipStreamSynchronize(c->stream)); });
+}
+
+}  // extern "C"

@@ -1,0 +1,189 @@
+// fmx_device.hpp — device helpers shared by the fmx HIP kernels (gfx950, wave64).
+//
+// Rounding contract: every .hip file is compiled with -ffp-contract=off, so the
+// float/double expressions below round exactly like the reference's SSE2 Eigen
+// code (CMakeLists.txt sets no -march; no FMA):
+//   PointXYZf::squaredNorm / (a - b).squaredNorm() on vec4 with zero pad
+//     -> (dx*dx + dz*dz) + dy*dy          (Packet4f predux: (a0+a2)+(a1+a3))
+//   Matrix3d * Vector3d -> ((R0 v0 + R1 v1) + R2 v2) per row.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fmx {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- poses
+struct Pose34 {  // row-major [R | t]
+  double m[12];
+};
+
+__device__ __forceinline__ void d_xform(const double* T, double x, double y, double z, double o[3]) {
+  o[0] = ((T[0] * x + T[1] * y) + T[2] * z) + T[3];
+  o[1] = ((T[4] * x + T[5] * y) + T[6] * z) + T[7];
+  o[2] = ((T[8] * x + T[9] * y) + T[10] * z) + T[11];
+}
+__device__ __forceinline__ void d_rot(const double* T, double x, double y, double z, double o[3]) {
+  o[0] = (T[0] * x + T[1] * y) + T[2] * z;
+  o[1] = (T[4] * x + T[5] * y) + T[6] * z;
+  o[2] = (T[8] * x + T[9] * y) + T[10] * z;
+}
+// R^T v
+__device__ __forceinline__ void d_rotT(const double* T, double x, double y, double z, double o[3]) {
+  o[0] = (T[0] * x + T[4] * y) + T[8] * z;
+  o[1] = (T[1] * x + T[5] * y) + T[9] * z;
+  o[2] = (T[2] * x + T[6] * y) + T[10] * z;
+}
+
+__device__ __forceinline__ float sqnorm4f(float x, float y, float z) { return (x * x + z * z) + y * y; }
+__device__ __forceinline__ float dist2f(float4 a, float4 b) {
+  const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+  return (dx * dx + dz * dz) + dy * dy;
+}
+
+// ---------------------------------------------------------------- wave ops
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T u = __shfl_up(v, o, 64);
+    if (l >= o) v += u;
+  }
+  return v;
+}
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------- device-wide scan
+// Exclusive scan of n uint32 values produced by in(i) into out(i, v); *total = sum.
+// Three launches (tile reduce, block-sum scan, tile scan): deterministic.
+constexpr int kScanThreads = 1024;
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+template <class In>
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(In in, size_t n, uint32_t* bsum) {
+  __shared__ uint32_t ws[kScanThreads / kWave];
+  const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j)
+    if (base + j < n) s += in(base + j);
+  s = wave_sum(s);
+  if (lane_id() == 0) ws[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kScanThreads / kWave; ++w) t += ws[w];
+    bsum[blockIdx.x] = t;
+  }
+}
+
+// single block: exclusive scan of nb block sums in place; *total = sum
+template <int Dummy = 0>
+__global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* bsum, uint32_t nb, uint32_t* total) {
+  __shared__ uint32_t ws[kScanThreads / kWave];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += kScanThreads) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nb ? bsum[i] : 0u;
+    const uint32_t incl = wave_incl_scan(v);
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (int k = 0; k < kScanThreads / kWave; ++k) {
+      if (k < w) woff += ws[k];
+      tot += ws[k];
+    }
+    const uint32_t c = carry;
+    if (i < nb) bsum[i] = c + woff + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry = c + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+template <class In, class Out>
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(In in, Out out, size_t n, const uint32_t* bsum) {
+  __shared__ uint32_t ws[kScanThreads / kWave];
+  const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    v[j] = base + j < n ? in(base + j) : 0u;
+    s += v[j];
+  }
+  const uint32_t incl = wave_incl_scan(s);
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == 63) ws[w] = incl;
+  __syncthreads();
+  uint32_t woff = 0;
+  for (int i = 0; i < w; ++i) woff += ws[i];
+  uint32_t run = bsum[blockIdx.x] + woff + incl - s;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    if (base + j < n) out(base + j, run);
+    run += v[j];
+  }
+}
+
+template <class In, class Out>
+inline void exclusive_scan(In in, Out out, size_t n, uint32_t* scratch /* >= nb */, uint32_t* total,
+                           hipStream_t st) {
+  const uint32_t nb = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  if (nb == 0) {
+    (void)hipMemsetAsync(total, 0, sizeof(uint32_t), st);
+    return;
+  }
+  k_scan_reduce<In><<<nb, kScanThreads, 0, st>>>(in, n, scratch);
+  k_scan_blocks<0><<<1, kScanThreads, 0, st>>>(scratch, nb, total);
+  k_scan_tiles<In, Out><<<nb, kScanThreads, 0, st>>>(in, out, n, scratch);
+}
+inline size_t scan_scratch_size(size_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+// ---------------------------------------------------------------- voxel keys
+// Packed voxel key: 21 bits per signed coordinate (offset 2^20), +1 so that 0 is
+// the empty slot marker.  Valid coordinates: |c| < 2^20 - 1.
+constexpr int kKeyBias = 1 << 20;
+__device__ __forceinline__ uint64_t pack_key(int x, int y, int z) {
+  return (((uint64_t)(uint32_t)(x + kKeyBias) << 42) | ((uint64_t)(uint32_t)(y + kKeyBias) << 21) |
+          (uint64_t)(uint32_t)(z + kKeyBias)) +
+         1ull;
+}
+__device__ __forceinline__ bool key_in_range(int x, int y, int z) {
+  const int L = kKeyBias - 2;
+  return x > -L && x < L && y > -L && y < L && z > -L && z < L;
+}
+__device__ __forceinline__ uint64_t mix64(uint64_t k) {  // splitmix64 finalizer
+  k ^= k >> 30;
+  k *= 0xbf58476d1ce4e5b9ull;
+  k ^= k >> 27;
+  k *= 0x94d049bb133111ebull;
+  k ^= k >> 31;
+  return k;
+}
+
+// Hash slot: {key, first record, record count}; 16 B, one probe = one 16-B load.
+struct alignas(16) Slot {
+  unsigned long long key;
+  uint32_t first;
+  uint32_t count;
+};
+
+}  // namespace fmx

@@ -1,0 +1,223 @@
+// fmx_internal.hpp — context layout and kernel-launcher interfaces of libfmx.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fmx/fmx.h"
+
+namespace fmx {
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct StatusError : std::runtime_error {
+  fmx_status st;
+  StatusError(fmx_status s, const std::string& m) : std::runtime_error(m), st(s) {}
+};
+
+#define FMX_HIP(call)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      throw ::fmx::HipError(std::string(#call) + ": " + hipGetErrorString(e_));              \
+  } while (0)
+
+// Growable device buffer (grows only; contents are not preserved across growth).
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    size_t c = n + n / 4 + 64;
+    FMX_HIP(hipMalloc(&p, c * sizeof(T)));
+    cap = c;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+template <class T>
+struct HBuf {  // pinned host staging
+  T* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) (void)hipHostFree(p);
+    size_t c = n + n / 4 + 64;
+    FMX_HIP(hipHostMalloc(&p, c * sizeof(T), hipHostMallocDefault));
+    cap = c;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// Profiled kernel classes (bench.py roofline).
+enum ProfId {
+  PROF_EXTRACT_ROWS = 0,
+  PROF_CLOSEST,
+  PROF_FIT,
+  PROF_COMPACT,
+  PROF_MAP_BUILD,
+  PROF_MATCH,
+  PROF_PAIR_SORT,
+  PROF_LINEARIZE,
+  PROF_ERROR,
+  PROF_INSERT,
+  PROF_COUNT
+};
+
+struct Prof {
+  bool on = false;
+  double ms[PROF_COUNT] = {};
+  uint64_t launches[PROF_COUNT] = {};
+  double bytes[PROF_COUNT] = {};
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<double> pending_bytes;
+  std::vector<hipEvent_t> free_events;
+};
+
+// Scoped kernel timer: HIP events on the context stream around one launch group.
+struct ProfScope {
+  Prof& pr;
+  int id;
+  double bytes;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(Prof& p, int i, double by, hipStream_t s);
+  ~ProfScope();
+};
+
+// Keypoint store of one feature type: device pool + per-scan ranges (host side).
+struct Pool {
+  DBuf<float4> pos, nrm;  // nrm unused for point features
+  bool planar = true;
+  uint64_t used = 0;
+  std::map<uint64_t, std::pair<uint64_t, uint32_t>> ranges;  // scan -> (offset, count)
+};
+
+// One built voxel map (VoxelMap<P>, map.hpp:66-94) in HBM.
+struct VoxMap {
+  DBuf<uint4> table;      // fmx::Slot[cap]
+  DBuf<uint32_t> cursor;  // scatter cursors [cap]
+  uint64_t cap = 0;       // power of two
+  DBuf<double4> tpos, tnrm;     // transformed records, build order
+  DBuf<uint32_t> rslot, rseg;   // per build-order record
+  DBuf<double4> pos, nrm;       // voxel-sorted
+  DBuf<uint32_t> seg, rid;      // voxel-sorted segment (pair) and build-order id
+  uint32_t n = 0;
+  uint32_t voxels = 0;
+};
+
+struct Seg {
+  uint32_t off;       // first build-order record
+  uint32_t n;         // records
+  uint32_t pool_off;  // offset in the pool
+  uint32_t pad;
+};
+
+struct Chunk {
+  uint32_t type;  // 0 plane rows, 1 point pairs
+  uint32_t pair;
+  uint32_t begin;
+  uint32_t end;
+};
+
+}  // namespace fmx
+
+struct fmx_ctx {
+  fmx_params P{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  fmx::Prof prof;
+
+  // ---- extraction scratch
+  fmx::DBuf<float4> scan;
+  fmx::DBuf<uint8_t> planar_mask;
+  fmx::DBuf<uint32_t> sel_slots, pt_slots, row_counts, row_ok, row_off;
+  fmx::DBuf<int2> closest;
+  fmx::DBuf<float4> nrm_slots;
+  fmx::DBuf<uint32_t> scan_scratch, dev_u32;  // dev_u32: small device scalars
+  fmx::HBuf<uint32_t> h_u32;
+  int rows = 0, cols = 0;
+
+  // ---- current query set (scan being registered)
+  uint64_t q_scan = 0;
+  uint32_t n_qpl = 0, n_qpt = 0, n_sel = 0;
+  fmx::DBuf<float4> q_pl_pos, q_pl_nrm, q_pt_pos;
+  fmx::DBuf<uint32_t> q_pl_idx, q_pt_idx;
+  bool have_queries = false;
+
+  // ---- window keypoint store + maps
+  fmx::Pool pool[2];
+  fmx::VoxMap map[2];
+  std::vector<uint64_t> map_scans;  // pair k -> scan id
+  fmx::DBuf<fmx::Seg> segs[2];
+  fmx::HBuf<fmx::Seg> h_segs[2];
+  fmx::HBuf<double> h_mapposes;
+  fmx::DBuf<double> map_poses, map_inv_poses;  // K x 12
+  double voxel_w = 0;
+  bool have_map = false;
+  fmx::DBuf<uint32_t> map_err;
+
+  // ---- match results (query-indexed; planar then point)
+  fmx::DBuf<int32_t> m_pair;
+  fmx::DBuf<double> m_d2;
+  fmx::DBuf<double4> m_pi, m_ni;
+  fmx::DBuf<uint8_t> m_ins;
+  fmx::DBuf<uint32_t> hist, hist_off;
+  bool have_match = false;
+
+  // ---- sorted correspondences (pair-major SoA) + chunk table
+  uint32_t K = 0;
+  fmx::DBuf<double> c_pl, c_pt;  // [9][cap_pl], [6][cap_pt]
+  size_t ld_pl = 0, ld_pt = 0;
+  fmx::DBuf<uint32_t> pair_counts;  // [2][K] plane rows, point pairs
+  fmx::DBuf<uint32_t> chunk_range;  // [K+1]
+  fmx::DBuf<fmx::Chunk> chunks;
+  fmx::DBuf<uint32_t> n_chunks;
+  uint32_t max_chunks = 0;
+  bool have_corr = false;
+  uint64_t rows_pl = 0, rows_pt = 0;           // correspondences (plane rows, point pairs)
+  std::vector<uint32_t> cnt_pl, cnt_pt;         // per pair, host copy after match
+  fmx::HBuf<double> h_corr;
+  fmx::HBuf<uint32_t> h_meta, h_counts;
+  bool lds_attr_set = false;
+
+  // ---- linearize
+  fmx::DBuf<double> poses_ij, partials, G;
+  fmx::HBuf<double> h_poses, h_G;
+  fmx::HBuf<int32_t> h_i32;
+
+  // ---- host estimator state (register_scan)
+  struct Est;
+  Est* est = nullptr;
+  uint64_t stats[8] = {};
+};
+
+namespace fmx {
+// launchers (extract.hip / voxelmap.hip / linearize.hip)
+void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out);
+void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w);
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map);
+void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
+void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
+                   double* G_out, double* err_out);
+void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
+                 const double* ppj, const uint32_t* nt, const double* tpi, const double* tpj);
+constexpr int kPlaneChunk = 1024;  // plane rows per linearize chunk
+constexpr int kPointChunk = 512;   // point pairs per linearize chunk
+}  // namespace fmx

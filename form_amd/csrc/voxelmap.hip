@@ -1,0 +1,596 @@
+// voxelmap.hip — stage 2: device voxel-hash submap and nearest-neighbour matching.
+//
+// Replaces tsl::robin_map<Vector3i, std::vector<Point>> (form/mapping/map.hpp:66-94)
+// and the TBB matcher (form/optimization/matcher.hpp:67-112):
+//   build  : KeypointMap::to_voxel_map (map.tpp:128-146) — transform every window
+//            keypoint to the world frame (double), insert its voxel key
+//            floor(p / w) (map.tpp:35-38) into an open-addressed table (atomic CAS,
+//            linear probing, load <= 0.5), count per voxel, exclusive-scan the
+//            counts, scatter records voxel-contiguously.  One 16-B probe yields
+//            {key, first, count}.
+//   match  : VoxelMap::find_closest (map.tpp:70-91) — the 27 neighbour voxels,
+//            squared distance (dx*dx + dz*dz) + dy*dy in double; ties broken by the
+//            record's build order (the reference keeps the first in shift/insertion
+//            order; identical except for exact distance ties, parity hazard 10).
+//            Voxels whose box lies farther than the acceptance bound are skipped:
+//            only d^2 < max_dist^2 (acceptance, matcher.hpp:103-105) and
+//            d^2 > min_dist_map^2 (insertion, map.tpp:160-163) are observable, and
+//            with w = max_dist_matching every point within that bound lies in the
+//            27 voxels, so the decisions equal the reference's.
+//   pairs  : bucketing per map scan (matcher.hpp:103-111) as a stable counting sort
+//            (block histograms -> offsets -> ranked scatter) into pair-major SoA.
+//   insert : KeypointMap::insert_matches (map.tpp:148-165) as an ordered compaction.
+#include "fmx_device.hpp"
+#include "fmx_internal.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+namespace fmx {
+namespace {
+
+constexpr int kMatchThreads = 256;
+
+__device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
+  int lo = 0, hi = K - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].off <= rec) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_map_insert(const float4* __restrict__ pool_pos,
+                                                    const float4* __restrict__ pool_nrm, int planar,
+                                                    const Seg* __restrict__ segs, int K,
+                                                    const double* __restrict__ poses, uint32_t nrec,
+                                                    double w, Slot* __restrict__ table, uint64_t mask,
+                                                    double4* __restrict__ tpos, double4* __restrict__ tnrm,
+                                                    uint32_t* __restrict__ rslot, uint32_t* __restrict__ rseg,
+                                                    uint32_t* __restrict__ err) {
+  const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rec >= nrec) return;
+  const int s = find_seg(segs, K, rec);
+  const Seg sg = segs[s];
+  const double* T = poses + 12 * s;
+  const float4 lp = pool_pos[sg.pool_off + (rec - sg.off)];
+  double wp[3];
+  d_xform(T, (double)lp.x, (double)lp.y, (double)lp.z, wp);  // PlanarFeat::transform (features.hpp:137-140)
+  tpos[rec] = make_double4(wp[0], wp[1], wp[2], 0.0);
+  if (planar) {
+    const float4 ln = pool_nrm[sg.pool_off + (rec - sg.off)];
+    double wn[3];
+    d_rot(T, (double)ln.x, (double)ln.y, (double)ln.z, wn);
+    tnrm[rec] = make_double4(wn[0], wn[1], wn[2], 0.0);
+  }
+  rseg[rec] = (uint32_t)s;
+  const int cx = (int)floor(wp[0] / w), cy = (int)floor(wp[1] / w), cz = (int)floor(wp[2] / w);
+  if (!key_in_range(cx, cy, cz)) {
+    atomicOr(err, 1u);
+    rslot[rec] = 0xFFFFFFFFu;
+    return;
+  }
+  const unsigned long long key = pack_key(cx, cy, cz);
+  uint64_t h = mix64(key) & mask;
+  for (;;) {
+    const unsigned long long prev = atomicCAS(&table[h].key, 0ull, key);
+    if (prev == 0ull || prev == key) break;
+    h = (h + 1) & mask;
+  }
+  atomicAdd(&table[h].count, 1u);
+  rslot[rec] = (uint32_t)h;
+}
+
+struct CountIn {
+  const Slot* t;
+  __device__ uint32_t operator()(size_t i) const { return t[i].count; }
+};
+struct FirstOut {
+  Slot* t;
+  __device__ void operator()(size_t i, uint32_t v) const { t[i].first = v; }
+};
+
+__global__ __launch_bounds__(256) void k_map_scatter(uint32_t nrec, const uint32_t* __restrict__ rslot,
+                                                     const uint32_t* __restrict__ rseg,
+                                                     const double4* __restrict__ tpos,
+                                                     const double4* __restrict__ tnrm, int planar,
+                                                     const Slot* __restrict__ table, uint32_t* __restrict__ cursor,
+                                                     double4* __restrict__ pos, double4* __restrict__ nrm,
+                                                     uint32_t* __restrict__ seg, uint32_t* __restrict__ rid) {
+  const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rec >= nrec) return;
+  const uint32_t s = rslot[rec];
+  if (s == 0xFFFFFFFFu) return;
+  const uint32_t o = table[s].first + atomicAdd(&cursor[s], 1u);
+  pos[o] = tpos[rec];
+  if (planar) nrm[o] = tnrm[rec];
+  seg[o] = rseg[rec];
+  rid[o] = rec;
+}
+
+struct MapView {
+  const Slot* table;
+  uint64_t mask;
+  const double4* pos;
+  const double4* nrm;
+  const uint32_t* seg;
+  const uint32_t* rid;
+};
+
+__device__ __constant__ int c_shift[27][3] = {
+    {0, 0, 0},   {1, 0, 0},   {-1, 0, 0},  {0, 1, 0},   {0, -1, 0},  {0, 0, 1},  {0, 0, -1},
+    {1, 1, 0},   {1, -1, 0},  {-1, 1, 0},  {-1, -1, 0}, {1, 0, 1},   {1, 0, -1}, {-1, 0, 1},
+    {-1, 0, -1}, {0, 1, 1},   {0, 1, -1},  {0, -1, 1},  {0, -1, -1}, {1, 1, 1},  {1, 1, -1},
+    {1, -1, 1},  {1, -1, -1}, {-1, 1, 1},  {-1, 1, -1}, {-1, -1, 1}, {-1, -1, -1}};
+
+struct MatchArgs {
+  double Tj[12];
+  double w;
+  double bound;  // prune bound on d^2 (+inf: no pruning)
+  double max_d2, min_d2;
+  uint32_t nq_pl, nq_pt, nb_pl;  // queries; planar blocks
+  int K;
+};
+
+// One lane per query; blocks [0, nb_pl) planar queries, the rest point queries.
+__global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp, MapView mt,
+                                                         const float4* __restrict__ q_pl,
+                                                         const float4* __restrict__ q_pt,
+                                                         const double* __restrict__ inv_poses,
+                                                         int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
+                                                         double4* __restrict__ m_pi, double4* __restrict__ m_ni,
+                                                         uint8_t* __restrict__ m_ins, uint32_t* __restrict__ hist) {
+  extern __shared__ uint32_t s_hist[];  // [K]
+  const bool planar = blockIdx.x < a.nb_pl;
+  const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kMatchThreads + threadIdx.x;
+  const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
+  const MapView& M = planar ? mp : mt;
+  for (int k = threadIdx.x; k < a.K; k += kMatchThreads) s_hist[k] = 0;
+  __syncthreads();
+  if (qi < nq) {
+    const float4 lq = planar ? q_pl[qi] : q_pt[qi];
+    double wq[3];
+    d_xform(a.Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
+    const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
+    // distances from the query to its voxel's faces (for the per-voxel lower bound)
+    const double lo[3] = {wq[0] - bx * a.w, wq[1] - by * a.w, wq[2] - bz * a.w};
+    const double hi[3] = {(bx + 1) * a.w - wq[0], (by + 1) * a.w - wq[1], (bz + 1) * a.w - wq[2]};
+    double best = a.bound;
+    uint32_t best_rid = 0xFFFFFFFFu, best_i = 0;
+    bool found = false;
+    if (key_in_range(bx, by, bz)) {
+      for (int s = 0; s < 27; ++s) {
+        const int sx = c_shift[s][0], sy = c_shift[s][1], sz = c_shift[s][2];
+        double lb = 0.0;
+        {
+          const double ex = sx < 0 ? lo[0] : (sx > 0 ? hi[0] : 0.0);
+          const double ey = sy < 0 ? lo[1] : (sy > 0 ? hi[1] : 0.0);
+          const double ez = sz < 0 ? lo[2] : (sz > 0 ? hi[2] : 0.0);
+          const double mx = fmax(ex - 1e-9, 0.0), my = fmax(ey - 1e-9, 0.0), mz = fmax(ez - 1e-9, 0.0);
+          lb = mx * mx + my * my + mz * mz;
+        }
+        if (lb > best) continue;
+        const unsigned long long key = pack_key(bx + sx, by + sy, bz + sz);
+        uint64_t h = mix64(key) & M.mask;
+        uint32_t first = 0, count = 0;
+        for (;;) {
+          const Slot sl = M.table[h];
+          if (sl.key == key) {
+            first = sl.first;
+            count = sl.count;
+            break;
+          }
+          if (sl.key == 0ull) break;
+          h = (h + 1) & M.mask;
+        }
+        for (uint32_t i = first; i < first + count; ++i) {
+          const double4 p = M.pos[i];
+          const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
+          const double d2 = (dx * dx + dz * dz) + dy * dy;
+          if (d2 < best || (d2 == best && M.rid[i] < best_rid)) {
+            best = d2;
+            best_rid = M.rid[i];
+            best_i = i;
+            found = true;
+          }
+        }
+      }
+    }
+    int32_t pair = -1;
+    double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
+    if (found) {
+      const uint32_t sg = M.seg[best_i];
+      const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
+      const double4 p = M.pos[best_i];
+      double o[3];
+      d_xform(Ti, p.x, p.y, p.z, o);
+      pi = make_double4(o[0], o[1], o[2], 0.0);
+      if (planar) {
+        const double4 n = M.nrm[best_i];
+        d_rot(Ti, n.x, n.y, n.z, o);
+        ni = make_double4(o[0], o[1], o[2], 0.0);
+      }
+      if (best < a.max_d2) pair = (int32_t)sg;
+    }
+    const uint32_t gq = planar ? qi : a.nq_pl + qi;
+    m_pair[gq] = pair;
+    m_d2[gq] = found ? best : DBL_MAX;
+    m_pi[gq] = pi;
+    if (planar) m_ni[qi] = ni;
+    m_ins[gq] = (!found || best > a.min_d2) ? 1 : 0;
+    if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[(size_t)blockIdx.x * a.K + k] = s_hist[k];
+}
+
+// One block: per-type per-pair block offsets (stable counting sort), pair counts,
+// and the linearize chunk table (pair-major: plane chunks then point chunks).
+__global__ __launch_bounds__(1024) void k_pair_offsets(const uint32_t* __restrict__ hist, uint32_t nb_pl,
+                                                       uint32_t nb_pt, int K, uint32_t* __restrict__ hist_off,
+                                                       uint32_t* __restrict__ pair_counts,
+                                                       uint32_t* __restrict__ chunk_range, Chunk* __restrict__ chunks,
+                                                       uint32_t* __restrict__ n_chunks) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry;
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t b0 = t == 0 ? 0 : nb_pl, nb = t == 0 ? nb_pl : nb_pt;
+    // per pair: running sum over blocks
+    for (int k = threadIdx.x; k < K; k += 1024) {
+      uint32_t run = 0;
+      for (uint32_t b = 0; b < nb; ++b) {
+        const size_t i = (size_t)(b0 + b) * K + k;
+        hist_off[i] = run;
+        run += hist[i];
+      }
+      pair_counts[t * K + k] = run;
+    }
+    __syncthreads();
+    // exclusive scan of totals over pairs -> base
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int k0 = 0; k0 < K; k0 += 1024) {
+      const int k = k0 + threadIdx.x;
+      const uint32_t v = k < K ? pair_counts[t * K + k] : 0u;
+      const uint32_t incl = wave_incl_scan(v);
+      const int w = threadIdx.x / kWave;
+      if (lane_id() == 63) ws[w] = incl;
+      __syncthreads();
+      uint32_t off = 0, tot = 0;
+      for (int i = 0; i < 16; ++i) {
+        if (i < w) off += ws[i];
+        tot += ws[i];
+      }
+      const uint32_t base = carry + off + incl - v;
+      if (k < K)
+        for (uint32_t b = 0; b < nb; ++b) hist_off[(size_t)(b0 + b) * K + k] += base;
+      __syncthreads();
+      if (threadIdx.x == 0) carry += tot;
+      __syncthreads();
+    }
+  }
+  // chunk table
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int k0 = 0; k0 < K; k0 += 1024) {
+    const int k = k0 + threadIdx.x;
+    uint32_t npl = 0, npt = 0, v = 0;
+    if (k < K) {
+      npl = pair_counts[k];
+      npt = pair_counts[K + k];
+      v = (npl + kPlaneChunk - 1) / kPlaneChunk + (npt + kPointChunk - 1) / kPointChunk;
+    }
+    const uint32_t incl = wave_incl_scan(v);
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < 16; ++i) {
+      if (i < w) off += ws[i];
+      tot += ws[i];
+    }
+    if (k < K) {
+      uint32_t cb = carry + off + incl - v;
+      chunk_range[k] = cb;
+      // plane rows of pair k start at the sum of the plane counts of pairs < k:
+      // recovered from the first block offset of that pair.
+      const uint32_t pl0 = nb_pl ? hist_off[k] : 0u;
+      const uint32_t pt0 = nb_pt ? hist_off[(size_t)nb_pl * K + k] : 0u;
+      for (uint32_t r = 0; r < npl; r += kPlaneChunk) chunks[cb++] = Chunk{0, (uint32_t)k, pl0 + r, pl0 + min(npl, r + kPlaneChunk)};
+      for (uint32_t r = 0; r < npt; r += kPointChunk) chunks[cb++] = Chunk{1, (uint32_t)k, pt0 + r, pt0 + min(npt, r + kPointChunk)};
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    chunk_range[K] = carry;
+    *n_chunks = carry;
+  }
+}
+
+// Stable scatter of accepted matches into pair-major SoA correspondences.
+__global__ __launch_bounds__(kMatchThreads) void k_pair_scatter(uint32_t nq_pl, uint32_t nq_pt, uint32_t nb_pl, int K,
+                                                                const int32_t* __restrict__ m_pair,
+                                                                const double4* __restrict__ m_pi,
+                                                                const double4* __restrict__ m_ni,
+                                                                const float4* __restrict__ q_pl,
+                                                                const float4* __restrict__ q_pt,
+                                                                const uint32_t* __restrict__ hist_off,
+                                                                double* __restrict__ c_pl, size_t ld_pl,
+                                                                double* __restrict__ c_pt, size_t ld_pt) {
+  extern __shared__ uint32_t s_wc[];  // [4][K] per-wave counts, then exclusive per wave
+  const bool planar = blockIdx.x < nb_pl;
+  const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - nb_pl) * kMatchThreads + threadIdx.x;
+  const uint32_t nq = planar ? nq_pl : nq_pt;
+  const int w = threadIdx.x / kWave;
+  for (int i = threadIdx.x; i < 4 * K; i += kMatchThreads) s_wc[i] = 0;
+  __syncthreads();
+  const int32_t pair = qi < nq ? m_pair[planar ? qi : nq_pl + qi] : -1;
+  // rank within wave among lanes with the same pair (stable by lane)
+  uint32_t rank = 0;
+  bool todo = pair >= 0;
+  while (__ballot(todo)) {
+    const int lead = __ffsll((unsigned long long)__ballot(todo)) - 1;
+    const int v = __shfl(pair, lead, 64);
+    const uint64_t m = __ballot(todo && pair == v);
+    if (todo && pair == v) {
+      rank = __popcll(m & lanemask_lt());
+      todo = false;
+    }
+    if (lane_id() == 0) s_wc[w * K + v] = __popcll(m);
+  }
+  __syncthreads();
+  if (pair >= 0) {
+    uint32_t before = 0;
+    for (int i = 0; i < w; ++i) before += s_wc[i * K + pair];
+    const uint32_t dst = hist_off[(size_t)blockIdx.x * K + pair] + before + rank;
+    const size_t gq = planar ? qi : nq_pl + qi;
+    const double4 pi = m_pi[gq];
+    if (planar) {
+      const double4 ni = m_ni[qi];
+      const float4 pj = q_pl[qi];
+      c_pl[0 * ld_pl + dst] = pi.x; c_pl[1 * ld_pl + dst] = pi.y; c_pl[2 * ld_pl + dst] = pi.z;
+      c_pl[3 * ld_pl + dst] = ni.x; c_pl[4 * ld_pl + dst] = ni.y; c_pl[5 * ld_pl + dst] = ni.z;
+      c_pl[6 * ld_pl + dst] = (double)pj.x; c_pl[7 * ld_pl + dst] = (double)pj.y;
+      c_pl[8 * ld_pl + dst] = (double)pj.z;
+    } else {
+      const float4 pj = q_pt[qi];
+      c_pt[0 * ld_pt + dst] = pi.x; c_pt[1 * ld_pt + dst] = pi.y; c_pt[2 * ld_pt + dst] = pi.z;
+      c_pt[3 * ld_pt + dst] = (double)pj.x; c_pt[4 * ld_pt + dst] = (double)pj.y;
+      c_pt[5 * ld_pt + dst] = (double)pj.z;
+    }
+  }
+}
+
+struct InsIn {
+  const uint8_t* f;
+  __device__ uint32_t operator()(size_t i) const { return f[i]; }
+};
+struct InsOutPl {
+  const uint8_t* f;
+  const float4* pos;
+  const float4* nrm;
+  float4* dpos;
+  float4* dnrm;
+  __device__ void operator()(size_t i, uint32_t o) const {
+    if (f[i]) {
+      dpos[o] = pos[i];
+      dnrm[o] = nrm[i];
+    }
+  }
+};
+struct InsOutPt {
+  const uint8_t* f;
+  const float4* pos;
+  float4* dpos;
+  __device__ void operator()(size_t i, uint32_t o) const {
+    if (f[i]) dpos[o] = pos[i];
+  }
+};
+
+uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- host
+void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w) {
+  hipStream_t st = c->stream;
+  const int K = (int)scans.size();
+  c->map_scans = scans;
+  c->voxel_w = w;
+  c->K = (uint32_t)K;
+  // poses and their inverses (GTSAM Pose3::inverse: (R^T, R^T (-t))), computed on the
+  // host with the same expression order as the device transforms.
+  c->h_mapposes.ensure(24 * (size_t)std::max(K, 1));
+  double* hp = c->h_mapposes.p;
+  for (int k = 0; k < K; ++k) {
+    const double* T = poses34 + 12 * k;
+    std::memcpy(hp + 12 * k, T, 12 * sizeof(double));
+    double* I = hp + 12 * (K + k);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) I[4 * i + j] = T[4 * j + i];
+    const double nt[3] = {-T[3], -T[7], -T[11]};
+    for (int i = 0; i < 3; ++i) I[4 * i + 3] = (I[4 * i] * nt[0] + I[4 * i + 1] * nt[1]) + I[4 * i + 2] * nt[2];
+  }
+  c->map_poses.ensure(12 * (size_t)std::max(K, 1));
+  c->map_inv_poses.ensure(12 * (size_t)std::max(K, 1));
+  if (K > 0) {
+    FMX_HIP(hipMemcpyAsync(c->map_poses.p, hp, 12 * K * sizeof(double), hipMemcpyHostToDevice, st));
+    FMX_HIP(hipMemcpyAsync(c->map_inv_poses.p, hp + 12 * K, 12 * K * sizeof(double), hipMemcpyHostToDevice, st));
+  }
+  c->map_err.ensure(1);
+  FMX_HIP(hipMemsetAsync(c->map_err.p, 0, 4, st));
+  for (int t = 0; t < 2; ++t) {
+    Pool& pool = c->pool[t];
+    VoxMap& M = c->map[t];
+    std::vector<Seg> hs(std::max(K, 1));
+    uint32_t n = 0;
+    for (int k = 0; k < K; ++k) {
+      auto it = pool.ranges.find(scans[k]);
+      const uint32_t cnt = it == pool.ranges.end() ? 0u : it->second.second;
+      const uint32_t po = it == pool.ranges.end() ? 0u : (uint32_t)it->second.first;
+      hs[k] = Seg{n, cnt, po, 0};
+      n += cnt;
+    }
+    M.n = n;
+    c->segs[t].ensure(std::max(K, 1));
+    // pinned staging owned by the map build (never reused before the next sync)
+    c->h_segs[t].ensure(std::max(K, 1));
+    std::memcpy(c->h_segs[t].p, hs.data(), sizeof(Seg) * std::max(K, 1));
+    FMX_HIP(hipMemcpyAsync(c->segs[t].p, c->h_segs[t].p, sizeof(Seg) * std::max(K, 1), hipMemcpyHostToDevice, st));
+    const uint64_t use = next_pow2(std::max<uint64_t>(2ull * n, 1024));  // load factor <= 0.5
+    M.table.ensure(use);
+    M.cursor.ensure(use);
+    M.cap = use;
+    FMX_HIP(hipMemsetAsync(M.table.p, 0, use * sizeof(Slot), st));
+    FMX_HIP(hipMemsetAsync(M.cursor.p, 0, use * sizeof(uint32_t), st));
+    M.tpos.ensure(n + 1);
+    M.rslot.ensure(n + 1);
+    M.rseg.ensure(n + 1);
+    M.pos.ensure(n + 1);
+    M.seg.ensure(n + 1);
+    M.rid.ensure(n + 1);
+    if (t == 0) {
+      M.tnrm.ensure(n + 1);
+      M.nrm.ensure(n + 1);
+    }
+    const double bytes = (t == 0 ? 2.0 * 32.0 : 2.0 * 16.0) * n + 16.0 * (double)use;
+    ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
+    if (n > 0) {
+      hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, pool.pos.p, pool.nrm.p, t == 0 ? 1 : 0,
+                         c->segs[t].p, K, c->map_poses.p, n, w, reinterpret_cast<Slot*>(M.table.p), use - 1,
+                         M.tpos.p, M.tnrm.p, M.rslot.p, M.rseg.p, c->map_err.p);
+      FMX_HIP(hipGetLastError());
+      c->scan_scratch.ensure(scan_scratch_size(use) + 4);
+      c->dev_u32.ensure(8);
+      exclusive_scan(CountIn{reinterpret_cast<const Slot*>(M.table.p)}, FirstOut{reinterpret_cast<Slot*>(M.table.p)},
+                     use, c->scan_scratch.p, c->dev_u32.p + 4, st);
+      hipLaunchKernelGGL(k_map_scatter, dim3((n + 255) / 256), dim3(256), 0, st, n, M.rslot.p, M.rseg.p, M.tpos.p,
+                         M.tnrm.p, t == 0 ? 1 : 0, reinterpret_cast<const Slot*>(M.table.p), M.cursor.p, M.pos.p,
+                         M.nrm.p, M.seg.p, M.rid.p);
+      FMX_HIP(hipGetLastError());
+    }
+  }
+  c->have_map = true;
+  c->have_match = false;
+}
+
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map) {
+  hipStream_t st = c->stream;
+  const int K = std::max<int>((int)c->K, 1);
+  MatchArgs a;
+  std::memcpy(a.Tj, pose_j34, sizeof(a.Tj));
+  a.w = c->voxel_w;
+  a.max_d2 = max_dist * max_dist;
+  a.min_d2 = min_dist_map * min_dist_map;
+  const double obs = std::max(a.max_d2, a.min_d2);
+  a.bound = obs <= a.w * a.w ? obs : INFINITY;
+  a.nq_pl = c->n_qpl;
+  a.nq_pt = c->n_qpt;
+  a.nb_pl = (c->n_qpl + kMatchThreads - 1) / kMatchThreads;
+  const uint32_t nb_pt = (c->n_qpt + kMatchThreads - 1) / kMatchThreads;
+  a.K = (int)c->K;
+  const uint32_t nq = c->n_qpl + c->n_qpt;
+  c->m_pair.ensure(nq + 1);
+  c->m_d2.ensure(nq + 1);
+  c->m_pi.ensure(nq + 1);
+  c->m_ni.ensure(c->n_qpl + 1);
+  c->m_ins.ensure(nq + 1);
+  const uint32_t nb = a.nb_pl + nb_pt;
+  c->hist.ensure((size_t)(nb + 1) * K);
+  c->hist_off.ensure((size_t)(nb + 1) * K);
+  c->pair_counts.ensure(2 * (size_t)K);
+  c->chunk_range.ensure(K + 1);
+  const uint32_t maxch = c->n_qpl / kPlaneChunk + c->n_qpt / kPointChunk + 2 * K + 2;
+  c->chunks.ensure(maxch);
+  c->n_chunks.ensure(1);
+  c->max_chunks = maxch;
+  c->ld_pl = c->n_qpl + 1;
+  c->ld_pt = c->n_qpt + 1;
+  c->c_pl.ensure(9 * c->ld_pl);
+  c->c_pt.ensure(6 * c->ld_pt);
+  auto view = [&](int t) {
+    VoxMap& M = c->map[t];
+    return MapView{reinterpret_cast<const Slot*>(M.table.p), M.cap ? M.cap - 1 : 0, M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
+  };
+  if (nb > 0) {
+    const double bytes = 32.0 * c->n_qpl + 16.0 * c->n_qpt;
+    ProfScope ps(c->prof, PROF_MATCH, bytes, st);
+    hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
+                       c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_poses.p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
+                       c->m_ni.p, c->m_ins.p, c->hist.p);
+    FMX_HIP(hipGetLastError());
+  }
+  {
+    ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
+    hipLaunchKernelGGL(k_pair_offsets, dim3(1), dim3(1024), 0, st, c->hist.p, a.nb_pl, nb_pt, a.K, c->hist_off.p,
+                       c->pair_counts.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p);
+    FMX_HIP(hipGetLastError());
+    if (nb > 0) {
+      hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(kMatchThreads), 4 * K * sizeof(uint32_t), st, c->n_qpl,
+                         c->n_qpt, a.nb_pl, a.K, c->m_pair.p, c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p,
+                         c->hist_off.p, c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
+      FMX_HIP(hipGetLastError());
+    }
+  }
+  // per-pair counts to the host (the caller needs them; one sync per match)
+  c->h_counts.ensure(2 * (size_t)K);
+  FMX_HIP(hipMemcpyAsync(c->h_counts.p, c->pair_counts.p, 2 * (size_t)c->K * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  c->cnt_pl.assign(c->h_counts.p, c->h_counts.p + c->K);
+  c->cnt_pt.assign(c->h_counts.p + c->K, c->h_counts.p + 2 * c->K);
+  c->rows_pl = c->rows_pt = 0;
+  for (uint32_t k = 0; k < c->K; ++k) {
+    c->rows_pl += c->cnt_pl[k];
+    c->rows_pt += c->cnt_pt[k];
+  }
+  c->have_match = true;
+  c->have_corr = true;
+}
+
+void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
+  hipStream_t st = c->stream;
+  uint32_t tot[2] = {0, 0};
+  c->dev_u32.ensure(8);
+  c->h_u32.ensure(8);
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t nq = t == 0 ? c->n_qpl : c->n_qpt;
+    const uint8_t* f = c->m_ins.p + (t == 0 ? 0 : c->n_qpl);
+    Pool& pool = c->pool[t];
+    // worst case every query inserted
+    if (pool.used + nq > pool.pos.cap) throw StatusError(FMX_E_OOM, "keypoint pool capacity exceeded");
+    c->scan_scratch.ensure(scan_scratch_size(nq) + 4);
+    ProfScope ps(c->prof, PROF_INSERT, (t == 0 ? 33.0 : 17.0) * nq, st);
+    if (t == 0)
+      exclusive_scan(InsIn{f}, InsOutPl{f, c->q_pl_pos.p, c->q_pl_nrm.p, pool.pos.p + pool.used, pool.nrm.p + pool.used},
+                     nq, c->scan_scratch.p, c->dev_u32.p + t, st);
+    else
+      exclusive_scan(InsIn{f}, InsOutPt{f, c->q_pt_pos.p, pool.pos.p + pool.used}, nq, c->scan_scratch.p,
+                     c->dev_u32.p + t, st);
+  }
+  FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->dev_u32.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  for (int t = 0; t < 2; ++t) {
+    tot[t] = (t == 0 ? c->n_qpl : c->n_qpt) ? c->h_u32.p[t] : 0u;
+    Pool& pool = c->pool[t];
+    auto& rg = pool.ranges[scan];
+    if (rg.second == 0) rg.first = pool.used;
+    else if (rg.first + rg.second != pool.used) throw StatusError(FMX_E_STATE, "non-contiguous insert for scan");
+    rg.second += tot[t];
+    pool.used += tot[t];
+  }
+  if (n_inserted) {
+    n_inserted[0] = tot[0];
+    n_inserted[1] = tot[1];
+  }
+}
+
+}  // namespace fmx

@@ -1,0 +1,358 @@
+"""ctypes host layer over libfmx.so (include/fmx/fmx.h).
+
+Mirrors the reference's Python-facing surface for this path:
+  * ``KeypointExtractionParams`` / ``extract_keypoints`` — form._core
+    (python/bindings.cpp:194-240): returns (planar_points, normals, point_points).
+  * ``Estimator`` — form::Estimator (form/form.hpp:40-84): ``register_scan(scan)``
+    returns the (planar, point) features, ``current_lidar_estimate()`` the pose.
+  * ``Context`` — the stage-level seams (extract / map_build / match /
+    linearize / error / insert) used by the parity tests.
+
+There is no CPU fallback: if libfmx.so is missing or no HIP device is visible the
+import or the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, fields
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfmx.so")
+_LIB = None
+
+FMX_OK = 0
+_STATUS = {1: "FMX_E_INVAL", 2: "FMX_E_SIZE", 3: "FMX_E_OOM", 4: "FMX_E_HIP", 5: "FMX_E_STATE",
+           6: "FMX_E_RANGE"}
+
+
+class FmxError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{_STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+class _ExtractParams(C.Structure):
+    _fields_ = [
+        ("neighbor_points", C.c_uint32), ("num_sectors", C.c_uint32),
+        ("planar_threshold", C.c_double), ("planar_feats_per_sector", C.c_uint32),
+        ("point_feats_per_sector", C.c_uint32), ("radius", C.c_double),
+        ("min_points", C.c_uint32), ("min_norm_squared", C.c_double),
+        ("max_norm_squared", C.c_double), ("num_columns", C.c_int32), ("num_rows", C.c_int32),
+    ]
+
+
+class _Params(C.Structure):
+    _fields_ = [
+        ("extraction", _ExtractParams), ("max_dist_matching", C.c_double),
+        ("new_pose_threshold", C.c_double), ("max_num_rematches", C.c_uint32),
+        ("planar_constraint_sigma", C.c_double), ("disable_smoothing", C.c_int32),
+        ("max_num_keyscans", C.c_int64), ("max_steps_unused_keyscan", C.c_int64),
+        ("max_num_recent_scans", C.c_uint32), ("keyscan_match_ratio", C.c_double),
+        ("min_dist_map", C.c_double), ("keypoint_pool_capacity", C.c_uint64),
+        ("max_pairs", C.c_uint32),
+    ]
+
+
+class _Counts(C.Structure):
+    _fields_ = [("planar", C.c_uint32), ("point", C.c_uint32), ("planar_selected", C.c_uint32)]
+
+
+def lib():
+    """Load libfmx.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C form_amd/csrc)")
+        L = C.CDLL(LIB_PATH)
+        L.fmx_last_error.restype = C.c_char_p
+        L.fmx_profile_name.restype = C.c_char_p
+        _LIB = L
+    return _LIB
+
+
+EXPORTED = [
+    "fmx_abi_version", "fmx_default_params", "fmx_create", "fmx_destroy", "fmx_last_error",
+    "fmx_extract", "fmx_extract_download", "fmx_set_queries", "fmx_keypoints_add",
+    "fmx_keypoints_remove", "fmx_map_build", "fmx_match", "fmx_match_download", "fmx_map_insert",
+    "fmx_corr_set", "fmx_linearize", "fmx_error", "fmx_register_scan", "fmx_current_pose",
+    "fmx_last_stats", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
+    "fmx_profile_name", "fmx_profile_read", "fmx_sync",
+]
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+@dataclass
+class KeypointExtractionParams:
+    """form::FeatureExtractor::Params (extraction.hpp:59-88); same names as the
+    nanobind class KeypointExtractionParams (bindings.cpp:194-211)."""
+    neighbor_points: int = 5
+    num_sectors: int = 6
+    planar_threshold: float = 1.0
+    planar_feats_per_sector: int = 50
+    point_feats_per_sector: int = 3
+    radius: float = 1.0
+    min_points: int = 5
+    min_norm_squared: float = 1.0
+    max_norm_squared: float = 100.0 * 100.0
+    num_columns: int = 1024
+    num_rows: int = 64
+
+    def as_dict(self):
+        return {f.name: getattr(self, f.name) for f in fields(self)}
+
+
+@dataclass
+class EstimatorParams:
+    """form::Estimator::Params (form.hpp:42-56), flattened like the evalio YAML keys
+    (bindings.cpp:66-88)."""
+    extraction: KeypointExtractionParams = None
+    max_dist_matching: float = 0.8
+    new_pose_threshold: float = 1e-4
+    max_num_rematches: int = 30
+    planar_constraint_sigma: float = 0.1
+    disable_smoothing: bool = True
+    max_num_keyscans: int = 50
+    max_steps_unused_keyscan: int = 10
+    max_num_recent_scans: int = 10
+    keyscan_match_ratio: float = 0.1
+    min_dist_map: float = 0.1
+    keypoint_pool_capacity: int = 4 << 20
+    max_pairs: int = 1024
+
+    def __post_init__(self):
+        if self.extraction is None:
+            self.extraction = KeypointExtractionParams()
+
+    def to_c(self) -> _Params:
+        p = _Params()
+        lib().fmx_default_params(C.byref(p))
+        for k, v in self.extraction.as_dict().items():
+            setattr(p.extraction, k, v)
+        for f in fields(self):
+            if f.name != "extraction":
+                setattr(p, f.name, int(getattr(self, f.name)) if isinstance(getattr(self, f.name), bool)
+                        else getattr(self, f.name))
+        return p
+
+
+class Context:
+    """One fmx context (one HIP device + stream).  Thin, stage-level API."""
+
+    def __init__(self, params: EstimatorParams | None = None, device: int = 0):
+        self.params = params or EstimatorParams()
+        self._L = lib()
+        h = C.c_void_p()
+        st = self._L.fmx_create(C.byref(self.params.to_c()), C.c_int(device), C.byref(h))
+        if st != FMX_OK:
+            raise FmxError(st, "fmx_create failed (is a HIP device visible?)")
+        self.h = h
+        self.K = 0
+        self.n_planar = 0
+        self.n_point = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.fmx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, st: int):
+        if st != FMX_OK:
+            raise FmxError(st, self._L.fmx_last_error(self.h).decode())
+
+    # ---------------------------------------------------------------- stage 1
+    def extract(self, scan, scan_idx: int = 0):
+        """scan: (N, 4) float32 numpy array (host) or torch tensor (host or device)."""
+        on_dev, ptr, n, keep = _scan_ptr(scan)
+        c = _Counts()
+        self._chk(self._L.fmx_extract(self.h, ptr, C.c_size_t(n), C.c_uint64(scan_idx),
+                                      C.c_int(on_dev), C.byref(c)))
+        del keep
+        self.n_planar, self.n_point = c.planar, c.point
+        return c.planar, c.point, c.planar_selected
+
+    def extract_download(self, with_mask: bool = False):
+        npl, npt = self.n_planar, self.n_point
+        planar = np.zeros((npl, 6), np.float32)
+        pidx = np.zeros(npl, np.uint32)
+        point = np.zeros((npt, 3), np.float32)
+        tidx = np.zeros(npt, np.uint32)
+        e = self.params.extraction
+        mask = np.zeros(e.num_rows * e.num_columns, np.uint8) if with_mask else None
+        self._chk(self._L.fmx_extract_download(self.h, _p(planar), _p(pidx), _p(point), _p(tidx), _p(mask)))
+        out = dict(planar=planar, planar_index=pidx, point=point, point_index=tidx)
+        if with_mask:
+            out["planar_mask"] = mask.astype(bool)
+        return out
+
+    def set_queries(self, planar: np.ndarray, point: np.ndarray, scan_idx: int = 0):
+        planar = np.ascontiguousarray(planar, np.float32).reshape(-1, 6)
+        point = np.ascontiguousarray(point, np.float32).reshape(-1, 3)
+        self._chk(self._L.fmx_set_queries(self.h, C.c_uint64(scan_idx), _p(planar), C.c_uint32(len(planar)),
+                                          _p(point), C.c_uint32(len(point))))
+        self.n_planar, self.n_point = len(planar), len(point)
+
+    # ---------------------------------------------------------------- stage 2
+    def keypoints_add(self, scan_idx: int, planar: np.ndarray, point: np.ndarray):
+        planar = np.ascontiguousarray(planar, np.float32).reshape(-1, 6)
+        point = np.ascontiguousarray(point, np.float32).reshape(-1, 3)
+        self._chk(self._L.fmx_keypoints_add(self.h, C.c_uint64(scan_idx), _p(planar), C.c_uint32(len(planar)),
+                                            _p(point), C.c_uint32(len(point))))
+
+    def keypoints_remove(self, scan_idx: int):
+        self._chk(self._L.fmx_keypoints_remove(self.h, C.c_uint64(scan_idx)))
+
+    def map_build(self, scans, poses34, voxel_width: float):
+        scans = np.ascontiguousarray(scans, np.uint64)
+        poses = np.ascontiguousarray(poses34, np.float64).reshape(-1, 12)
+        self._chk(self._L.fmx_map_build(self.h, _p(scans), _p(poses), C.c_uint32(len(scans)),
+                                        C.c_double(voxel_width)))
+        self.K = len(scans)
+
+    def match(self, pose_j34, max_dist: float):
+        pose = np.ascontiguousarray(pose_j34, np.float64).reshape(12)
+        cpl = np.zeros(max(self.K, 1), np.uint32)
+        cpt = np.zeros(max(self.K, 1), np.uint32)
+        self._chk(self._L.fmx_match(self.h, _p(pose), C.c_double(max_dist), _p(cpl), _p(cpt)))
+        return cpl[:self.K], cpt[:self.K]
+
+    def match_download(self):
+        nq = self.n_planar + self.n_point
+        pair = np.zeros(nq, np.int32)
+        d2 = np.zeros(nq, np.float64)
+        pi = np.zeros((nq, 3), np.float64)
+        ni = np.zeros((self.n_planar, 3), np.float64)
+        self._chk(self._L.fmx_match_download(self.h, _p(pair), _p(d2), _p(pi), _p(ni)))
+        return dict(pair=pair, d2=d2, pi=pi, ni=ni)
+
+    def map_insert(self, min_dist_map: float | None = None):
+        n = np.zeros(2, np.uint32)
+        md = self.params.min_dist_map if min_dist_map is None else min_dist_map
+        self._chk(self._L.fmx_map_insert(self.h, C.c_double(md), _p(n)))
+        return int(n[0]), int(n[1])
+
+    # ---------------------------------------------------------------- stage 3
+    def corr_set(self, n_plane, plane_pi, plane_ni, plane_pj, n_point, point_pi, point_pj):
+        n_plane = np.ascontiguousarray(n_plane, np.uint32)
+        n_point = np.ascontiguousarray(n_point, np.uint32)
+        arrs = [np.ascontiguousarray(a, np.float64).reshape(-1, 3) for a in
+                (plane_pi, plane_ni, plane_pj, point_pi, point_pj)]
+        self._chk(self._L.fmx_corr_set(self.h, C.c_uint32(len(n_plane)), _p(n_plane), _p(arrs[0]), _p(arrs[1]),
+                                       _p(arrs[2]), _p(n_point), _p(arrs[3]), _p(arrs[4])))
+        self.K = len(n_plane)
+
+    def linearize(self, poses_i, poses_j, sigma: float = 0.1, single: bool = False):
+        pi_ = np.ascontiguousarray(poses_i, np.float64).reshape(-1, 12)
+        pj_ = np.ascontiguousarray(poses_j, np.float64).reshape(-1, 12)
+        G = np.zeros((max(self.K, 1), 28 if single else 91))
+        err = np.zeros(max(self.K, 1))
+        self._chk(self._L.fmx_linearize(self.h, _p(pi_), _p(pj_), C.c_double(sigma), C.c_int(int(single)),
+                                        _p(G), _p(err)))
+        return G[:self.K], err[:self.K]
+
+    def error(self, poses_i, poses_j, sigma: float = 0.1):
+        pi_ = np.ascontiguousarray(poses_i, np.float64).reshape(-1, 12)
+        pj_ = np.ascontiguousarray(poses_j, np.float64).reshape(-1, 12)
+        err = np.zeros(max(self.K, 1))
+        self._chk(self._L.fmx_error(self.h, _p(pi_), _p(pj_), C.c_double(sigma), _p(err)))
+        return err[:self.K]
+
+    # ---------------------------------------------------------------- estimator
+    def register_scan(self, scan):
+        on_dev, ptr, n, keep = _scan_ptr(scan)
+        c = _Counts()
+        self._chk(self._L.fmx_register_scan(self.h, ptr, C.c_size_t(n), C.c_int(on_dev), C.byref(c)))
+        del keep
+        self.n_planar, self.n_point = c.planar, c.point
+        return c.planar, c.point
+
+    def current_pose(self) -> np.ndarray:
+        T = np.zeros(12)
+        self._chk(self._L.fmx_current_pose(self.h, _p(T)))
+        return T.reshape(3, 4)
+
+    def last_stats(self) -> dict:
+        s = np.zeros(8, np.uint64)
+        self._chk(self._L.fmx_last_stats(self.h, _p(s)))
+        keys = ["icp_iters", "lm_iters", "matched_planar", "matched_point", "map_planar", "map_point",
+                "linearizations", "map_scans"]
+        return {k: int(v) for k, v in zip(keys, s)}
+
+    # ---------------------------------------------------------------- profiling
+    def profile(self, on: bool = True):
+        self._chk(self._L.fmx_profile_enable(self.h, C.c_int(int(on))))
+
+    def profile_reset(self):
+        self._chk(self._L.fmx_profile_reset(self.h))
+
+    def profile_read(self) -> dict:
+        n = self._L.fmx_profile_count()
+        ms = np.zeros(n)
+        la = np.zeros(n, np.uint64)
+        by = np.zeros(n)
+        self._chk(self._L.fmx_profile_read(self.h, _p(ms), _p(la), _p(by), C.c_int(n)))
+        return {self._L.fmx_profile_name(k).decode(): dict(ms=float(ms[k]), launches=int(la[k]), bytes=float(by[k]))
+                for k in range(n)}
+
+    def sync(self):
+        self._chk(self._L.fmx_sync(self.h))
+
+
+def _scan_ptr(scan):
+    """(on_device, pointer, n_points, keepalive) for a numpy array or torch tensor."""
+    try:
+        import torch
+        if isinstance(scan, torch.Tensor):
+            if scan.dtype != torch.float32 or scan.dim() != 2 or scan.shape[1] != 4:
+                raise ValueError("scan tensor must be (N, 4) float32")
+            t = scan.contiguous()
+            return (1 if t.is_cuda else 0), C.c_void_p(t.data_ptr()), t.shape[0], t
+    except ImportError:
+        pass
+    a = np.ascontiguousarray(scan, np.float32)
+    if a.ndim != 2 or a.shape[1] != 4:
+        raise ValueError("scan must be (N, 4) float32 (PointXYZf layout)")
+    return 0, _p(a), a.shape[0], a
+
+
+class Estimator:
+    """form::Estimator (form/form.hpp:40-84) backed by the MI355X path."""
+
+    def __init__(self, params: EstimatorParams | None = None, device: int = 0):
+        self.ctx = Context(params, device)
+
+    def register_scan(self, scan):
+        """Returns (planar (F,6) xyz+normal, point (F,3)) like register_scan's tuple."""
+        self.ctx.register_scan(scan)
+        d = self.ctx.extract_download()
+        return d["planar"], d["point"]
+
+    def current_lidar_estimate(self) -> np.ndarray:
+        return self.ctx.current_pose()
+
+
+def extract_keypoints(points, params: KeypointExtractionParams, lidar_params=None):
+    """form._core.extract_keypoints (bindings.cpp:214-240): (planar_points, normals,
+    point_points).  lidar_params is accepted and ignored, as in the reference."""
+    pts = np.asarray(points, np.float64).reshape(-1, 3)
+    scan = np.zeros((len(pts), 4), np.float32)
+    scan[:, :3] = pts.astype(np.float32)
+    ctx = Context(EstimatorParams(extraction=params))
+    try:
+        ctx.extract(scan, 0)
+        d = ctx.extract_download()
+    finally:
+        ctx.close()
+    planar = d["planar"].astype(np.float64)
+    return planar[:, :3].copy(), planar[:, 3:].copy(), d["point"].astype(np.float64)

@@ -1,0 +1,183 @@
+/*
+ * fmx.h — C-ABI of the MI355X-native scan-to-submap registration path for FORM.
+ *
+ * Drop-in boundary for form::Estimator's hot path (huangjuite/form).  Every entry
+ * point names the reference interface it replaces (file:line under the reference's
+ * form/ tree).  Plain pointers and sizes only; no exceptions cross this boundary;
+ * errors are status codes + fmx_last_error().  One context = one HIP device + one
+ * HIP stream; a context is NOT thread-safe (the reference's register_scan is also
+ * driven from a single caller thread, bindings.cpp:147-179).
+ *
+ * Conventions
+ *   - points: PointXYZf layout, 4 x float32 per point (x, y, z, pad), row-major
+ *     organized R x C scan (form/utils.hpp:38-46; extraction.tpp:141-145).
+ *   - poses: row-major 3x4 double [R | t] (gtsam::Pose3 = (R, t)).
+ *   - planar features: 6 floats (x, y, z, nx, ny, nz); point features: 3 floats
+ *     (form/feature/features.hpp:31-163 stores the same values as doubles).
+ *   - Jacobian columns: GTSAM Pose3 tangent [w; v], right perturbation.
+ *   - Augmented Hessian G: packed upper triangle, row-major, of [A b]^T [A b] with
+ *     A, b whitened by 1/sigma (gtsam.hpp:67-86, 129-139).  Full mode: 13 x 13 ->
+ *     91 doubles (A = [H_i H_j]); single-pose mode: 7 x 7 -> 28 doubles (A = H_j).
+ */
+#ifndef FMX_FMX_H_
+#define FMX_FMX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMX_ABI_VERSION 1
+
+typedef enum fmx_status {
+  FMX_OK = 0,
+  FMX_E_INVAL = 1, /* bad argument */
+  FMX_E_SIZE = 2,  /* scan size != rows*cols (reference throws, extraction.tpp:141-145) */
+  FMX_E_OOM = 3,   /* device allocation failed or a capacity was exceeded */
+  FMX_E_HIP = 4,   /* HIP runtime error */
+  FMX_E_STATE = 5, /* call out of order (e.g. match before map_build) */
+  FMX_E_RANGE = 6  /* voxel coordinate outside the +-2^20 packed-key range */
+} fmx_status;
+
+/* form::FeatureExtractor::Params (form/feature/extraction.hpp:59-88). */
+typedef struct fmx_extract_params {
+  uint32_t neighbor_points;
+  uint32_t num_sectors;
+  double planar_threshold;
+  uint32_t planar_feats_per_sector;
+  uint32_t point_feats_per_sector;
+  double radius;
+  uint32_t min_points;
+  double min_norm_squared;
+  double max_norm_squared;
+  int32_t num_columns;
+  int32_t num_rows;
+} fmx_extract_params;
+
+/* form::Estimator::Params (form/form.hpp:42-56) flattened, plus device capacities. */
+typedef struct fmx_params {
+  fmx_extract_params extraction;
+  double max_dist_matching;        /* MatcherParams, matcher.hpp:32-41 */
+  double new_pose_threshold;
+  uint32_t max_num_rematches;
+  double planar_constraint_sigma;  /* ConstraintManager::Params, constraints.hpp:54-70 */
+  int32_t disable_smoothing;       /* host adapter implements the single-pose mode */
+  int64_t max_num_keyscans;        /* KeyScanner::Params, keyscanner.hpp:55-64 */
+  int64_t max_steps_unused_keyscan;
+  uint32_t max_num_recent_scans;
+  double keyscan_match_ratio;
+  double min_dist_map;             /* KeypointMapParams, map.hpp:97-100 */
+  /* device capacities (not in the reference: it allocates on demand) */
+  uint64_t keypoint_pool_capacity; /* records per feature type kept in the window store */
+  uint32_t max_pairs;              /* scans per submap (window size bound) */
+} fmx_params;
+
+typedef struct fmx_ctx fmx_ctx;
+
+typedef struct fmx_feature_counts {
+  uint32_t planar; /* planar features with a normal (extraction.tpp:99-118) */
+  uint32_t point;  /* point features (extraction.tpp:120-129) */
+  uint32_t planar_selected; /* planar indices before normal estimation */
+} fmx_feature_counts;
+
+int fmx_abi_version(void);
+void fmx_default_params(fmx_params* p);
+
+/* Estimator(const Params&) (form/form.hpp:74-76, form.cpp:31-38). */
+fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out);
+void fmx_destroy(fmx_ctx* ctx);
+const char* fmx_last_error(const fmx_ctx* ctx);
+
+/* ---------------- stage 1: FeatureExtractor::extract ----------------------
+ * Replaces FeatureExtractor::extract<PointXYZf> (extraction.hpp:99-101,
+ * extraction.tpp:29-132).  xyzw: rows*cols float4; src_on_device != 0 means
+ * xyzw is a device pointer on the context's device, else host memory.
+ * The features stay device-resident as the context's current query set. */
+fmx_status fmx_extract(fmx_ctx* ctx, const float* xyzw, size_t n_points, uint64_t scan_idx,
+                       int src_on_device, fmx_feature_counts* out);
+/* Copy the last extraction to host (any pointer may be NULL):
+ * planar[6*planar], planar_index[planar] (scan point index), point[3*point],
+ * point_index[point], planar_mask[rows*cols] (compute_valid_points, 0/1). */
+fmx_status fmx_extract_download(fmx_ctx* ctx, float* planar, uint32_t* planar_index,
+                                float* point, uint32_t* point_index, uint8_t* planar_mask);
+
+/* Replace the current query set (the scan being registered) with caller features. */
+fmx_status fmx_set_queries(fmx_ctx* ctx, uint64_t scan_idx, const float* planar, uint32_t n_planar,
+                           const float* point, uint32_t n_point);
+
+/* ---------------- stage 2: KeypointMap / VoxelMap / Matcher ---------------
+ * Window keypoint store: KeypointMap::get(scan).push_back / insert_matches /
+ * remove (map.tpp:95-126, 148-165).  Features are in the scan's local frame. */
+fmx_status fmx_keypoints_add(fmx_ctx* ctx, uint64_t scan_idx, const float* planar,
+                             uint32_t n_planar, const float* point, uint32_t n_point);
+fmx_status fmx_keypoints_remove(fmx_ctx* ctx, uint64_t scan_idx);
+/* KeypointMap::to_voxel_map for both feature types (map.tpp:128-146, form.cpp:61-65):
+ * builds the device voxel hash of every stored keypoint of scans[0..n) at the given
+ * world poses.  Pair k of later calls refers to scans[k]. */
+fmx_status fmx_map_build(fmx_ctx* ctx, const uint64_t* scans, const double* poses34,
+                         uint32_t n_scans, double voxel_width);
+/* Matcher<PlanarFeat>::match<0> + Matcher<PointFeat>::match<1> (matcher.hpp:67-112):
+ * nearest map keypoint of every query at pose_j (VoxelMap::find_closest,
+ * map.tpp:70-91), moved back to its scan's frame, accepted if d^2 < max_dist^2 and
+ * bucketed per pair on the device.  counts_planar / counts_point (may be NULL):
+ * K = n_scans accepted correspondences per pair. */
+fmx_status fmx_match(fmx_ctx* ctx, const double pose_j34[12], double max_dist,
+                     uint32_t* counts_planar, uint32_t* counts_point);
+/* Per-query match results of the last fmx_match, planar queries then point
+ * queries (any pointer may be NULL): pair[q] (-1 if not accepted), d2[q]
+ * (DBL_MAX when no map point lies within max_dist), pi[3q], ni[3q] (planar only). */
+fmx_status fmx_match_download(fmx_ctx* ctx, int32_t* pair, double* d2, double* pi, double* ni);
+/* KeypointMap::insert_matches (map.tpp:148-165): append every query of the last
+ * match whose NN distance^2 > min_dist_map^2 to the store under the query scan. */
+fmx_status fmx_map_insert(fmx_ctx* ctx, double min_dist_map, uint32_t* n_inserted);
+
+/* ---------------- stage 3: FeatureFactor + DenseFactor::linearize ---------
+ * Load correspondences directly (replacing the match output), pair-major:
+ * plane rows p_i, n_i, p_j (3 doubles each) and point pairs p_i, p_j.
+ * PlanePoint / PointPoint buffers, factor.hpp:43-130. */
+fmx_status fmx_corr_set(fmx_ctx* ctx, uint32_t K, const uint32_t* n_plane,
+                        const double* plane_pi, const double* plane_ni, const double* plane_pj,
+                        const uint32_t* n_point, const double* point_pi, const double* point_pj);
+/* DenseFactor::linearize of every pair's FeatureFactor (gtsam.hpp:67-86,
+ * factor.cpp:142-186): poses_i / poses_j are K x 12.  G: K x 91 (single_pose=0)
+ * or K x 28 (single_pose=1); err: K x 1 = 0.5*||r/sigma||^2 (may be NULL). */
+fmx_status fmx_linearize(fmx_ctx* ctx, const double* poses_i34, const double* poses_j34,
+                         double sigma, int single_pose, double* G, double* err);
+/* NoiseModelFactor::error of every pair (FeatureFactor::evaluateError without
+ * Jacobians), err: K x 1. */
+fmx_status fmx_error(fmx_ctx* ctx, const double* poses_i34, const double* poses_j34,
+                     double sigma, double* err);
+
+/* ---------------- host adapter: Estimator::register_scan -------------------
+ * form::Estimator::register_scan (form/form.hpp:82-83, form.cpp:40-114) with the
+ * smoother in single-pose mode (ConstraintManager disable_smoothing path,
+ * constraints.cpp:103-111, 235-250): predict, extract, map build, ICP loop
+ * (match + LM), final LM, insert_matches, keyscan selection, marginalization. */
+fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, int src_on_device,
+                             fmx_feature_counts* out);
+/* Estimator::current_lidar_estimate (form/form.hpp:79). */
+fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
+
+/* Statistics of the last register_scan: {icp_iters, lm_iters, matched_planar,
+ * matched_point, map_planar, map_point, voxels_planar, voxels_point}. */
+fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t stats[8]);
+
+/* ---------------- profiling (bench.py roofline) ----------------------------
+ * When enabled, each kernel launch is bracketed by HIP events on the context
+ * stream.  fmx_profile_read fills, for kernel id k < n: total ms, launches and
+ * algorithmic bytes accumulated since the last reset. */
+fmx_status fmx_profile_enable(fmx_ctx* ctx, int on);
+fmx_status fmx_profile_reset(fmx_ctx* ctx);
+int fmx_profile_count(void);
+const char* fmx_profile_name(int k);
+fmx_status fmx_profile_read(fmx_ctx* ctx, double* ms, uint64_t* launches, double* bytes, int n);
+
+/* Synchronize the context stream. */
+fmx_status fmx_sync(fmx_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMX_FMX_H_ */

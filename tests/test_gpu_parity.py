@@ -1,0 +1,143 @@
+"""HIP path (libfmx.so through the C-ABI) vs the CPU oracle on identical inputs.
+
+Bars: bit-exact for integer/index work (selected indices, pair assignments, insert
+decisions); fp32 normals |n_gpu . n_oracle| >= 1 - 1e-6; fp64 G within 1e-10
+relative (summation-order differences only); poses within 1e-6 m / rad.
+"""
+import numpy as np
+import pytest
+
+from form_amd import synth
+from scenario import perturb, random_corr, stream_features
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(fmx, p):
+    return fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**p)))
+
+
+@pytest.mark.parametrize("config,k", [("tiny", 0), ("tiny", 5), ("small", 2), ("c2", 0), ("c3", 1), ("c4", 0)])
+def test_extract_matches_oracle(fmx_mod, oracle, config, k):
+    import torch
+    scan, T, geo = synth.make_scan(config, k)
+    p = synth.default_params(geo)
+    ref = oracle.extract(scan.numpy(), p)
+    ctx = _ctx(fmx_mod, p)
+    ctx.extract(scan.to("cuda:0"), k)
+    got = ctx.extract_download(with_mask=True)
+    assert np.array_equal(got["planar_mask"], ref["planar_mask"])
+    ok = ref["normal_ok"]
+    assert np.array_equal(got["planar_index"], ref["sel"][ok])
+    assert np.array_equal(got["point_index"], ref["point_idx"])
+    s = scan.numpy()
+    assert np.array_equal(got["planar"][:, :3], s[ref["sel"][ok], :3])
+    assert np.array_equal(got["point"], s[ref["point_idx"], :3])
+    dots = np.abs(np.sum(got["planar"][:, 3:].astype(np.float64) * ref["normals"][ok], 1))
+    assert dots.min() >= 1 - 1e-6
+    # host-pointer path gives the same answer
+    ctx.extract(scan.numpy(), k)
+    got2 = ctx.extract_download()
+    assert np.array_equal(got2["planar_index"], got["planar_index"])
+    del torch
+
+
+def test_extract_edge_cases(fmx_mod, oracle):
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    ctx = _ctx(fmx_mod, p)
+    n = geo.rows * geo.cols
+    # all-invalid scan (every point at the origin): no features
+    z = np.zeros((n, 4), np.float32)
+    assert ctx.extract(z, 0)[:2] == (0, 0)
+    # size mismatch -> FMX_E_SIZE (the reference throws, extraction.tpp:141-145)
+    with pytest.raises(fmx_mod.FmxError) as e:
+        ctx.extract(np.zeros((n - 1, 4), np.float32), 0)
+    assert e.value.status == 2
+    # half the rows dropped
+    scan, _, _ = synth.make_scan("tiny", 3)
+    s = scan.numpy().copy()
+    s[: n // 2] = 0
+    ref = oracle.extract(s, p)
+    ctx.extract(s, 0)
+    got = ctx.extract_download()
+    assert np.array_equal(got["planar_index"], ref["sel"][ref["normal_ok"]])
+    assert np.array_equal(got["point_index"], ref["point_idx"])
+    # out-of-range points everywhere but a band
+    s2 = scan.numpy().copy()
+    s2[::3, :3] *= 500.0
+    ref = oracle.extract(s2, p)
+    ctx.extract(s2, 0)
+    got = ctx.extract_download()
+    assert np.array_equal(got["planar_index"], ref["sel"][ref["normal_ok"]])
+    assert np.array_equal(got["point_index"], ref["point_idx"])
+
+
+@pytest.mark.parametrize("config", ["tiny", "c2"])
+def test_match_matches_oracle(fmx_mod, oracle, config):
+    feats = stream_features(oracle, config, 6)
+    p = feats[0]["params"]
+    ctx = _ctx(fmx_mod, p)
+    w = 0.8
+    omaps = [oracle.VoxelMap(w, 0), oracle.VoxelMap(w, 1)]
+    scans, poses = [], []
+    for k in range(5):
+        f = feats[k]
+        ctx.keypoints_add(k, f["planar"], f["point"])
+        omaps[0].add_scan(k, f["pose"], f["planar"])
+        omaps[1].add_scan(k, f["pose"], f["point"])
+        scans.append(k)
+        poses.append(f["pose"])
+    ctx.map_build(scans, np.stack(poses), w)
+    q = feats[5]
+    ctx.set_queries(q["planar"], q["point"], 5)
+    Tj = perturb(q["pose"], np.random.default_rng(1), 0.005, 0.03)
+    cpl, cpt = ctx.match(Tj, w)
+    got = ctx.match_download()
+    npl = len(q["planar"])
+    for t, (om, Q) in enumerate(zip(omaps, (q["planar"], q["point"]))):
+        ref = om.match(Q, Tj)
+        sl = slice(0, npl) if t == 0 else slice(npl, None)
+        acc_ref = ref["found"] & (ref["d2"] < w * w)
+        pair = got["pair"][sl]
+        assert np.array_equal(pair >= 0, acc_ref)
+        assert np.array_equal(pair[acc_ref].astype(np.uint64), ref["scan"][acc_ref])
+        assert np.array_equal(got["d2"][sl][acc_ref], ref["d2"][acc_ref])
+        assert np.array_equal(got["pi"][sl][acc_ref], ref["pi"][acc_ref])
+        if t == 0:
+            assert np.array_equal(got["ni"][acc_ref], ref["ni"][acc_ref])
+        ins_ref = ~ref["found"] | (ref["d2"] > 0.01)
+        ins_got = got["d2"][sl] > 0.01
+        assert np.array_equal(ins_got, ins_ref)
+        counts = np.bincount(ref["scan"][acc_ref].astype(np.int64), minlength=5)
+        assert np.array_equal((cpl if t == 0 else cpt), counts)
+
+
+@pytest.mark.parametrize("single", [False, True])
+def test_linearize_matches_oracle(fmx_mod, oracle, single):
+    rng = np.random.default_rng(7 + int(single))
+    np_, ppi, pni, ppj, nt, tpi, tpj, Pi, Pj = random_corr(rng, 9)
+    p = synth.default_params(synth.GEOMETRIES["tiny"])
+    ctx = _ctx(fmx_mod, p)
+    ctx.corr_set(np_, ppi, pni, ppj, nt, tpi, tpj)
+    G, err = ctx.linearize(Pi, Pj, 0.1, single)
+    Gr, er = oracle.linearize(np_, ppi, pni, ppj, nt, tpi, tpj, Pi, Pj, 0.1, single)
+    scale = np.abs(Gr).max(axis=1, keepdims=True) + 1e-300
+    assert np.all(np.abs(G - Gr) <= 1e-10 * scale)
+    assert np.allclose(err, er, rtol=1e-10, atol=0)
+    e2 = ctx.error(Pi, Pj, 0.1)
+    assert np.allclose(e2, er, rtol=1e-10, atol=0)
+
+
+def test_register_stream_matches_oracle(fmx_mod, oracle):
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    world = synth.World()
+    ctx = _ctx(fmx_mod, p)
+    oest = oracle.Estimator(oracle.default_params(p))
+    for k in range(8):
+        s, T, _ = synth.make_scan("tiny", k, world=world)
+        ctx.register_scan(s.to("cuda:0"))
+        Tg = ctx.current_pose()
+        To, st, _ = oest.register_scan(s.numpy())
+        assert np.abs(Tg - To).max() < 1e-6, (k, np.abs(Tg - To).max())
