@@ -1,0 +1,200 @@
+"""bench.py — scan-to-submap registration throughput on MI355X (driver contract).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3]
+  (N > 1: launched by torch.distributed.run, one rank per GPU)
+
+A step = Estimator::register_scan of one synthetic organized scan (form/form.cpp:40-114):
+feature extraction, voxel-map build of the window keyscans, the ICP loop (match + LM
+whose linearizations and error evaluations run on the GPU) and map insertion.  Scans
+are ray-cast on the GPU before the timed region (inputs resident in HBM).  Multi-GPU:
+real scans do not shard, so every rank registers its own independent
+stream ("replicas only", weak scaling); value = all ranks' scans / max-over-ranks time.
+
+Prints ONE JSON line (rank 0) with the contract fields plus `roofline` (dominant
+kernel, HIP-event timed inside the timed region) and `cpu_baseline` (the C++ oracle
+on the host cores, bounded sample of the same stream).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from form_amd import fmx, synth  # noqa: E402
+
+METRIC = "scans/sec + Mpts/sec scan-to-submap ICP (128-beam); ATE delta vs reference"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c4", choices=["c2", "c3", "c4"])
+    ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
+    return ap.parse_args()
+
+
+def dist_setup(n):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world, local):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world, local):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_baseline(scans_host, params, budget_s):
+    """Oracle register_scan on the host cores over the first scans of the same stream."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as O  # CPU baseline only (test infrastructure)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    est = O.Estimator(O.default_params(params), threads)
+    times = []
+    t_all = time.perf_counter()
+    for s in scans_host:
+        t0 = time.perf_counter()
+        est.register_scan(s)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_all > budget_s:
+            break
+    # steady state: skip the first (empty-map) scan when there is more than one
+    steady = times[1:] if len(times) > 2 else times
+    per = float(np.median(steady))
+    return dict(value=1.0 / per, unit="scans/s", cores=threads, kind="port",
+                sample=f"oracle register_scan (C++ restatement, std::thread at the reference's two TBB sites) "
+                       f"over the first {len(times)} scans of the same synthetic stream; median of "
+                       f"{len(steady)} steady-state scans = {per * 1e3:.1f} ms/scan",
+                ms_per_scan=per * 1e3)
+
+
+def main():
+    a = parse()
+    rank, world, local = dist_setup(a.gpus)
+    dev = f"cuda:{local}"
+    torch.cuda.set_device(local)
+    geo = synth.GEOMETRIES[a.workload]
+    params = synth.default_params(geo)
+    n_pts = geo.rows * geo.cols
+    # independent stream per rank (replicas): different trajectory phase
+    world_obj = synth.World()
+    k0 = 1000 * rank
+    total = a.warmup + a.steps
+    scans = [synth.raycast(world_obj, synth.trajectory_pose(k0 + k), geo, synth.SEED + 7919 * (k0 + k + 1), dev)
+             for k in range(total)]
+    torch.cuda.synchronize()
+    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params)), device=local)
+    for k in range(a.warmup):
+        ctx.register_scan(scans[k])
+    ctx.sync()
+    ctx.profile(True)
+    ctx.profile_reset()
+    stats = []
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.warmup, total):
+        ctx.register_scan(scans[k])
+        stats.append(ctx.last_stats())
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier(world)
+    t_local = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    t_max = max_over_ranks(t_local, world, local)
+    scans_total = sum_over_ranks(float(a.steps), world, local)
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    value = scans_total / t_max
+    ms_per_step = t_max / a.steps * 1e3
+    # dominant kernel by device time in the timed region
+    dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    name, d = dom
+    avg_ms = d["ms"] / max(d["launches"], 1)
+    bytes_per = d["bytes"] / max(d["launches"], 1)
+    achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    try:
+        with open(a.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("workload") == a.workload and name in tj.get("kernels", {}):
+            traffic = tj["kernels"][name]["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+    roof = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, avg_launch_us=round(avg_ms * 1e3, 3),
+                alg_bytes_per_launch=bytes_per)
+    st_mean = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "scans/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 points / fp64 map, residuals and normal equations",
+        "data": "synthetic (ray-cast organized scans, seed 0x464F524D; no datasets offline)",
+        "config": {"workload": f"{a.workload}: {geo.rows}x{geo.cols} organized scan stream ({n_pts} pts/scan), "
+                               "register_scan single-pose mode",
+                   "points_per_scan": n_pts, "parallelism": f"replicas x{world}"},
+        "mpts_per_s": round(value * n_pts / 1e6, 3),
+        "roofline": roof,
+        "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 4) for k, v in prof.items()},
+        "counters": st_mean,
+    }
+    if not a.no_cpu_baseline and world == 1:
+        host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
+        out["cpu_baseline"] = cpu_baseline(host, params, a.cpu_sample_s)
+    print(json.dumps(out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

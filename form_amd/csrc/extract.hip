@@ -76,7 +76,8 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
   float4* pts = reinterpret_cast<float4*>(smem);
   float* curv = reinterpret_cast<float*>(pts + C);
   int* list = reinterpret_cast<int*>(curv + C);
-  uint8_t* flg = reinterpret_cast<uint8_t*>(list + C);  // bit0 point-valid, bit1 out-of-range, bit2 planar-valid
+  int* rk = list + C;                                      // ranks of accepted planar points
+  uint8_t* flg = reinterpret_cast<uint8_t*>(rk + C);  // bit0 point-valid, bit1 out-of-range, bit2 planar-valid
   uint8_t* used = flg + C;                               // used_points (planar) then point mask
   uint8_t* state = used + C;
   uint8_t* win = state + C;
@@ -185,10 +186,15 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     __syncthreads();
     const int n_acc = s_cnt;
     const int keep = n_acc < a.P + 1 ? n_acc : a.P + 1;
+    for (int i = tid; i < n_acc; i += kRowThreads) rk[i] = 0;
+    __syncthreads();
+    for (int idx = tid; idx < n_acc * n_acc; idx += kRowThreads) {  // rank by pair counting
+      const int i = idx / n_acc, j = idx - i * n_acc;
+      if (key_less(curv, list[j], list[i])) atomicAdd(&rk[i], 1);
+    }
+    __syncthreads();
     for (int i = tid; i < n_acc; i += kRowThreads) {
-      const int c = list[i];
-      int rank = 0;
-      for (int j = 0; j < n_acc; ++j) rank += key_less(curv, list[j], c) ? 1 : 0;
+      const int c = list[i], rank = rk[i];
       if (rank < keep) {
         sel_slots[(size_t)r * a.cap_pl + pl_count + rank] = (uint32_t)c;
         state[c] = 4;
@@ -219,12 +225,15 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     const int b = s * pps;
     const int e = (s == a.S - 1) ? C : b + pps;
     const int nu = block_compact(b, e, [&](int c) { return win[c] != 0; }, list, ws);
-    if (tid == 0) {
-      // extract_point (:360-399), literal: factor passes with the per-offset break
-      int nf = 0;
-      if (a.Ppt > 0) {
-        const int factor = 1 + nu / a.Ppt;
-        for (int off = 0; off < factor; ++off) {
+    if (tid < kWave) {
+      // extract_point (:360-399).  Phase A, literal, lane 0: passes off = 0, 1, ...
+      // over U[off], U[off+factor], ... until the (Ppt+1)-th accept; the break at
+      // :395-396 then leaves exactly one element, U[off], per later pass (phase B).
+      int nf = 0, offA = 0;
+      bool stopA = false;
+      const int factor = a.Ppt > 0 ? 1 + nu / a.Ppt : 0;
+      if (tid == 0 && a.Ppt > 0) {
+        for (int off = 0; off < factor && !stopA; ++off) {
           for (int ui = off; ui < nu; ui += factor) {
             const int c = list[ui];
             if (win[c]) {
@@ -235,11 +244,57 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
               }
               nf++;
             }
-            if (nf > a.Ppt) break;
+            if (nf > a.Ppt) {
+              stopA = true;
+              offA = off;
+              break;
+            }
           }
         }
       }
-      s_cnt = pt_count + nf;
+      nf = __shfl(nf, 0, 64);
+      stopA = __shfl((int)stopA, 0, 64) != 0;
+      offA = __shfl(offA, 0, 64);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (stopA) {
+        // Phase B: heads U[o], o = offA+1 .. factor-1, are consecutive in U (column
+        // order).  A head is taken iff still eligible after phase A (win[]) and more
+        // than k-1 columns past the last taken head: a 1-D greedy scanned from
+        // registers, 64 heads per chunk, state kept wave-uniform.
+        int last = -0x40000000;
+        for (int o0 = offA + 1; o0 < factor; o0 += kWave) {
+          const int o = o0 + tid;
+          const int c = o < factor ? list[o] : 0x7FFFFFFF;
+          const int el = o < factor ? (int)win[c] : 0;
+          const int nl = min(kWave, factor - o0);
+          for (int l = 0; l < nl; ++l) {
+            const int cl = __builtin_amdgcn_readlane(c, l);
+            const int ell = __builtin_amdgcn_readlane(el, l);
+            if (ell && cl > last + (k - 1)) {
+              if (tid == 0) pt_slots[(size_t)r * a.cap_pt + pt_count + nf] = (uint32_t)cl;
+              last = cl;
+              nf++;
+            }
+          }
+        }
+        // suppression of the phase-B heads (spills into the next sector, :388-391)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (tid == 0) s_cnt = pt_count + nf;
+    }
+    __syncthreads();
+    // apply phase-B suppression from the written slots (phase A already applied)
+    {
+      const int n0 = pt_count, n1 = s_cnt;
+      for (int i = n0 + tid; i < n1; i += kRowThreads) {
+        const int c = (int)pt_slots[(size_t)r * a.cap_pt + i];
+        for (int n = 0; n < k; ++n) {
+          win[c + n] = 0;
+          win[c - n] = 0;
+        }
+      }
     }
     __syncthreads();
     pt_count = s_cnt;
@@ -251,17 +306,55 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
   }
 }
 
+// Per-row 64-column block AABBs of the planar-valid points (one wave per block),
+// used to prune find_closest exactly.  Empty block: lo = +inf, hi = -inf.
+__global__ __launch_bounds__(256) void k_row_blocks(const float4* __restrict__ scan,
+                                                    const uint8_t* __restrict__ mask, int R, int C,
+                                                    float4* __restrict__ blo, float4* __restrict__ bhi) {
+  const int nblk = (C + kWave - 1) / kWave;
+  const int wv = blockIdx.x * 4 + threadIdx.x / kWave;
+  if (wv >= R * nblk) return;
+  const int r = wv / nblk, bk = wv % nblk;
+  const int j = bk * kWave + lane_id();
+  float lx = INFINITY, ly = INFINITY, lz = INFINITY, hx = -INFINITY, hy = -INFINITY, hz = -INFINITY;
+  if (j < C && mask[(size_t)r * C + j]) {
+    const float4 p = scan[(size_t)r * C + j];
+    lx = hx = p.x;
+    ly = hy = p.y;
+    lz = hz = p.z;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lx = fminf(lx, __shfl_xor(lx, o, 64));
+    ly = fminf(ly, __shfl_xor(ly, o, 64));
+    lz = fminf(lz, __shfl_xor(lz, o, 64));
+    hx = fmaxf(hx, __shfl_xor(hx, o, 64));
+    hy = fmaxf(hy, __shfl_xor(hy, o, 64));
+    hz = fmaxf(hz, __shfl_xor(hz, o, 64));
+  }
+  if (lane_id() == 0) {
+    blo[wv] = make_float4(lx, ly, lz, 0.f);
+    bhi[wv] = make_float4(hx, hy, hz, 0.f);
+  }
+}
+
 // find_closest (extraction.tpp:402-420) over rows r-1 and r+1: one wave per slot.
+// Exact argmin with the reference's semantics (float distance promoted to double,
+// strict <, first index on ties): the block holding the query's own column is
+// scanned first, then only blocks whose box lower bound, shrunk by 1e-5 relative
+// (>> the few-ulp error of the fp32 distance), does not exceed the running best.
 __global__ __launch_bounds__(256) void k_closest(const float4* __restrict__ scan,
                                                  const uint8_t* __restrict__ mask,
                                                  const uint32_t* __restrict__ sel_slots,
                                                  const uint32_t* __restrict__ row_counts, int R, int C,
-                                                 int cap, int2* __restrict__ closest) {
+                                                 int cap, const float4* __restrict__ blo,
+                                                 const float4* __restrict__ bhi, int2* __restrict__ closest) {
   const int wv = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
   const int r = wv / cap, slot = wv % cap;
   if (r >= R) return;
   if ((uint32_t)slot >= row_counts[2 * r]) return;
   const int lane = lane_id();
+  const int nblk = (C + kWave - 1) / kWave;
   const int c = (int)sel_slots[(size_t)r * cap + slot];
   const float4 p = scan[(size_t)r * C + c];
   int res[2];
@@ -273,23 +366,52 @@ __global__ __launch_bounds__(256) void k_closest(const float4* __restrict__ scan
     const uint8_t* mrow = mask + (size_t)rr * C;
     float best = 0.f;
     int bj = -1;
-    for (int j = lane; j < C; j += kWave) {
-      if (!mrow[j]) continue;
-      const float d = dist2f(row[j], p);
-      // reference: double(d) < min_dist2 (init DBL_MAX), so only finite d qualify
-      if (d <= FLT_MAX && (bj < 0 || d < best)) {
-        best = d;
-        bj = j;
+    auto scan_block = [&](int bk) {
+      const int j = bk * kWave + lane;
+      float d = 0.f;
+      int dj = -1;
+      if (j < C && mrow[j]) {
+        d = dist2f(row[j], p);
+        if (d <= FLT_MAX) dj = j;  // reference: double(d) < DBL_MAX
       }
-    }
-    // lexicographic (found, d, j) wave argmin
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oj = __shfl_xor(bj, o, 64);
-      if (oj >= 0 && (bj < 0 || ob < best || (ob == best && oj < bj))) {
-        best = ob;
-        bj = oj;
+      for (int o = 32; o > 0; o >>= 1) {
+        const float od = __shfl_xor(d, o, 64);
+        const int oj = __shfl_xor(dj, o, 64);
+        if (oj >= 0 && (dj < 0 || od < d || (od == d && oj < dj))) {
+          d = od;
+          dj = oj;
+        }
+      }
+      if (dj >= 0 && (bj < 0 || d < best || (d == best && dj < bj))) {
+        best = d;
+        bj = dj;
+      }
+    };
+    const int own = c / kWave;
+    scan_block(own);
+    // lane l owns block l (and l + 64, ... for very wide rows)
+    for (int b0 = 0; b0 < nblk; b0 += kWave) {
+      const int bk = b0 + lane;
+      double lb = INFINITY;
+      if (bk < nblk && bk != own) {
+        const float4 lo = blo[(size_t)rr * nblk + bk], hi = bhi[(size_t)rr * nblk + bk];
+        if (lo.x <= hi.x) {  // non-empty
+          const double qx = p.x, qy = p.y, qz = p.z;
+          const double ex = fmax(fmax((double)lo.x - qx, qx - (double)hi.x), 0.0);
+          const double ey = fmax(fmax((double)lo.y - qy, qy - (double)hi.y), 0.0);
+          const double ez = fmax(fmax((double)lo.z - qz, qz - (double)hi.z), 0.0);
+          lb = (ex * ex + ey * ey + ez * ez) * (1.0 - 1e-5);
+        }
+      }
+      uint64_t cand = __ballot(bk < nblk && bk != own && lb < INFINITY && (bj < 0 || lb <= (double)best));
+      while (cand) {
+        const int l = __ffsll((unsigned long long)cand) - 1;
+        cand &= cand - 1;
+        // re-check against the (possibly improved) best before scanning
+        const double lbl = __shfl(lb, l, 64);
+        if (bj >= 0 && lbl > (double)best) continue;
+        scan_block(b0 + l);
       }
     }
     res[dir] = bj < 0 ? -1 : rr * C + bj;
@@ -350,16 +472,29 @@ __device__ void smallest_eigvec(const float cov[3][3], double n[3]) {
 }
 
 // compute_normal (extraction.tpp:263-329): one lane per selected planar point.
+__device__ int fit_one(const float4* __restrict__ scan, const uint32_t* __restrict__ sel_slots,
+                       const int2* __restrict__ closest, const ExArgs& a, float4* __restrict__ nrm_slots,
+                       int r, int slot);
+
+// Block (r, part): slots part*blockDim .. of row r; the row's found-normal count is
+// a block count (__syncthreads_count) + one atomic per block.
 __global__ __launch_bounds__(256) void k_fit(const float4* __restrict__ scan,
                                              const uint32_t* __restrict__ sel_slots,
                                              const uint32_t* __restrict__ row_counts,
                                              const int2* __restrict__ closest, ExArgs a,
                                              float4* __restrict__ nrm_slots,
                                              uint32_t* __restrict__ row_ok) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  const int r = g / a.cap_pl, slot = g % a.cap_pl;
-  if (r >= a.R) return;
-  if ((uint32_t)slot >= row_counts[2 * r]) return;
+  const int r = blockIdx.y;
+  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = (uint32_t)slot < row_counts[2 * r];
+  const int found = active ? fit_one(scan, sel_slots, closest, a, nrm_slots, r, slot) : 0;
+  const int nfound = __syncthreads_count(found);
+  if (threadIdx.x == 0 && nfound) atomicAdd(&row_ok[r], (uint32_t)nfound);
+}
+
+__device__ int fit_one(const float4* __restrict__ scan, const uint32_t* __restrict__ sel_slots,
+                       const int2* __restrict__ closest, const ExArgs& a, float4* __restrict__ nrm_slots,
+                       int r, int slot) {
   const int C = a.C, k = a.k;
   const size_t idx = (size_t)r * C + sel_slots[(size_t)r * a.cap_pl + slot];
   const float4 p = scan[idx];
@@ -413,9 +548,9 @@ __global__ __launch_bounds__(256) void k_fit(const float4* __restrict__ scan,
       n[2] = -n[2];
     }
     out = make_float4((float)n[0], (float)n[1], (float)n[2], 1.0f);  // w = 1: normal found
-    atomicAdd(&row_ok[r], 1u);
   }
   nrm_slots[(size_t)r * a.cap_pl + slot] = out;
+  return out.w != 0.f ? 1 : 0;
 }
 
 // per-row offsets of {planar with normal, points, planar selected}: one block
@@ -526,10 +661,10 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   c->h_u32.ensure(8);
   c->rows = R;
   c->cols = C;
-  const size_t lds = (size_t)C * (16 + 4 + 4 + 4);
+  const size_t lds = (size_t)C * (16 + 4 + 4 + 4 + 4);
   if (!c->lds_attr_set) {
     FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extract_rows),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * (16 + 4 + 4 + 4)));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * (16 + 4 + 4 + 4 + 4)));
     c->lds_attr_set = true;
   }
   {
@@ -540,14 +675,19 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   FMX_HIP(hipGetLastError());
   FMX_HIP(hipMemsetAsync(c->row_ok.p, 0, R * sizeof(uint32_t), st));
   const int nslots = R * a.cap_pl;
+  const int nblk = (C + 63) / 64;
+  c->blk_lo.ensure((size_t)R * nblk);
+  c->blk_hi.ensure((size_t)R * nblk);
   {
-    ProfScope ps(c->prof, PROF_CLOSEST, 0.0, st);
+    ProfScope ps(c->prof, PROF_CLOSEST, 16.0 * N + N + 8.0 * nslots, st);
+    hipLaunchKernelGGL(k_row_blocks, dim3((R * nblk + 3) / 4), dim3(256), 0, st, d_scan, c->planar_mask.p, R, C,
+                       c->blk_lo.p, c->blk_hi.p);
     hipLaunchKernelGGL(k_closest, dim3((nslots + 3) / 4), dim3(256), 0, st, d_scan, c->planar_mask.p,
-                       c->sel_slots.p, c->row_counts.p, R, C, a.cap_pl, c->closest.p);
+                       c->sel_slots.p, c->row_counts.p, R, C, a.cap_pl, c->blk_lo.p, c->blk_hi.p, c->closest.p);
   }
   {
     ProfScope ps(c->prof, PROF_FIT, 0.0, st);
-    hipLaunchKernelGGL(k_fit, dim3((nslots + 255) / 256), dim3(256), 0, st, d_scan, c->sel_slots.p,
+    hipLaunchKernelGGL(k_fit, dim3((a.cap_pl + 255) / 256, R), dim3(256), 0, st, d_scan, c->sel_slots.p,
                        c->row_counts.p, c->closest.p, a, c->nrm_slots.p, c->row_ok.p);
   }
   {

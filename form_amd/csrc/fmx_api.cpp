@@ -20,7 +20,7 @@ using namespace fmx;
 // ============================================================================ profiling
 namespace fmx {
 static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest", "fit",      "compact",   "map_build",
-                                             "match",        "pair_sort", "linearize", "error_eval", "insert"};
+                                             "match",        "pair_sort", "linearize", "lin_final", "error_eval", "insert"};
 
 ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), bytes(by), st(s) {
   if (!pr.on) return;
@@ -417,14 +417,19 @@ Pose predict_next(const fmx_ctx::Est& e) {
 }
 
 // Single-pose LM on X(j), map poses fixed (disable_smoothing, constraints.cpp:103-111,
-// 235-250) with GTSAM LevenbergMarquardtOptimizer defaults; the linearization and
-// error evaluations run on the device (fmx stage 3, 7x7 layout).
+// 235-250) with GTSAM LevenbergMarquardtOptimizer defaults.  Linearizations run on
+// the device (fmx stage 3, 7x7 layout).  Every trial pose is evaluated with a full
+// linearization: it returns the error the accept test needs AND, if the step is
+// accepted, the next iteration's system — one device round trip per trial, and the
+// arithmetic is identical to evaluating the error alone.
 struct DeviceLM {
   fmx_ctx* c;
   fmx_ctx::Est& e;
   double sigma;
   double lambda = 1e-5;
   int linearizations = 0;
+  // cached linearization
+  double Hs[6][6], g[6], cc, err;
   void fill(const Pose& Tj) {
     const uint32_t K = c->K;
     e.poses_i.resize(12 * (size_t)K);
@@ -434,23 +439,21 @@ struct DeviceLM {
       std::memcpy(&e.poses_j[12 * k], Tj.m, 12 * sizeof(double));
     }
   }
-  double error_at(const Pose& Tj) {
-    if (c->K == 0) return 0.0;
-    fill(Tj);
-    e.err.resize(c->K);
-    run_linearize(c, e.poses_i.data(), e.poses_j.data(), sigma, 2, nullptr, e.err.data());
-    double s = 0;
-    for (uint32_t k = 0; k < c->K; ++k) s += e.err[k];
-    return s;
-  }
-  void iterate(Pose& T, double& err) {
+  // linearize at Tj into (H, g, c, err); returns err
+  double linearize(const Pose& Tj, double H[6][6], double gg[6], double& c2) {
     const uint32_t K = c->K;
-    fill(T);
+    for (int i = 0; i < 6; ++i) {
+      gg[i] = 0;
+      for (int j = 0; j < 6; ++j) H[i][j] = 0;
+    }
+    c2 = 0;
+    if (K == 0) return 0.0;
+    fill(Tj);
     e.G.resize(28 * (size_t)K);
     e.err.resize(K);
     run_linearize(c, e.poses_i.data(), e.poses_j.data(), sigma, 1, e.G.data(), e.err.data());
     ++linearizations;
-    double Hs[6][6] = {}, g[6] = {}, cc = 0;
+    double er = 0;
     for (uint32_t k = 0; k < K; ++k) {
       const double* Gk = &e.G[28 * (size_t)k];
       double full[7][7];
@@ -458,13 +461,18 @@ struct DeviceLM {
       for (int i = 0; i < 7; ++i)
         for (int j = i; j < 7; ++j) full[i][j] = full[j][i] = Gk[o++];
       for (int i = 0; i < 6; ++i) {
-        for (int j = 0; j < 6; ++j) Hs[i][j] += full[i][j];
-        g[i] += full[i][6];
+        for (int j = 0; j < 6; ++j) H[i][j] += full[i][j];
+        gg[i] += full[i][6];
       }
-      cc += full[6][6];
+      c2 += full[6][6];
+      er += e.err[k];
     }
+    return er;
+  }
+  // one LevenbergMarquardtOptimizer::iterate() from the cached system at T
+  void iterate(Pose& T) {
     const double oldLin = 0.5 * cc;
-    for (;;) {  // LevenbergMarquardtOptimizer::tryLambda
+    for (;;) {  // tryLambda
       double Hd[6][6];
       for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) Hd[i][j] = Hs[i][j] + (i == j ? lambda : 0.0);
@@ -472,7 +480,7 @@ struct DeviceLM {
       const bool ok = chol_solve6(Hd, g, dx);
       bool success = false, stop = false;
       Pose Tn = T;
-      double nerr = err;
+      double nerr = err, nH[6][6], ng[6], ncc = 0;
       if (ok) {
         double dHd = 0, dg = 0;
         for (int i = 0; i < 6; ++i) {
@@ -485,7 +493,7 @@ struct DeviceLM {
         const double linChange = oldLin - newLin;
         if (linChange >= 0) {
           Tn = compose(T, expmap(dx));
-          nerr = error_at(Tn);
+          nerr = linearize(Tn, nH, ng, ncc);
           const double costChange = err - nerr;
           if (linChange > DBL_EPSILON * oldLin) success = (costChange / linChange) > 1e-3;
           else success = true;
@@ -496,6 +504,9 @@ struct DeviceLM {
         lambda = std::max(0.0, lambda / 10.0);
         T = Tn;
         err = nerr;
+        std::memcpy(Hs, nH, sizeof(Hs));
+        std::memcpy(g, ng, sizeof(g));
+        cc = ncc;
         return;
       } else if (!stop) {
         lambda *= 10.0;
@@ -506,8 +517,9 @@ struct DeviceLM {
     }
   }
   Pose optimize(const Pose& T0, int* iters) {  // NonlinearOptimizer::defaultOptimize
+    lambda = 1e-5;
     Pose T = T0;
-    double err = error_at(T);
+    err = linearize(T, Hs, g, cc);
     int it = 0;
     if (err <= 0.0) {
       *iters = 0;
@@ -517,7 +529,7 @@ struct DeviceLM {
     bool conv;
     do {
       cur = newErr;
-      iterate(T, err);
+      iterate(T);
       ++it;
       newErr = err;
       if (newErr <= 0.0) conv = true;
@@ -579,11 +591,12 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   // ICP loop (form.cpp:67-89)
   DeviceLM lm{c, e, P.planar_constraint_sigma};
   uint64_t icp = 0, lm_it = 0;
+  bool converged = false;
+  Pose last_after = e.values.at(j);
   for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
     ++icp;
     const Pose before = e.values.at(j);
     run_match(c, before.m, P.max_dist_matching, P.min_dist_map);
-    lm.lambda = 1e-5;
     int li = 0;
     const Pose after = lm.optimize(before, &li);
     lm_it += li;
@@ -591,15 +604,25 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     logmap(compose(inverse(before), after), xi);
     double dn = 0;
     for (double x : xi) dn += x * x;
-    if (std::sqrt(dn) < P.new_pose_threshold) break;
+    if (std::sqrt(dn) < P.new_pose_threshold) {
+      converged = true;
+      last_after = after;
+      break;
+    }
     e.values[j] = after;  // update_current_pose
   }
-  {  // optimize(false) + update_values (form.cpp:92-93)
-    lm.lambda = 1e-5;
+  // optimize(false) + update_values (form.cpp:92-93).  In the single-pose mode the
+  // graph is the same current-scan factor set (get_single_graph ignores `fast`), so
+  // after a converged break it restarts from `before` with the same data and
+  // returns `after` again, bit for bit: reuse it.  Otherwise run it.
+  if (converged) {
+    e.values[j] = last_after;
+  } else {
     int li = 0;
     e.values[j] = lm.optimize(e.values.at(j), &li);
     lm_it += li;
   }
+  match_counts_fetch(c);
   uint64_t mpl = 0, mpt = 0;
   for (uint32_t k = 0; k < c->K; ++k) {
     cj[c->map_scans[k]] = {c->cnt_pl[k], c->cnt_pt[k]};
@@ -800,6 +823,7 @@ fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint3
     if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
     if (!(max_dist > 0)) throw StatusError(FMX_E_INVAL, "max_dist must be > 0");
     run_match(c, pose_j, max_dist, c->P.min_dist_map);
+    match_counts_fetch(c);
     c->h_u32.ensure(8);
     FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->map_err.p, 4, hipMemcpyDeviceToHost, c->stream));
     FMX_HIP(hipStreamSynchronize(c->stream));

@@ -74,6 +74,7 @@ enum ProfId {
   PROF_MATCH,
   PROF_PAIR_SORT,
   PROF_LINEARIZE,
+  PROF_LIN_FINAL,
   PROF_ERROR,
   PROF_INSERT,
   PROF_COUNT
@@ -149,7 +150,7 @@ struct fmx_ctx {
   fmx::DBuf<uint8_t> planar_mask;
   fmx::DBuf<uint32_t> sel_slots, pt_slots, row_counts, row_ok, row_off;
   fmx::DBuf<int2> closest;
-  fmx::DBuf<float4> nrm_slots;
+  fmx::DBuf<float4> nrm_slots, blk_lo, blk_hi;
   fmx::DBuf<uint32_t> scan_scratch, dev_u32;  // dev_u32: small device scalars
   fmx::HBuf<uint32_t> h_u32;
   int rows = 0, cols = 0;
@@ -195,6 +196,12 @@ struct fmx_ctx {
   std::vector<uint32_t> cnt_pl, cnt_pt;         // per pair, host copy after match
   fmx::HBuf<double> h_corr;
   fmx::HBuf<uint32_t> h_meta, h_counts;
+  fmx::DBuf<uint32_t> pair_base;                // [2][K] first row of each pair
+  fmx::DBuf<uint32_t> work;                     // match work counters per block (probes, candidates)
+  fmx::HBuf<uint32_t> h_work;
+  uint32_t work_blocks = 0;
+  double last_probes = 0, last_cands = 0;
+  bool counts_pending = false;
   bool lds_attr_set = false;
 
   // ---- linearize
@@ -214,10 +221,11 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w);
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map);
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
+void match_counts_fetch(fmx_ctx* c);
 void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
                    double* G_out, double* err_out);
 void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
                  const double* ppj, const uint32_t* nt, const double* tpi, const double* tpj);
-constexpr int kPlaneChunk = 1024;  // plane rows per linearize chunk
-constexpr int kPointChunk = 512;   // point pairs per linearize chunk
+constexpr int kPlaneChunk = 64;  // plane rows per linearize chunk (one wave, one row per lane)
+constexpr int kPointChunk = 64;  // point pairs per linearize chunk (three rows per lane)
 }  // namespace fmx

@@ -25,7 +25,7 @@
 namespace fmx {
 namespace {
 
-constexpr int kLinThreads = 256;
+constexpr int kLinThreads = 64;
 
 template <int MODE>
 struct LinShape;
@@ -128,15 +128,16 @@ __device__ __forceinline__ void point_row(const double* Ti, const double* Tj, co
   }
 }
 
+// One wave per chunk (<= 64 plane rows or <= 64 point pairs of one pair), one row
+// (or point pair) per lane; the wave's NG sums go to partials[NG][max_chunks].
 template <int MODE>
 __global__ __launch_bounds__(kLinThreads) void k_linearize(const Chunk* __restrict__ chunks,
                                                            const uint32_t* __restrict__ n_chunks,
                                                            const double* __restrict__ c_pl, size_t ld_pl,
                                                            const double* __restrict__ c_pt, size_t ld_pt,
                                                            const double* __restrict__ poses, double inv,
-                                                           double* __restrict__ partials) {
+                                                           double* __restrict__ partials, size_t ldp) {
   constexpr int NG = LinShape<MODE>::NG;
-  __shared__ double s_red[kLinThreads / kWave][NG];
   const uint32_t ch = blockIdx.x;
   if (ch >= *n_chunks) return;
   const Chunk d = chunks[ch];
@@ -148,17 +149,16 @@ __global__ __launch_bounds__(kLinThreads) void k_linearize(const Chunk* __restri
   double H[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) H[i] = 0.0;
-  if (d.type == 0) {
-    for (uint32_t row = d.begin + threadIdx.x; row < d.end; row += kLinThreads) {
+  const uint32_t row = d.begin + threadIdx.x;
+  if (row < d.end) {
+    if (d.type == 0) {
       const double pi[3] = {c_pl[row], c_pl[ld_pl + row], c_pl[2 * ld_pl + row]};
       const double ni[3] = {c_pl[3 * ld_pl + row], c_pl[4 * ld_pl + row], c_pl[5 * ld_pl + row]};
       const double pj[3] = {c_pl[6 * ld_pl + row], c_pl[7 * ld_pl + row], c_pl[8 * ld_pl + row]};
       double r;
       plane_row<MODE>(Ti, Tj, pi, ni, pj, r, H);
       accum_row<MODE>(H, r, inv, acc);
-    }
-  } else {
-    for (uint32_t row = d.begin + threadIdx.x; row < d.end; row += kLinThreads) {
+    } else {
       const double pi[3] = {c_pt[row], c_pt[ld_pt + row], c_pt[2 * ld_pt + row]};
       const double pj[3] = {c_pt[3 * ld_pt + row], c_pt[4 * ld_pt + row], c_pt[5 * ld_pt + row]};
       double wpi[3], wpj[3];
@@ -172,27 +172,37 @@ __global__ __launch_bounds__(kLinThreads) void k_linearize(const Chunk* __restri
       }
     }
   }
-  const int w = threadIdx.x / kWave;
+  // butterfly sums: every lane ends with every total; lane i keeps entry i (and i+64)
+  double mine0 = 0.0, mine1 = 0.0;
+  const int lane = lane_id();
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
     const double s = wave_sum(acc[i]);
-    if (lane_id() == 0) s_red[w][i] = s;
+    if (i < 64) {
+      if (lane == i) mine0 = s;
+    } else {
+      if (lane == i - 64) mine1 = s;
+    }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < NG; i += kLinThreads)
-    partials[(size_t)ch * NG + i] = ((s_red[0][i] + s_red[1][i]) + s_red[2][i]) + s_red[3][i];
+  if (lane < NG) partials[(size_t)lane * ldp + ch] = mine0;
+  if (lane + 64 < NG) partials[(size_t)(lane + 64) * ldp + ch] = mine1;
 }
 
+// One wave per (pair k, entry i): sum the pair's chunk partials (lane-strided, in
+// a fixed order, then a fixed butterfly) -> G[k][i]; err[k] = 0.5 * G[k][last].
 template <int MODE>
-__global__ __launch_bounds__(128) void k_lin_final(const uint32_t* __restrict__ chunk_range,
-                                                   const double* __restrict__ partials, double* __restrict__ G,
-                                                   double* __restrict__ err, int K) {
+__global__ __launch_bounds__(256) void k_lin_final(const uint32_t* __restrict__ chunk_range,
+                                                   const double* __restrict__ partials, size_t ldp,
+                                                   double* __restrict__ G, double* __restrict__ err, int K) {
   constexpr int NG = LinShape<MODE>::NG;
-  const int k = blockIdx.x;
+  const int item = blockIdx.x * 4 + threadIdx.x / kWave;
+  if (item >= K * NG) return;
+  const int k = item / NG, i = item % NG;
   const uint32_t b = chunk_range[k], e = chunk_range[k + 1];
-  for (int i = threadIdx.x; i < NG; i += 128) {
-    double s = 0.0;
-    for (uint32_t c = b; c < e; ++c) s += partials[(size_t)c * NG + i];
+  double s = 0.0;
+  for (uint32_t c = b + lane_id(); c < e; c += kWave) s += partials[(size_t)i * ldp + c];
+  s = wave_sum(s);
+  if (lane_id() == 0) {
     if constexpr (MODE == 2) {
       err[k] = 0.5 * s;
     } else {
@@ -218,37 +228,44 @@ void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34,
   }
   c->poses_ij.ensure(24 * (size_t)K);
   FMX_HIP(hipMemcpyAsync(c->poses_ij.p, c->h_poses.p, 24 * K * sizeof(double), hipMemcpyHostToDevice, st));
-  c->partials.ensure((size_t)c->max_chunks * 91 + 1);
+  c->partials.ensure((size_t)std::max<uint32_t>(c->max_chunks, 1) * 91 + 1);
   c->G.ensure((size_t)K * 92 + 1);
   double* dG = c->G.p;
-  double* dErr = c->G.p + (size_t)K * NG;
+  double* dErr = mode == 2 ? dG : dG + (size_t)K * NG;  // error-only: err is the whole output
   const double inv = 1.0 / sigma;  // FastIsotropic invsigma_ (gtsam.hpp:96)
   const uint32_t nb = std::max<uint32_t>(c->max_chunks, 1);
+  const size_t ldp = nb;
+  if (c->counts_pending && c->prof.on) match_counts_fetch(c);  // exact byte model for the profile
   const double bytes = 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * NG * K;
+  const int nfin = (K * NG + 3) / 4;
   {
     ProfScope ps(c->prof, mode == 2 ? PROF_ERROR : PROF_LINEARIZE, bytes, st);
     if (mode == 0)
       hipLaunchKernelGGL(k_linearize<0>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p);
+                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p, ldp);
     else if (mode == 1)
       hipLaunchKernelGGL(k_linearize<1>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p);
+                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p, ldp);
     else
       hipLaunchKernelGGL(k_linearize<2>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p);
+                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p, ldp);
     FMX_HIP(hipGetLastError());
+  }
+  {
+    ProfScope ps(c->prof, PROF_LIN_FINAL, 8.0 * NG * (double)nb + 8.0 * NG * K, st);
     if (mode == 0)
-      hipLaunchKernelGGL(k_lin_final<0>, dim3(K), dim3(128), 0, st, c->chunk_range.p, c->partials.p, dG, dErr, K);
+      hipLaunchKernelGGL(k_lin_final<0>, dim3(nfin), dim3(256), 0, st, c->chunk_range.p, c->partials.p, ldp, dG, dErr, K);
     else if (mode == 1)
-      hipLaunchKernelGGL(k_lin_final<1>, dim3(K), dim3(128), 0, st, c->chunk_range.p, c->partials.p, dG, dErr, K);
+      hipLaunchKernelGGL(k_lin_final<1>, dim3(nfin), dim3(256), 0, st, c->chunk_range.p, c->partials.p, ldp, dG, dErr, K);
     else
-      hipLaunchKernelGGL(k_lin_final<2>, dim3(K), dim3(128), 0, st, c->chunk_range.p, c->partials.p, dG, dErr, K);
+      hipLaunchKernelGGL(k_lin_final<2>, dim3(nfin), dim3(256), 0, st, c->chunk_range.p, c->partials.p, ldp, dG, dErr, K);
     FMX_HIP(hipGetLastError());
   }
   const size_t nout = (size_t)K * (mode == 2 ? 1 : NG + 1);
   c->h_G.ensure(nout);
   FMX_HIP(hipMemcpyAsync(c->h_G.p, dG, nout * sizeof(double), hipMemcpyDeviceToHost, st));
   FMX_HIP(hipStreamSynchronize(st));
+  match_counts_fetch(c);  // already copied; no extra wait
   if (mode == 2) {
     if (err_out) std::memcpy(err_out, c->h_G.p, K * sizeof(double));
   } else {
@@ -320,6 +337,7 @@ void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, 
   c->max_chunks = std::max<uint32_t>(nch, 1);
   c->rows_pl = Np;
   c->rows_pt = Nt;
+  c->counts_pending = false;
   c->have_corr = true;
   c->have_match = false;
 }

@@ -31,8 +31,6 @@
 namespace fmx {
 namespace {
 
-constexpr int kMatchThreads = 256;
-
 __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
   int lo = 0, hi = K - 1;
   while (lo < hi) {
@@ -135,128 +133,234 @@ struct MatchArgs {
   int K;
 };
 
-// One lane per query; blocks [0, nb_pl) planar queries, the rest point queries.
+// kGroup lanes cooperate on one query: lane g of the group visits shifts
+// g, g+kGroup, ... (3-4 of the 27 voxels), then the group min-reduces
+// (d^2, build order).  ~8x the threads of a lane-per-query kernel: at per-scan
+// sizes (~4e4 queries) the chip would otherwise hold ~2 waves per CU and every
+// probe's latency would be exposed.
+constexpr int kGroup = 8;
+constexpr int kQPB = 64;                     // queries per block
+constexpr int kMatchThreads = kQPB * kGroup;  // 512
+
 __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
                                                          const float4* __restrict__ q_pt,
                                                          const double* __restrict__ inv_poses,
                                                          int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
                                                          double4* __restrict__ m_pi, double4* __restrict__ m_ni,
-                                                         uint8_t* __restrict__ m_ins, uint32_t* __restrict__ hist) {
+                                                         uint8_t* __restrict__ m_ins, uint32_t* __restrict__ hist,
+                                                         uint32_t* __restrict__ work) {
   extern __shared__ uint32_t s_hist[];  // [K]
   const bool planar = blockIdx.x < a.nb_pl;
-  const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kMatchThreads + threadIdx.x;
+  const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kQPB + threadIdx.x / kGroup;
+  const int g = threadIdx.x % kGroup;
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
   const MapView& M = planar ? mp : mt;
   for (int k = threadIdx.x; k < a.K; k += kMatchThreads) s_hist[k] = 0;
   __syncthreads();
+  uint32_t n_probe = 0, n_cand = 0;
   if (qi < nq) {
     const float4 lq = planar ? q_pl[qi] : q_pt[qi];
     double wq[3];
     d_xform(a.Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
     const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
-    // distances from the query to its voxel's faces (for the per-voxel lower bound)
+    // distances from the query to its voxel's faces (per-voxel lower bound)
     const double lo[3] = {wq[0] - bx * a.w, wq[1] - by * a.w, wq[2] - bz * a.w};
     const double hi[3] = {(bx + 1) * a.w - wq[0], (by + 1) * a.w - wq[1], (bz + 1) * a.w - wq[2]};
     double best = a.bound;
-    uint32_t best_rid = 0xFFFFFFFFu, best_i = 0;
-    bool found = false;
-    if (key_in_range(bx, by, bz)) {
-      for (int s = 0; s < 27; ++s) {
-        const int sx = c_shift[s][0], sy = c_shift[s][1], sz = c_shift[s][2];
-        double lb = 0.0;
-        {
-          const double ex = sx < 0 ? lo[0] : (sx > 0 ? hi[0] : 0.0);
-          const double ey = sy < 0 ? lo[1] : (sy > 0 ? hi[1] : 0.0);
-          const double ez = sz < 0 ? lo[2] : (sz > 0 ? hi[2] : 0.0);
-          const double mx = fmax(ex - 1e-9, 0.0), my = fmax(ey - 1e-9, 0.0), mz = fmax(ez - 1e-9, 0.0);
-          lb = mx * mx + my * my + mz * mz;
+    uint32_t best_rid = 0xFFFFFFFFu, best_i = 0xFFFFFFFFu;
+    auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count) {
+      const unsigned long long key = pack_key(bx + sx, by + sy, bz + sz);
+      uint64_t h = mix64(key) & M.mask;
+      first = 0;
+      count = 0;
+      for (;;) {
+        ++n_probe;
+        const Slot sl = M.table[h];
+        if (sl.key == key) {
+          first = sl.first;
+          count = sl.count;
+          return;
         }
-        if (lb > best) continue;
-        const unsigned long long key = pack_key(bx + sx, by + sy, bz + sz);
-        uint64_t h = mix64(key) & M.mask;
-        uint32_t first = 0, count = 0;
-        for (;;) {
-          const Slot sl = M.table[h];
-          if (sl.key == key) {
-            first = sl.first;
-            count = sl.count;
-            break;
-          }
-          if (sl.key == 0ull) break;
-          h = (h + 1) & M.mask;
-        }
-        for (uint32_t i = first; i < first + count; ++i) {
-          const double4 p = M.pos[i];
-          const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
-          const double d2 = (dx * dx + dz * dz) + dy * dy;
-          if (d2 < best || (d2 == best && M.rid[i] < best_rid)) {
-            best = d2;
-            best_rid = M.rid[i];
-            best_i = i;
-            found = true;
-          }
+        if (sl.key == 0ull) return;
+        h = (h + 1) & M.mask;
+      }
+    };
+    auto test = [&](uint32_t i) {
+      const double4 p = M.pos[i];
+      const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
+      const double d2 = (dx * dx + dz * dz) + dy * dy;
+      if (d2 <= best) {
+        const uint32_t rid = M.rid[i];
+        if (d2 < best || rid < best_rid) {
+          best = d2;
+          best_rid = rid;
+          best_i = i;
         }
       }
-    }
-    int32_t pair = -1;
-    double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
-    if (found) {
-      const uint32_t sg = M.seg[best_i];
-      const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
-      const double4 p = M.pos[best_i];
-      double o[3];
-      d_xform(Ti, p.x, p.y, p.z, o);
-      pi = make_double4(o[0], o[1], o[2], 0.0);
-      if (planar) {
-        const double4 n = M.nrm[best_i];
-        d_rot(Ti, n.x, n.y, n.z, o);
-        ni = make_double4(o[0], o[1], o[2], 0.0);
+    };
+    auto group_min = [&]() {  // argmin over (d^2, build order) across the kGroup lanes
+#pragma unroll
+      for (int o = kGroup / 2; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o, kGroup);
+        const uint32_t orid = __shfl_xor(best_rid, o, kGroup);
+        const uint32_t oi = __shfl_xor(best_i, o, kGroup);
+        if (oi != 0xFFFFFFFFu && (best_i == 0xFFFFFFFFu || ob < best || (ob == best && orid < best_rid))) {
+          best = ob;
+          best_rid = orid;
+          best_i = oi;
+        }
       }
-      if (best < a.max_d2) pair = (int32_t)sg;
+    };
+    const bool inr = key_in_range(bx, by, bz);
+    // phase 1: the query's own voxel (shift 0, visited first by the reference too),
+    // its records split over the group's lanes
+    if (inr) {
+      uint32_t first, count;
+      if (g == 0) probe(0, 0, 0, first, count);
+      first = __shfl(first, 0, kGroup);
+      count = __shfl(count, 0, kGroup);
+      n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
+      for (uint32_t i = first + g; i < first + count; i += kGroup) test(i);
     }
-    const uint32_t gq = planar ? qi : a.nq_pl + qi;
-    m_pair[gq] = pair;
-    m_d2[gq] = found ? best : DBL_MAX;
-    m_pi[gq] = pi;
-    if (planar) m_ni[qi] = ni;
-    m_ins[gq] = (!found || best > a.min_d2) ? 1 : 0;
-    if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
+    group_min();  // every lane now holds the own-voxel best: the bound for phase 2
+    // phase 2: the other 26 voxels.  Lane g bounds and probes shifts g+1, g+1+kGroup,
+    // ... (<= 4) in parallel; then the group walks every surviving voxel together
+    // (records split over the lanes), re-checking each bound against the shared best.
+    constexpr int kPer = (26 + kGroup - 1) / kGroup;
+    uint32_t vf[kPer], vc[kPer];
+    double vlb[kPer];
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+      vc[t] = 0;
+      vf[t] = 0;
+      vlb[t] = INFINITY;
+      const int s = 1 + g + t * kGroup;
+      if (!inr || s >= 27) continue;
+      const int sx = c_shift[s][0], sy = c_shift[s][1], sz = c_shift[s][2];
+      const double ex = sx < 0 ? lo[0] : (sx > 0 ? hi[0] : 0.0);
+      const double ey = sy < 0 ? lo[1] : (sy > 0 ? hi[1] : 0.0);
+      const double ez = sz < 0 ? lo[2] : (sz > 0 ? hi[2] : 0.0);
+      const double mx = fmax(ex - 1e-9, 0.0), my = fmax(ey - 1e-9, 0.0), mz = fmax(ez - 1e-9, 0.0);
+      const double lb = mx * mx + my * my + mz * mz;
+      if (lb > best) continue;  // conservative: no point inside can win
+      probe(sx, sy, sz, vf[t], vc[t]);
+      vlb[t] = lb;
+    }
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+      for (int l = 0; l < kGroup; ++l) {
+        const uint32_t cnt = __shfl(vc[t], l, kGroup);
+        if (cnt == 0) continue;
+        const double lb = __shfl(vlb[t], l, kGroup);
+        if (lb > best) continue;  // best is group-uniform here
+        const uint32_t first = __shfl(vf[t], l, kGroup);
+        n_cand += cnt / kGroup + (g < (int)(cnt % kGroup) ? 1 : 0);
+        for (uint32_t i = first + g; i < first + cnt; i += kGroup) test(i);
+        group_min();
+      }
+    }
+    if (g == 0) {
+      const bool found = best_i != 0xFFFFFFFFu;
+      int32_t pair = -1;
+      double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
+      if (found) {
+        const uint32_t sg = M.seg[best_i];
+        const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
+        const double4 p = M.pos[best_i];
+        double o[3];
+        d_xform(Ti, p.x, p.y, p.z, o);
+        pi = make_double4(o[0], o[1], o[2], 0.0);
+        if (planar) {
+          const double4 n = M.nrm[best_i];
+          d_rot(Ti, n.x, n.y, n.z, o);
+          ni = make_double4(o[0], o[1], o[2], 0.0);
+        }
+        if (best < a.max_d2) pair = (int32_t)sg;
+      }
+      const uint32_t gq = planar ? qi : a.nq_pl + qi;
+      m_pair[gq] = pair;
+      m_d2[gq] = found ? best : DBL_MAX;
+      m_pi[gq] = pi;
+      if (planar) m_ni[qi] = ni;
+      m_ins[gq] = (!found || best > a.min_d2) ? 1 : 0;
+      if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
+    }
+  }
+  // work counters (probes, candidate records) for the algorithmic-byte model: one
+  // plain store per block (no same-address atomics), summed on the host
+  __shared__ uint32_t s_work[2][kMatchThreads / kWave];
+  const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
+  if (lane_id() == 0) {
+    s_work[0][threadIdx.x / kWave] = wp;
+    s_work[1][threadIdx.x / kWave] = wc;
   }
   __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tp = 0, tc = 0;
+    for (int i = 0; i < kMatchThreads / kWave; ++i) {
+      tp += s_work[0][i];
+      tc += s_work[1][i];
+    }
+    work[2 * blockIdx.x] = tp;
+    work[2 * blockIdx.x + 1] = tc;
+  }
   for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[(size_t)blockIdx.x * a.K + k] = s_hist[k];
 }
 
-// One block: per-type per-pair block offsets (stable counting sort), pair counts,
-// and the linearize chunk table (pair-major: plane chunks then point chunks).
-__global__ __launch_bounds__(1024) void k_pair_offsets(const uint32_t* __restrict__ hist, uint32_t nb_pl,
-                                                       uint32_t nb_pt, int K, uint32_t* __restrict__ hist_off,
-                                                       uint32_t* __restrict__ pair_counts,
-                                                       uint32_t* __restrict__ chunk_range, Chunk* __restrict__ chunks,
-                                                       uint32_t* __restrict__ n_chunks) {
-  __shared__ uint32_t ws[16];
+// Per (pair, type): exclusive scan of the block histograms over blocks -> rank
+// offsets of each block within that pair, plus the pair total.  Grid (K, 2).
+__global__ __launch_bounds__(256) void k_pair_colscan(const uint32_t* __restrict__ hist, uint32_t nb_pl, uint32_t nb_pt,
+                                                      int K, uint32_t* __restrict__ hist_off,
+                                                      uint32_t* __restrict__ pair_counts) {
+  __shared__ uint32_t ws[4];
   __shared__ uint32_t carry;
-  for (int t = 0; t < 2; ++t) {
-    const uint32_t b0 = t == 0 ? 0 : nb_pl, nb = t == 0 ? nb_pl : nb_pt;
-    // per pair: running sum over blocks
-    for (int k = threadIdx.x; k < K; k += 1024) {
-      uint32_t run = 0;
-      for (uint32_t b = 0; b < nb; ++b) {
-        const size_t i = (size_t)(b0 + b) * K + k;
-        hist_off[i] = run;
-        run += hist[i];
-      }
-      pair_counts[t * K + k] = run;
+  const int k = blockIdx.x, t = blockIdx.y;
+  const uint32_t b0 = t == 0 ? 0 : nb_pl, nb = t == 0 ? nb_pl : nb_pt;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < nb; c0 += 256) {
+    const uint32_t b = c0 + threadIdx.x;
+    const uint32_t v = b < nb ? hist[(size_t)(b0 + b) * K + k] : 0u;
+    const uint32_t incl = wave_incl_scan(v);
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < 4; ++i) {
+      if (i < w) off += ws[i];
+      tot += ws[i];
     }
+    if (b < nb) hist_off[(size_t)(b0 + b) * K + k] = carry + off + incl - v;
     __syncthreads();
-    // exclusive scan of totals over pairs -> base
-    if (threadIdx.x == 0) carry = 0;
+    if (threadIdx.x == 0) carry += tot;
     __syncthreads();
-    for (int k0 = 0; k0 < K; k0 += 1024) {
-      const int k = k0 + threadIdx.x;
-      const uint32_t v = k < K ? pair_counts[t * K + k] : 0u;
-      const uint32_t incl = wave_incl_scan(v);
-      const int w = threadIdx.x / kWave;
+  }
+  if (threadIdx.x == 0) pair_counts[t * K + k] = carry;
+}
+
+// One block: pair bases (exclusive scan of the totals per type) and the linearize
+// chunk table (pair-major: plane chunks then point chunks of each pair).
+__global__ __launch_bounds__(1024) void k_pair_base(int K, const uint32_t* __restrict__ pair_counts,
+                                                    uint32_t* __restrict__ pair_base, uint32_t* __restrict__ chunk_range,
+                                                    Chunk* __restrict__ chunks, uint32_t* __restrict__ n_chunks) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry[3];
+  if (threadIdx.x < 3) carry[threadIdx.x] = 0;
+  __syncthreads();
+  for (int k0 = 0; k0 < K; k0 += 1024) {
+    const int k = k0 + threadIdx.x;
+    uint32_t npl = 0, npt = 0;
+    if (k < K) {
+      npl = pair_counts[k];
+      npt = pair_counts[K + k];
+    }
+    const uint32_t nch = (npl + kPlaneChunk - 1) / kPlaneChunk + (npt + kPointChunk - 1) / kPointChunk;
+    uint32_t ex[3];
+    const uint32_t vals[3] = {npl, npt, nch};
+    const int w = threadIdx.x / kWave;
+    for (int t = 0; t < 3; ++t) {
+      const uint32_t incl = wave_incl_scan(vals[t]);
       if (lane_id() == 63) ws[w] = incl;
       __syncthreads();
       uint32_t off = 0, tot = 0;
@@ -264,73 +368,45 @@ __global__ __launch_bounds__(1024) void k_pair_offsets(const uint32_t* __restric
         if (i < w) off += ws[i];
         tot += ws[i];
       }
-      const uint32_t base = carry + off + incl - v;
-      if (k < K)
-        for (uint32_t b = 0; b < nb; ++b) hist_off[(size_t)(b0 + b) * K + k] += base;
+      ex[t] = carry[t] + off + incl - vals[t];
       __syncthreads();
-      if (threadIdx.x == 0) carry += tot;
+      if (threadIdx.x == 0) carry[t] += tot;
       __syncthreads();
     }
-  }
-  // chunk table
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int k0 = 0; k0 < K; k0 += 1024) {
-    const int k = k0 + threadIdx.x;
-    uint32_t npl = 0, npt = 0, v = 0;
     if (k < K) {
-      npl = pair_counts[k];
-      npt = pair_counts[K + k];
-      v = (npl + kPlaneChunk - 1) / kPlaneChunk + (npt + kPointChunk - 1) / kPointChunk;
-    }
-    const uint32_t incl = wave_incl_scan(v);
-    const int w = threadIdx.x / kWave;
-    if (lane_id() == 63) ws[w] = incl;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int i = 0; i < 16; ++i) {
-      if (i < w) off += ws[i];
-      tot += ws[i];
-    }
-    if (k < K) {
-      uint32_t cb = carry + off + incl - v;
+      pair_base[k] = ex[0];
+      pair_base[K + k] = ex[1];
+      uint32_t cb = ex[2];
       chunk_range[k] = cb;
-      // plane rows of pair k start at the sum of the plane counts of pairs < k:
-      // recovered from the first block offset of that pair.
-      const uint32_t pl0 = nb_pl ? hist_off[k] : 0u;
-      const uint32_t pt0 = nb_pt ? hist_off[(size_t)nb_pl * K + k] : 0u;
-      for (uint32_t r = 0; r < npl; r += kPlaneChunk) chunks[cb++] = Chunk{0, (uint32_t)k, pl0 + r, pl0 + min(npl, r + kPlaneChunk)};
-      for (uint32_t r = 0; r < npt; r += kPointChunk) chunks[cb++] = Chunk{1, (uint32_t)k, pt0 + r, pt0 + min(npt, r + kPointChunk)};
+      for (uint32_t r = 0; r < npl; r += kPlaneChunk)
+        chunks[cb++] = Chunk{0, (uint32_t)k, ex[0] + r, ex[0] + min(npl, r + kPlaneChunk)};
+      for (uint32_t r = 0; r < npt; r += kPointChunk)
+        chunks[cb++] = Chunk{1, (uint32_t)k, ex[1] + r, ex[1] + min(npt, r + kPointChunk)};
     }
-    __syncthreads();
-    if (threadIdx.x == 0) carry += tot;
-    __syncthreads();
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    chunk_range[K] = carry;
-    *n_chunks = carry;
+    chunk_range[K] = carry[2];
+    *n_chunks = carry[2];
   }
 }
 
-// Stable scatter of accepted matches into pair-major SoA correspondences.
-__global__ __launch_bounds__(kMatchThreads) void k_pair_scatter(uint32_t nq_pl, uint32_t nq_pt, uint32_t nb_pl, int K,
-                                                                const int32_t* __restrict__ m_pair,
-                                                                const double4* __restrict__ m_pi,
-                                                                const double4* __restrict__ m_ni,
-                                                                const float4* __restrict__ q_pl,
-                                                                const float4* __restrict__ q_pt,
-                                                                const uint32_t* __restrict__ hist_off,
-                                                                double* __restrict__ c_pl, size_t ld_pl,
-                                                                double* __restrict__ c_pt, size_t ld_pt) {
-  extern __shared__ uint32_t s_wc[];  // [4][K] per-wave counts, then exclusive per wave
+// Stable scatter of accepted matches into pair-major SoA correspondences:
+// one wave per match block (kQPB = 64 queries), rank by ballot within the wave.
+__global__ __launch_bounds__(64) void k_pair_scatter(uint32_t nq_pl, uint32_t nq_pt, uint32_t nb_pl, int K,
+                                                     const int32_t* __restrict__ m_pair,
+                                                     const double4* __restrict__ m_pi,
+                                                     const double4* __restrict__ m_ni,
+                                                     const float4* __restrict__ q_pl,
+                                                     const float4* __restrict__ q_pt,
+                                                     const uint32_t* __restrict__ hist_off,
+                                                     const uint32_t* __restrict__ pair_base,
+                                                     double* __restrict__ c_pl, size_t ld_pl,
+                                                     double* __restrict__ c_pt, size_t ld_pt) {
   const bool planar = blockIdx.x < nb_pl;
-  const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - nb_pl) * kMatchThreads + threadIdx.x;
+  const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - nb_pl) * kQPB + threadIdx.x;
   const uint32_t nq = planar ? nq_pl : nq_pt;
-  const int w = threadIdx.x / kWave;
-  for (int i = threadIdx.x; i < 4 * K; i += kMatchThreads) s_wc[i] = 0;
-  __syncthreads();
   const int32_t pair = qi < nq ? m_pair[planar ? qi : nq_pl + qi] : -1;
-  // rank within wave among lanes with the same pair (stable by lane)
   uint32_t rank = 0;
   bool todo = pair >= 0;
   while (__ballot(todo)) {
@@ -341,28 +417,24 @@ __global__ __launch_bounds__(kMatchThreads) void k_pair_scatter(uint32_t nq_pl, 
       rank = __popcll(m & lanemask_lt());
       todo = false;
     }
-    if (lane_id() == 0) s_wc[w * K + v] = __popcll(m);
   }
-  __syncthreads();
-  if (pair >= 0) {
-    uint32_t before = 0;
-    for (int i = 0; i < w; ++i) before += s_wc[i * K + pair];
-    const uint32_t dst = hist_off[(size_t)blockIdx.x * K + pair] + before + rank;
-    const size_t gq = planar ? qi : nq_pl + qi;
-    const double4 pi = m_pi[gq];
-    if (planar) {
-      const double4 ni = m_ni[qi];
-      const float4 pj = q_pl[qi];
-      c_pl[0 * ld_pl + dst] = pi.x; c_pl[1 * ld_pl + dst] = pi.y; c_pl[2 * ld_pl + dst] = pi.z;
-      c_pl[3 * ld_pl + dst] = ni.x; c_pl[4 * ld_pl + dst] = ni.y; c_pl[5 * ld_pl + dst] = ni.z;
-      c_pl[6 * ld_pl + dst] = (double)pj.x; c_pl[7 * ld_pl + dst] = (double)pj.y;
-      c_pl[8 * ld_pl + dst] = (double)pj.z;
-    } else {
-      const float4 pj = q_pt[qi];
-      c_pt[0 * ld_pt + dst] = pi.x; c_pt[1 * ld_pt + dst] = pi.y; c_pt[2 * ld_pt + dst] = pi.z;
-      c_pt[3 * ld_pt + dst] = (double)pj.x; c_pt[4 * ld_pt + dst] = (double)pj.y;
-      c_pt[5 * ld_pt + dst] = (double)pj.z;
-    }
+  if (pair < 0) return;
+  const int t = planar ? 0 : 1;
+  const uint32_t dst = pair_base[t * K + pair] + hist_off[(size_t)blockIdx.x * K + pair] + rank;
+  const size_t gq = planar ? qi : nq_pl + qi;
+  const double4 pi = m_pi[gq];
+  if (planar) {
+    const double4 ni = m_ni[qi];
+    const float4 pj = q_pl[qi];
+    c_pl[0 * ld_pl + dst] = pi.x; c_pl[1 * ld_pl + dst] = pi.y; c_pl[2 * ld_pl + dst] = pi.z;
+    c_pl[3 * ld_pl + dst] = ni.x; c_pl[4 * ld_pl + dst] = ni.y; c_pl[5 * ld_pl + dst] = ni.z;
+    c_pl[6 * ld_pl + dst] = (double)pj.x; c_pl[7 * ld_pl + dst] = (double)pj.y;
+    c_pl[8 * ld_pl + dst] = (double)pj.z;
+  } else {
+    const float4 pj = q_pt[qi];
+    c_pt[0 * ld_pt + dst] = pi.x; c_pt[1 * ld_pt + dst] = pi.y; c_pt[2 * ld_pt + dst] = pi.z;
+    c_pt[3 * ld_pt + dst] = (double)pj.x; c_pt[4 * ld_pt + dst] = (double)pj.y;
+    c_pt[5 * ld_pt + dst] = (double)pj.z;
   }
 }
 
@@ -495,8 +567,8 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   a.bound = obs <= a.w * a.w ? obs : INFINITY;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
-  a.nb_pl = (c->n_qpl + kMatchThreads - 1) / kMatchThreads;
-  const uint32_t nb_pt = (c->n_qpt + kMatchThreads - 1) / kMatchThreads;
+  a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
+  const uint32_t nb_pt = (c->n_qpt + kQPB - 1) / kQPB;
   a.K = (int)c->K;
   const uint32_t nq = c->n_qpl + c->n_qpt;
   c->m_pair.ensure(nq + 1);
@@ -508,6 +580,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->hist.ensure((size_t)(nb + 1) * K);
   c->hist_off.ensure((size_t)(nb + 1) * K);
   c->pair_counts.ensure(2 * (size_t)K);
+  c->pair_base.ensure(2 * (size_t)K);
   c->chunk_range.ensure(K + 1);
   const uint32_t maxch = c->n_qpl / kPlaneChunk + c->n_qpt / kPointChunk + 2 * K + 2;
   c->chunks.ensure(maxch);
@@ -517,34 +590,61 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->ld_pt = c->n_qpt + 1;
   c->c_pl.ensure(9 * c->ld_pl);
   c->c_pt.ensure(6 * c->ld_pt);
+  c->work.ensure(2 * (size_t)nb + 2);
+  c->work_blocks = nb;
   auto view = [&](int t) {
     VoxMap& M = c->map[t];
     return MapView{reinterpret_cast<const Slot*>(M.table.p), M.cap ? M.cap - 1 : 0, M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
   };
+  // Algorithmic bytes of a match launch: query read (16 B) +
+  // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + 16 B per hash probe +
+  // 36 B per candidate record tested (double4 position + build-order id), using the
+  // probe/candidate counts of the previous launch (counted by the kernel).
+  const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + 16.0 * c->last_probes + 36.0 * c->last_cands;
   if (nb > 0) {
-    const double bytes = 32.0 * c->n_qpl + 16.0 * c->n_qpt;
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
     hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
                        c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_poses.p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
-                       c->m_ni.p, c->m_ins.p, c->hist.p);
+                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p);
     FMX_HIP(hipGetLastError());
   }
   {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
-    hipLaunchKernelGGL(k_pair_offsets, dim3(1), dim3(1024), 0, st, c->hist.p, a.nb_pl, nb_pt, a.K, c->hist_off.p,
-                       c->pair_counts.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p);
+    if (c->K > 0 && nb > 0) {
+      hipLaunchKernelGGL(k_pair_colscan, dim3(c->K, 2), dim3(256), 0, st, c->hist.p, a.nb_pl, nb_pt, a.K,
+                         c->hist_off.p, c->pair_counts.p);
+      FMX_HIP(hipGetLastError());
+    } else if (c->K > 0) {
+      FMX_HIP(hipMemsetAsync(c->pair_counts.p, 0, 2 * c->K * sizeof(uint32_t), st));
+    }
+    hipLaunchKernelGGL(k_pair_base, dim3(1), dim3(1024), 0, st, a.K, c->pair_counts.p, c->pair_base.p,
+                       c->chunk_range.p, c->chunks.p, c->n_chunks.p);
     FMX_HIP(hipGetLastError());
-    if (nb > 0) {
-      hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(kMatchThreads), 4 * K * sizeof(uint32_t), st, c->n_qpl,
-                         c->n_qpt, a.nb_pl, a.K, c->m_pair.p, c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p,
-                         c->hist_off.p, c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
+    if (nb > 0 && c->K > 0) {
+      hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(64), 0, st, c->n_qpl, c->n_qpt, a.nb_pl, a.K, c->m_pair.p,
+                         c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, c->pair_base.p, c->c_pl.p,
+                         c->ld_pl, c->c_pt.p, c->ld_pt);
       FMX_HIP(hipGetLastError());
     }
   }
-  // per-pair counts to the host (the caller needs them; one sync per match)
-  c->h_counts.ensure(2 * (size_t)K);
-  FMX_HIP(hipMemcpyAsync(c->h_counts.p, c->pair_counts.p, 2 * (size_t)c->K * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  FMX_HIP(hipStreamSynchronize(st));
+  // per-pair counts + work counters to pinned host memory; consumed at the next sync
+  c->h_counts.ensure(2 * (size_t)K + 4);
+  if (c->K)
+    FMX_HIP(hipMemcpyAsync(c->h_counts.p, c->pair_counts.p, 2 * (size_t)c->K * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (c->prof.on) {  // per-block work counters, only needed for the profile's byte model
+    c->h_work.ensure(2 * (size_t)nb + 2);
+    if (nb) FMX_HIP(hipMemcpyAsync(c->h_work.p, c->work.p, 2 * (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  }
+  c->counts_pending = true;
+  c->have_match = true;
+  c->have_corr = true;
+}
+
+// Consume the asynchronously copied match counts (caller has synchronized or will).
+void match_counts_fetch(fmx_ctx* c) {
+  if (!c->counts_pending) return;
+  FMX_HIP(hipStreamSynchronize(c->stream));
+  const int K = std::max<int>((int)c->K, 1);
   c->cnt_pl.assign(c->h_counts.p, c->h_counts.p + c->K);
   c->cnt_pt.assign(c->h_counts.p + c->K, c->h_counts.p + 2 * c->K);
   c->rows_pl = c->rows_pt = 0;
@@ -552,8 +652,17 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     c->rows_pl += c->cnt_pl[k];
     c->rows_pt += c->cnt_pt[k];
   }
-  c->have_match = true;
-  c->have_corr = true;
+  (void)K;
+  if (c->prof.on) {
+    double tp = 0, tc = 0;
+    for (uint32_t b = 0; b < c->work_blocks; ++b) {
+      tp += c->h_work.p[2 * b];
+      tc += c->h_work.p[2 * b + 1];
+    }
+    c->last_probes = tp;
+    c->last_cands = tc;
+  }
+  c->counts_pending = false;
 }
 
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
