@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c4", choices=["c2", "c3", "c4"])
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--profile-steps", type=int, default=None,
+                    help="extra steps, after the timed ones, with per-kernel HIP-event timing (roofline); "
+                         "default = --steps.  The timed region itself runs without event overhead.")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
@@ -117,7 +120,8 @@ def main():
     # independent stream per rank (replicas): different trajectory phase
     world_obj = synth.World()
     k0 = 1000 * rank
-    total = a.warmup + a.steps
+    psteps = a.steps if a.profile_steps is None else a.profile_steps
+    total = a.warmup + a.steps + psteps
     scans = [synth.raycast(world_obj, synth.trajectory_pose(k0 + k), geo, synth.SEED + 7919 * (k0 + k + 1), dev)
              for k in range(total)]
     torch.cuda.synchronize()
@@ -125,20 +129,25 @@ def main():
     for k in range(a.warmup):
         ctx.register_scan(scans[k])
     ctx.sync()
-    ctx.profile(True)
-    ctx.profile_reset()
     stats = []
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.warmup, total):
+    for k in range(a.warmup, a.warmup + a.steps):
         ctx.register_scan(scans[k])
         stats.append(ctx.last_stats())
     ctx.sync()
     torch.cuda.synchronize()
     barrier(world)
     t_local = time.perf_counter() - t0
+    # roofline pass: same stream continued, per-kernel HIP events on the context stream
+    ctx.profile(True)
+    ctx.profile_reset()
+    for k in range(a.warmup + a.steps, total):
+        ctx.register_scan(scans[k])
+    ctx.sync()
     prof = ctx.profile_read()
+    ctx.profile(False)
     t_max = max_over_ranks(t_local, world, local)
     scans_total = sum_over_ranks(float(a.steps), world, local)
     if rank != 0:
@@ -184,7 +193,8 @@ def main():
                    "points_per_scan": n_pts, "parallelism": f"replicas x{world}"},
         "mpts_per_s": round(value * n_pts / 1e6, 3),
         "roofline": roof,
-        "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 4) for k, v in prof.items()},
+        "kernels_ms_per_step": {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()},
+        "profile_steps": psteps,
         "counters": st_mean,
     }
     if not a.no_cpu_baseline and world == 1:

@@ -555,7 +555,7 @@ __device__ int fit_one(const float4* __restrict__ scan, const uint32_t* __restri
 
 // per-row offsets of {planar with normal, points, planar selected}: one block
 __global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, const uint32_t* row_ok, int R,
-                                                   uint32_t* row_off /* [3][R+1] */) {
+                                                   uint32_t* row_off /* [3][R+1] */, uint32_t* host_totals) {
   __shared__ uint32_t ws[16];
   __shared__ uint32_t carry[3];
   if (threadIdx.x < 3) carry[threadIdx.x] = 0;
@@ -580,7 +580,10 @@ __global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, c
       __syncthreads();
     }
   }
-  if (threadIdx.x < 3) row_off[threadIdx.x * (R + 1) + R] = carry[threadIdx.x];
+  if (threadIdx.x < 3) {
+    row_off[threadIdx.x * (R + 1) + R] = carry[threadIdx.x];
+    host_totals[threadIdx.x] = carry[threadIdx.x];  // mapped host memory: no copy op
+  }
 }
 
 // ordered compaction of row slots into the query arrays (block per row)
@@ -692,14 +695,12 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   }
   {
     ProfScope ps(c->prof, PROF_COMPACT, 0.0, st);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, st, c->row_counts.p, c->row_ok.p, R, c->row_off.p);
+    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, st, c->row_counts.p, c->row_ok.p, R, c->row_off.p,
+                       c->h_u32.d);
   }
   FMX_HIP(hipGetLastError());
-  // totals: planar-with-normal, points, selected
-  FMX_HIP(hipMemcpyAsync(c->h_u32.p + 0, c->row_off.p + R, 4, hipMemcpyDeviceToHost, st));
-  FMX_HIP(hipMemcpyAsync(c->h_u32.p + 1, c->row_off.p + (R + 1) + R, 4, hipMemcpyDeviceToHost, st));
-  FMX_HIP(hipMemcpyAsync(c->h_u32.p + 2, c->row_off.p + 2 * (R + 1) + R, 4, hipMemcpyDeviceToHost, st));
-  FMX_HIP(hipStreamSynchronize(st));
+  // totals (planar-with-normal, points, selected) were written to mapped host memory
+  stream_wait(c);
   const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
   c->q_pl_pos.ensure(npl + 1);
   c->q_pl_nrm.ensure(npl + 1);

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -448,10 +449,10 @@ struct DeviceLM {
     }
     c2 = 0;
     if (K == 0) return 0.0;
-    fill(Tj);
     e.G.resize(28 * (size_t)K);
     e.err.resize(K);
-    run_linearize(c, e.poses_i.data(), e.poses_j.data(), sigma, 1, e.G.data(), e.err.data());
+    // window poses = the built map's poses (unchanged during the scan); Tj by value
+    run_linearize_mapj(c, Tj.m, sigma, 1, e.G.data(), e.err.data());
     ++linearizations;
     double er = 0;
     for (uint32_t k = 0; k < K; ++k) {
@@ -588,39 +589,87 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   std::vector<double> poses(12 * scans.size());
   for (size_t k = 0; k < scans.size(); ++k) std::memcpy(&poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double));
   run_map_build(c, scans, poses.data(), P.max_dist_matching);
-  // ICP loop (form.cpp:67-89)
-  DeviceLM lm{c, e, P.planar_constraint_sigma};
-  uint64_t icp = 0, lm_it = 0;
-  bool converged = false;
-  Pose last_after = e.values.at(j);
-  for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
-    ++icp;
-    const Pose before = e.values.at(j);
-    run_match(c, before.m, P.max_dist_matching, P.min_dist_map);
-    int li = 0;
-    const Pose after = lm.optimize(before, &li);
-    lm_it += li;
-    double xi[6];
-    logmap(compose(inverse(before), after), xi);
-    double dn = 0;
-    for (double x : xi) dn += x * x;
-    if (std::sqrt(dn) < P.new_pose_threshold) {
-      converged = true;
-      last_after = after;
-      break;
+  uint64_t icp = 0, lm_it = 0, lins = 0;
+  static const bool host_lm = std::getenv("FMX_DEVICE_LM") == nullptr;  // default: host LM
+  if (host_lm) {
+    // ICP loop (form.cpp:67-89) with the LM on the host (one sync per linearization)
+    DeviceLM lm{c, e, P.planar_constraint_sigma};
+    bool converged = false;
+    Pose last_after = e.values.at(j);
+    for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
+      ++icp;
+      const Pose before = e.values.at(j);
+      run_match(c, before.m, P.max_dist_matching, P.min_dist_map);
+      int li = 0;
+      const Pose after = lm.optimize(before, &li);
+      lm_it += li;
+      double xi[6];
+      logmap(compose(inverse(before), after), xi);
+      double dn = 0;
+      for (double x : xi) dn += x * x;
+      if (std::sqrt(dn) < P.new_pose_threshold) {
+        converged = true;
+        last_after = after;
+        break;
+      }
+      e.values[j] = after;  // update_current_pose
     }
-    e.values[j] = after;  // update_current_pose
-  }
-  // optimize(false) + update_values (form.cpp:92-93).  In the single-pose mode the
-  // graph is the same current-scan factor set (get_single_graph ignores `fast`), so
-  // after a converged break it restarts from `before` with the same data and
-  // returns `after` again, bit for bit: reuse it.  Otherwise run it.
-  if (converged) {
-    e.values[j] = last_after;
+    // optimize(false) + update_values (form.cpp:92-93).  In the single-pose mode the
+    // graph is the same current-scan factor set (get_single_graph ignores `fast`), so
+    // after a converged break it restarts from `before` with the same data and
+    // returns `after` again, bit for bit: reuse it.  Otherwise run it.
+    if (converged) {
+      e.values[j] = last_after;
+    } else {
+      int li = 0;
+      e.values[j] = lm.optimize(e.values.at(j), &li);
+      lm_it += li;
+    }
+    lins = lm.linearizations;
   } else {
-    int li = 0;
-    e.values[j] = lm.optimize(e.values.at(j), &li);
-    lm_it += li;
+    // ICP loop on the device (IcpDev): per iteration the host enqueues begin ->
+    // match -> pair sort -> kRounds x (linearize, LM step) -> end, then reads the
+    // ~0.5 KB state back once.  Kernels of a converged loop exit immediately.
+    constexpr int kRounds = 4;
+    c->icp.ensure(1);
+    c->h_icp.ensure(1);
+    IcpDev& hs = *c->h_icp.p;
+    std::memset(&hs, 0, sizeof(hs));
+    std::memcpy(hs.Tcur, e.values.at(j).m, sizeof(hs.Tcur));
+    hs.ended = -1;
+    hs.K = (int32_t)c->K;
+    FMX_HIP(hipMemcpyAsync(c->icp.p, &hs, sizeof(IcpDev), hipMemcpyHostToDevice, c->stream));
+    auto readback = [&]() {
+      FMX_HIP(hipMemcpyAsync(&hs, c->icp.p, sizeof(IcpDev), hipMemcpyDeviceToHost, c->stream));
+      stream_wait(c);
+    };
+    for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
+      icp_launch(c, 0);
+      run_match(c, nullptr, P.max_dist_matching, P.min_dist_map, c->icp.p);
+      lm_rounds(c, kRounds);
+      icp_launch(c, 1);
+      readback();
+      while (!hs.icp_done && hs.phase != 2) {  // LM needs more rounds
+        lm_rounds(c, kRounds);
+        icp_launch(c, 1);
+        readback();
+      }
+      if (hs.icp_done) break;
+    }
+    if (!hs.icp_done) {  // optimize(false) from the last updated pose
+      icp_launch(c, 2);
+      do {
+        lm_rounds(c, kRounds);
+        readback();
+      } while (hs.phase != 2);
+      hs.lm_total += hs.lm_iters;
+    }
+    Pose Tf;
+    std::memcpy(Tf.m, hs.T, sizeof(Tf.m));
+    e.values[j] = Tf;
+    icp = (uint64_t)hs.icp_iters;
+    lm_it = (uint64_t)hs.lm_total;
+    lins = (uint64_t)hs.lins;
   }
   match_counts_fetch(c);
   uint64_t mpl = 0, mpt = 0;
@@ -650,7 +699,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[3] = mpt;
   c->stats[4] = c->map[0].n;
   c->stats[5] = c->map[1].n;
-  c->stats[6] = lm.linearizations;
+  c->stats[6] = lins;
   c->stats[7] = scans.size();
   if (out) *out = fc;
 }
@@ -736,11 +785,13 @@ void fmx_destroy(fmx_ctx* c) {
   for (int t = 0; t < 2; ++t) {
     c->pool[t].pos.release(); c->pool[t].nrm.release();
     auto& M = c->map[t];
-    M.table.release(); M.cursor.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
+    M.table.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
     M.rseg.release(); M.pos.release(); M.nrm.release(); M.seg.release(); M.rid.release();
     c->segs[t].release(); c->h_segs[t].release();
   }
-  c->h_mapposes.release(); c->map_poses.release(); c->map_inv_poses.release(); c->map_err.release();
+  c->h_mapposes.release(); c->map_blob.release(); c->map_err.release();
+  c->blk_lo.release(); c->blk_hi.release(); c->icp.release(); c->h_icp.release(); c->h_work.release();
+  c->work.release(); c->pair_base.release();
   c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();
   c->hist.release(); c->hist_off.release(); c->c_pl.release(); c->c_pt.release(); c->pair_counts.release();
   c->chunk_range.release(); c->chunks.release(); c->n_chunks.release(); c->poses_ij.release();

@@ -47,14 +47,18 @@ struct DBuf {
   }
 };
 template <class T>
-struct HBuf {  // pinned host staging
+struct HBuf {  // pinned host memory, also mapped into the device address space
   T* p = nullptr;
+  T* d = nullptr;  // device-visible alias: kernels write small results here directly
   size_t cap = 0;
   void ensure(size_t n) {
     if (n <= cap) return;
     if (p) (void)hipHostFree(p);
     size_t c = n + n / 4 + 64;
-    FMX_HIP(hipHostMalloc(&p, c * sizeof(T), hipHostMallocDefault));
+    FMX_HIP(hipHostMalloc(&p, c * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent));
+    void* dp = nullptr;
+    FMX_HIP(hipHostGetDevicePointer(&dp, p, 0));
+    d = static_cast<T*>(dp);
     cap = c;
   }
   void release() {
@@ -112,7 +116,6 @@ struct Pool {
 // One built voxel map (VoxelMap<P>, map.hpp:66-94) in HBM.
 struct VoxMap {
   DBuf<uint4> table;      // fmx::Slot[cap]
-  DBuf<uint32_t> cursor;  // scatter cursors [cap]
   uint64_t cap = 0;       // power of two
   DBuf<double4> tpos, tnrm;     // transformed records, build order
   DBuf<uint32_t> rslot, rseg;   // per build-order record
@@ -127,6 +130,23 @@ struct Seg {
   uint32_t n;         // records
   uint32_t pool_off;  // offset in the pool
   uint32_t pad;
+};
+
+// Device-resident ICP + LM state (single-pose mode), one per context (icp.hip).
+struct IcpDev {
+  double Tcur[12];     // X(j) estimate (ConstraintManager::update_current_pose)
+  double Tbefore[12];  // pose this ICP iteration matched at
+  double T[12];        // LM: current values
+  double Tn[12];       // LM: trial values
+  double H[36], g[6], c, err, lambda, cur, linchg;
+  int32_t phase;       // LM: 0 linearize at T, 1 trial pending (linearize at Tn), 2 done
+  int32_t lm_iters;    // iterations of the running LM
+  int32_t lm_total;    // LM iterations this scan
+  int32_t lins;        // linearizations this scan
+  int32_t icp_iters;
+  int32_t icp_done;    // ICP converged (form.cpp:86-88 break)
+  int32_t ended;       // icp_iters value the end kernel last processed
+  int32_t K;
 };
 
 struct Chunk {
@@ -152,6 +172,7 @@ struct fmx_ctx {
   fmx::DBuf<int2> closest;
   fmx::DBuf<float4> nrm_slots, blk_lo, blk_hi;
   fmx::DBuf<uint32_t> scan_scratch, dev_u32;  // dev_u32: small device scalars
+  size_t scan_scratch_half = 0;
   fmx::HBuf<uint32_t> h_u32;
   int rows = 0, cols = 0;
 
@@ -169,7 +190,9 @@ struct fmx_ctx {
   fmx::DBuf<fmx::Seg> segs[2];
   fmx::HBuf<fmx::Seg> h_segs[2];
   fmx::HBuf<double> h_mapposes;
-  fmx::DBuf<double> map_poses, map_inv_poses;  // K x 12
+  fmx::DBuf<double> map_blob;                  // poses [K][12], inverses [K][12], segments
+  const double* map_poses_p = nullptr;
+  const double* map_inv_p = nullptr;
   double voxel_w = 0;
   bool have_map = false;
   fmx::DBuf<uint32_t> map_err;
@@ -209,6 +232,10 @@ struct fmx_ctx {
   fmx::HBuf<double> h_poses, h_G;
   fmx::HBuf<int32_t> h_i32;
 
+  // ---- device ICP/LM state
+  fmx::DBuf<fmx::IcpDev> icp;
+  fmx::HBuf<fmx::IcpDev> h_icp;
+
   // ---- host estimator state (register_scan)
   struct Est;
   Est* est = nullptr;
@@ -216,14 +243,28 @@ struct fmx_ctx {
 };
 
 namespace fmx {
+// Wait for the context stream by polling (hipStreamSynchronize's blocking wake-up
+// costs tens of microseconds; the ICP loop waits ~5-15 times per scan).
+inline void stream_wait(fmx_ctx* c) {
+  for (;;) {
+    const hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) throw HipError(std::string("hipStreamQuery: ") + hipGetErrorString(e));
+  }
+}
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out);
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w);
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map);
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,
+               const IcpDev* icp = nullptr);  // icp != null: pose from the device ICP state
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
 void match_counts_fetch(fmx_ctx* c);
+void icp_launch(fmx_ctx* c, int what);  // 0 begin ICP iteration, 1 end ICP iteration, 2 begin final LM
+void lm_rounds(fmx_ctx* c, int rounds);
 void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
                    double* G_out, double* err_out);
+// single-pose fast path: Ti = the built map's poses (device), Tj by value (no upload)
+void run_linearize_mapj(fmx_ctx* c, const double* pose_j34, double sigma, int mode, double* G_out, double* err_out);
 void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
                  const double* ppj, const uint32_t* nt, const double* tpi, const double* tpj);
 constexpr int kPlaneChunk = 64;  // plane rows per linearize chunk (one wave, one row per lane)

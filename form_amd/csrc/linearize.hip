@@ -136,13 +136,18 @@ __global__ __launch_bounds__(kLinThreads) void k_linearize(const Chunk* __restri
                                                            const double* __restrict__ c_pl, size_t ld_pl,
                                                            const double* __restrict__ c_pt, size_t ld_pt,
                                                            const double* __restrict__ poses, double inv,
-                                                           double* __restrict__ partials, size_t ldp) {
+                                                           double* __restrict__ partials, size_t ldp,
+                                                           const IcpDev* __restrict__ icp, Pose34 tjv, int tj_by_value) {
   constexpr int NG = LinShape<MODE>::NG;
+  if (icp && (icp->icp_done || icp->phase == 2)) return;  // device LM finished
   const uint32_t ch = blockIdx.x;
   if (ch >= *n_chunks) return;
   const Chunk d = chunks[ch];
-  const double* Ti = poses + 24 * d.pair;
-  const double* Tj = Ti + 12;
+  // poses: [K][Ti | Tj] (general API), or the map poses [K][Ti] with Tj from the
+  // device LM state (current / trial pose) or passed by value
+  const bool mapi = icp || tj_by_value;
+  const double* Ti = mapi ? poses + 12 * d.pair : poses + 24 * d.pair;
+  const double* Tj = icp ? (icp->phase == 0 ? icp->T : icp->Tn) : (tj_by_value ? tjv.m : Ti + 12);
   double acc[NG];
 #pragma unroll
   for (int i = 0; i < NG; ++i) acc[i] = 0.0;
@@ -212,25 +217,367 @@ __global__ __launch_bounds__(256) void k_lin_final(const uint32_t* __restrict__ 
   }
 }
 
+// ============================================================================ device LM
+// Single-pose Levenberg-Marquardt (GTSAM LevenbergMarquardtOptimizer defaults, the
+// same algorithm as the host DeviceLM in fmx_api.cpp and the oracle) and the ICP
+// loop control of form.cpp:67-93, run by single-lane kernels against IcpDev so the
+// host syncs once per ICP iteration instead of once per linearization.
+
+__device__ __forceinline__ void dpose_compose(const double* a, const double* b, double* o) {
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) o[4 * i + j] = (a[4 * i] * b[j] + a[4 * i + 1] * b[4 + j]) + a[4 * i + 2] * b[8 + j];
+    o[4 * i + 3] = ((a[4 * i] * b[3] + a[4 * i + 1] * b[7]) + a[4 * i + 2] * b[11]) + a[4 * i + 3];
+  }
+}
+__device__ __forceinline__ void dpose_inverse(const double* a, double* o) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) o[4 * i + j] = a[4 * j + i];
+  const double nt[3] = {-a[3], -a[7], -a[11]};
+  for (int i = 0; i < 3; ++i) o[4 * i + 3] = (o[4 * i] * nt[0] + o[4 * i + 1] * nt[1]) + o[4 * i + 2] * nt[2];
+}
+__device__ __forceinline__ void dcross(const double a[3], const double b[3], double o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+__device__ __forceinline__ void dpose_expmap(const double xi[6], double* T) {
+  const double* w = xi;
+  const double* v = xi + 3;
+  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  double A, B, a, b;
+  if (th2 <= 2.220446049250313e-16) {
+    A = 1.0;
+    B = 0.5;
+    a = 0.5;
+    b = 1.0 / 6.0;
+  } else {
+    const double th = sqrt(th2);
+    A = sin(th) / th;
+    B = (1.0 - cos(th)) / th2;
+    a = B;
+    b = (th - sin(th)) / (th2 * th);
+  }
+  const double W[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      const double w2 = W[i][0] * W[0][j] + W[i][1] * W[1][j] + W[i][2] * W[2][j];
+      T[4 * i + j] = (i == j ? 1.0 : 0.0) + A * W[i][j] + B * w2;
+    }
+  double wxv[3], wxwxv[3];
+  dcross(w, v, wxv);
+  dcross(w, wxv, wxwxv);
+  for (int i = 0; i < 3; ++i) T[4 * i + 3] = v[i] + a * wxv[i] + b * wxwxv[i];
+}
+__device__ double dpose_lognorm(const double* m) {  // ||Pose3::Logmap(T)||
+  const double tr = m[0] + m[5] + m[10];
+  double w[3];
+  if (tr + 1.0 < 1e-10) {
+    if (fabs(m[10] + 1.0) > 1e-10) {
+      const double s = M_PI / sqrt(2.0 + 2.0 * m[10]);
+      w[0] = s * m[2]; w[1] = s * m[6]; w[2] = s * (1.0 + m[10]);
+    } else if (fabs(m[5] + 1.0) > 1e-10) {
+      const double s = M_PI / sqrt(2.0 + 2.0 * m[5]);
+      w[0] = s * m[1]; w[1] = s * (1.0 + m[5]); w[2] = s * m[9];
+    } else {
+      const double s = M_PI / sqrt(2.0 + 2.0 * m[0]);
+      w[0] = s * (1.0 + m[0]); w[1] = s * m[4]; w[2] = s * m[8];
+    }
+  } else {
+    const double tr_3 = tr - 3.0;
+    double mag;
+    if (tr_3 < -1e-7) {
+      const double th = acos((tr - 1.0) / 2.0);
+      mag = th / (2.0 * sin(th));
+    } else {
+      mag = 0.5 - tr_3 * tr_3 / 12.0;
+    }
+    w[0] = mag * (m[9] - m[6]);
+    w[1] = mag * (m[2] - m[8]);
+    w[2] = mag * (m[4] - m[1]);
+  }
+  const double t = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  double xi[6] = {w[0], w[1], w[2], m[3], m[7], m[11]};
+  if (t >= 1e-10) {
+    const double wn[3] = {w[0] / t, w[1] / t, w[2] / t};
+    const double tt[3] = {m[3], m[7], m[11]};
+    double WT[3], WWT[3];
+    dcross(wn, tt, WT);
+    dcross(wn, WT, WWT);
+    const double Tan = tan(0.5 * t);
+    for (int i = 0; i < 3; ++i) xi[3 + i] = tt[i] - (0.5 * t) * WT[i] + (1 - t / (2. * Tan)) * WWT[i];
+  }
+  double n = 0;
+  for (int i = 0; i < 6; ++i) n += xi[i] * xi[i];
+  return sqrt(n);
+}
+__device__ __forceinline__ bool dchol_solve6(const double* H, const double* g, double lambda, double* x) {
+  double L[6][6];
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) L[i][j] = 0.0;
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = H[6 * i + j] + (i == j ? lambda : 0.0);
+      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+      if (i == j) {
+        if (s <= 0) return false;
+        L[i][i] = sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  double y[6];
+  for (int i = 0; i < 6; ++i) {
+    double s = g[i];
+    for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+  return true;
+}
+
+// LM state held in registers by the deciding lane (IcpDev fields it touches).
+struct LmReg {
+  double T[12], Tn[12], H[36], g[6], c, err, lambda, cur, linchg;
+  int phase, lm_iters;
+};
+
+// Advance the LM state machine until a trial pose is proposed (phase 1) or the
+// optimization ends (phase 2).  end_first: finish the current iteration first
+// (NonlinearOptimizer::defaultOptimize's convergence test), else propose directly
+// (tryLambda's solve: Cholesky of H + lambda I, validity of the linearized decrease,
+// increaseLambda on failure, give up at the upper bound 1e5).
+__device__ __forceinline__ void lm_advance(LmReg& s, bool end_first) {
+  bool end = end_first;
+  for (int guard = 0; guard < 256; ++guard) {
+    if (end) {
+      s.lm_iters++;
+      const double newErr = s.err;
+      bool conv;
+      if (newErr <= 0.0) conv = true;
+      else {
+        const double absDec = s.cur - newErr, relDec = absDec / s.cur;
+        conv = (relDec <= 1e-5) || (absDec <= 1e-5);
+      }
+      if (conv || s.lm_iters >= 100 || !isfinite(s.cur)) {
+        s.phase = 2;
+        return;
+      }
+      s.cur = newErr;
+      end = false;
+    }
+    const double oldLin = 0.5 * s.c;
+    double dx[6];
+    if (dchol_solve6(s.H, s.g, s.lambda, dx)) {
+      double dHd = 0, dg = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        double h = 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) h += s.H[6 * i + j] * dx[j];
+        dHd += dx[i] * h;
+        dg += dx[i] * s.g[i];
+      }
+      const double newLin = 0.5 * (dHd - 2 * dg + s.c);
+      const double linChange = oldLin - newLin;
+      if (linChange >= 0) {
+        double E[12];
+        dpose_expmap(dx, E);
+        dpose_compose(s.T, E, s.Tn);
+        s.linchg = linChange;
+        s.phase = 1;
+        return;
+      }
+    }
+    s.lambda *= 10.0;  // step not valid: increaseLambda
+    if (s.lambda >= 1e5) end = true;
+  }
+  s.phase = 2;
+}
+
+constexpr int kStepThreads = 256;  // 256: leaves the deciding lane enough VGPRs (no scratch)
+
+// Reduce the chunk partials of every pair (fixed order: 8 interleaved accumulators
+// per item, combined in order) and take one LM decision on a register copy.
+__global__ __launch_bounds__(kStepThreads) void k_lm_step(const uint32_t* __restrict__ chunk_range,
+                                                          const double* __restrict__ partials, size_t ldp, int K,
+                                                          double* __restrict__ Gs, IcpDev* __restrict__ s) {
+  extern __shared__ double sG[];  // [K * 28]
+  if (s->icp_done || s->phase == 2) return;
+  constexpr int NG = 28;
+  for (int it = threadIdx.x; it < K * NG; it += kStepThreads) {
+    const int k = it / NG, e = it % NG;
+    const uint32_t b = chunk_range[k], en = chunk_range[k + 1];
+    const double* p = partials + (size_t)e * ldp;
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t ch = b;
+    for (; ch + 8 <= en; ch += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += p[ch + u];
+    }
+    for (int u = 0; ch < en; ++ch, ++u) a[u] += p[ch];
+    sG[it] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  LmReg r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    r.T[i] = s->T[i];
+    r.Tn[i] = s->Tn[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 36; ++i) r.H[i] = s->H[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) r.g[i] = s->g[i];
+  r.c = s->c;
+  r.err = s->err;
+  r.lambda = s->lambda;
+  r.cur = s->cur;
+  r.linchg = s->linchg;
+  r.phase = s->phase;
+  r.lm_iters = s->lm_iters;
+  double H[36], g[6], c = 0, e = 0;
+#pragma unroll
+  for (int i = 0; i < 36; ++i) H[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) g[i] = 0;
+  for (int k = 0; k < K; ++k) {
+    const double* G = sG + NG * k;
+    int o = 0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int j = i; j < 7; ++j) {
+        const double v = G[o++];
+        if (i < 6 && j < 6) {
+          H[6 * i + j] += v;
+          if (i != j) H[6 * j + i] += v;
+        } else if (i < 6) {
+          g[i] += v;
+        } else {
+          c += v;
+        }
+      }
+    e += 0.5 * G[NG - 1];
+  }
+  if (r.phase == 0) {  // initial linearization at T
+#pragma unroll
+    for (int i = 0; i < 36; ++i) r.H[i] = H[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.g[i] = g[i];
+    r.c = c;
+    r.err = e;
+    if (e <= 0.0) r.phase = 2;
+    else {
+      r.cur = e;
+      lm_advance(r, false);
+    }
+  } else {  // trial linearized at Tn: tryLambda's accept test (minModelFidelity 1e-3)
+    const double oldLin = 0.5 * r.c;
+    const double costChange = r.err - e;
+    bool success;
+    if (r.linchg > 2.220446049250313e-16 * oldLin) success = (costChange / r.linchg) > 1e-3;
+    else success = true;
+    const bool stop = fabs(costChange) < 1e-5 * r.err;
+    if (success) {
+      r.lambda = fmax(0.0, r.lambda / 10.0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) r.T[i] = r.Tn[i];
+#pragma unroll
+      for (int i = 0; i < 36; ++i) r.H[i] = H[i];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) r.g[i] = g[i];
+      r.c = c;
+      r.err = e;
+      lm_advance(r, true);
+    } else if (!stop) {
+      r.lambda *= 10.0;
+      lm_advance(r, r.lambda >= 1e5);
+    } else {
+      lm_advance(r, true);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    s->T[i] = r.T[i];
+    s->Tn[i] = r.Tn[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 36; ++i) s->H[i] = r.H[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) s->g[i] = r.g[i];
+  s->c = r.c;
+  s->err = r.err;
+  s->lambda = r.lambda;
+  s->cur = r.cur;
+  s->linchg = r.linchg;
+  s->phase = r.phase;
+  s->lm_iters = r.lm_iters;
+  s->lins++;
+}
+
+// form.cpp:71-72: before = current pose; LM restarts (lambda0) from it.
+__global__ void k_icp_begin(IcpDev* s) {
+  if (s->icp_done) return;
+  for (int i = 0; i < 12; ++i) s->Tbefore[i] = s->T[i] = s->Tcur[i];
+  s->phase = 0;
+  s->lambda = 1e-5;
+  s->lm_iters = 0;
+  s->icp_iters++;
+}
+// form.cpp:83-88: stop if ||before.localCoordinates(after)|| < threshold, else
+// update_current_pose(after).
+__global__ void k_icp_end(IcpDev* s, double thr) {
+  if (s->icp_done || s->phase != 2 || s->ended == s->icp_iters) return;
+  s->ended = s->icp_iters;
+  s->lm_total += s->lm_iters;
+  double Bi[12], D[12];
+  dpose_inverse(s->Tbefore, Bi);
+  dpose_compose(Bi, s->T, D);
+  if (dpose_lognorm(D) < thr) s->icp_done = 1;
+  else
+    for (int i = 0; i < 12; ++i) s->Tcur[i] = s->T[i];
+}
+// optimize(false) after an unconverged loop: LM from the current pose.
+__global__ void k_lm_begin(IcpDev* s) {
+  for (int i = 0; i < 12; ++i) s->T[i] = s->Tcur[i];
+  s->phase = 0;
+  s->lambda = 1e-5;
+  s->lm_iters = 0;
+}
+
 }  // namespace
 
-void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
-                   double* G_out, double* err_out) {
+static void linearize_impl(fmx_ctx* c, const double* poses_i34, const double* poses_j34, const double* tj_val,
+                           double sigma, int mode, double* G_out, double* err_out) {
   if (!c->have_corr) throw StatusError(FMX_E_STATE, "no correspondences (call fmx_match or fmx_corr_set)");
   hipStream_t st = c->stream;
   const int K = (int)c->K;
   if (K == 0) return;
   const int NG = mode == 0 ? 91 : (mode == 1 ? 28 : 1);
-  c->h_poses.ensure(24 * (size_t)K);
-  for (int k = 0; k < K; ++k) {
-    std::memcpy(c->h_poses.p + 24 * k, poses_i34 + 12 * k, 12 * sizeof(double));
-    std::memcpy(c->h_poses.p + 24 * k + 12, poses_j34 + 12 * k, 12 * sizeof(double));
+  Pose34 tjv{};
+  const int tj_by_value = tj_val ? 1 : 0;
+  const double* dposes = c->map_poses_p;
+  if (tj_val) {
+    std::memcpy(tjv.m, tj_val, sizeof(tjv.m));
+  } else {
+    c->h_poses.ensure(24 * (size_t)K);
+    for (int k = 0; k < K; ++k) {
+      std::memcpy(c->h_poses.p + 24 * k, poses_i34 + 12 * k, 12 * sizeof(double));
+      std::memcpy(c->h_poses.p + 24 * k + 12, poses_j34 + 12 * k, 12 * sizeof(double));
+    }
+    c->poses_ij.ensure(24 * (size_t)K);
+    FMX_HIP(hipMemcpyAsync(c->poses_ij.p, c->h_poses.p, 24 * K * sizeof(double), hipMemcpyHostToDevice, st));
+    dposes = c->poses_ij.p;
   }
-  c->poses_ij.ensure(24 * (size_t)K);
-  FMX_HIP(hipMemcpyAsync(c->poses_ij.p, c->h_poses.p, 24 * K * sizeof(double), hipMemcpyHostToDevice, st));
   c->partials.ensure((size_t)std::max<uint32_t>(c->max_chunks, 1) * 91 + 1);
-  c->G.ensure((size_t)K * 92 + 1);
-  double* dG = c->G.p;
+  const size_t nout = (size_t)K * (mode == 2 ? 1 : NG + 1);
+  c->h_G.ensure(nout + 1);
+  double* dG = c->h_G.d;  // k_lin_final writes G / err into mapped host memory (no copy op)
   double* dErr = mode == 2 ? dG : dG + (size_t)K * NG;  // error-only: err is the whole output
   const double inv = 1.0 / sigma;  // FastIsotropic invsigma_ (gtsam.hpp:96)
   const uint32_t nb = std::max<uint32_t>(c->max_chunks, 1);
@@ -242,13 +589,16 @@ void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34,
     ProfScope ps(c->prof, mode == 2 ? PROF_ERROR : PROF_LINEARIZE, bytes, st);
     if (mode == 0)
       hipLaunchKernelGGL(k_linearize<0>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p, ldp);
+                         c->ld_pl, c->c_pt.p, c->ld_pt, dposes, inv, c->partials.p, ldp,
+                         (const IcpDev*)nullptr, tjv, tj_by_value);
     else if (mode == 1)
       hipLaunchKernelGGL(k_linearize<1>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p, ldp);
+                         c->ld_pl, c->c_pt.p, c->ld_pt, dposes, inv, c->partials.p, ldp,
+                         (const IcpDev*)nullptr, tjv, tj_by_value);
     else
       hipLaunchKernelGGL(k_linearize<2>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt, c->poses_ij.p, inv, c->partials.p, ldp);
+                         c->ld_pl, c->c_pt.p, c->ld_pt, dposes, inv, c->partials.p, ldp,
+                         (const IcpDev*)nullptr, tjv, tj_by_value);
     FMX_HIP(hipGetLastError());
   }
   {
@@ -261,10 +611,7 @@ void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34,
       hipLaunchKernelGGL(k_lin_final<2>, dim3(nfin), dim3(256), 0, st, c->chunk_range.p, c->partials.p, ldp, dG, dErr, K);
     FMX_HIP(hipGetLastError());
   }
-  const size_t nout = (size_t)K * (mode == 2 ? 1 : NG + 1);
-  c->h_G.ensure(nout);
-  FMX_HIP(hipMemcpyAsync(c->h_G.p, dG, nout * sizeof(double), hipMemcpyDeviceToHost, st));
-  FMX_HIP(hipStreamSynchronize(st));
+  stream_wait(c);
   match_counts_fetch(c);  // already copied; no extra wait
   if (mode == 2) {
     if (err_out) std::memcpy(err_out, c->h_G.p, K * sizeof(double));
@@ -272,6 +619,15 @@ void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34,
     if (G_out) std::memcpy(G_out, c->h_G.p, (size_t)K * NG * sizeof(double));
     if (err_out) std::memcpy(err_out, c->h_G.p + (size_t)K * NG, K * sizeof(double));
   }
+}
+
+void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
+                   double* G_out, double* err_out) {
+  linearize_impl(c, poses_i34, poses_j34, nullptr, sigma, mode, G_out, err_out);
+}
+void run_linearize_mapj(fmx_ctx* c, const double* pose_j34, double sigma, int mode, double* G_out, double* err_out) {
+  if (!c->have_map) throw StatusError(FMX_E_STATE, "no map");
+  linearize_impl(c, nullptr, nullptr, pose_j34, sigma, mode, G_out, err_out);
 }
 
 void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
@@ -340,6 +696,44 @@ void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, 
   c->counts_pending = false;
   c->have_corr = true;
   c->have_match = false;
+}
+
+}  // namespace fmx
+
+namespace fmx {
+
+void icp_launch(fmx_ctx* c, int what) {
+  hipStream_t st = c->stream;
+  if (what == 0) hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, st, c->icp.p);
+  else if (what == 1) hipLaunchKernelGGL(k_icp_end, dim3(1), dim3(1), 0, st, c->icp.p, c->P.new_pose_threshold);
+  else hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(1), 0, st, c->icp.p);
+  FMX_HIP(hipGetLastError());
+}
+
+// `rounds` x (linearize at the state's pose, reduce + LM decision); no host sync.
+void lm_rounds(fmx_ctx* c, int rounds) {
+  hipStream_t st = c->stream;
+  const int K = (int)c->K;
+  const uint32_t nb = std::max<uint32_t>(c->max_chunks, 1);
+  const size_t ldp = nb;
+  c->partials.ensure((size_t)nb * 91 + 1);
+  c->G.ensure((size_t)std::max(K, 1) * 92 + 1);
+  const double inv = 1.0 / c->P.planar_constraint_sigma;
+  for (int r = 0; r < rounds; ++r) {
+    {
+      ProfScope ps(c->prof, PROF_LINEARIZE, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * 28 * K, st);
+      if (K > 0)
+        hipLaunchKernelGGL(k_linearize<1>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
+                           c->ld_pl, c->c_pt.p, c->ld_pt, c->map_poses_p, inv, c->partials.p, ldp, c->icp.p,
+                           Pose34{}, 0);
+    }
+    {
+      ProfScope ps(c->prof, PROF_LIN_FINAL, 8.0 * 28 * (double)nb, st);
+      hipLaunchKernelGGL(k_lm_step, dim3(1), dim3(kStepThreads), (size_t)std::max(K, 1) * 28 * sizeof(double), st,
+                         c->chunk_range.p, c->partials.p, ldp, K, c->G.p, c->icp.p);
+    }
+    FMX_HIP(hipGetLastError());
+  }
 }
 
 }  // namespace fmx

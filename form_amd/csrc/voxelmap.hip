@@ -91,18 +91,20 @@ struct FirstOut {
   __device__ void operator()(size_t i, uint32_t v) const { t[i].first = v; }
 };
 
+// After the scatter each slot's `first` has advanced by `count`: records of a voxel
+// are [first - count, first).
 __global__ __launch_bounds__(256) void k_map_scatter(uint32_t nrec, const uint32_t* __restrict__ rslot,
                                                      const uint32_t* __restrict__ rseg,
                                                      const double4* __restrict__ tpos,
                                                      const double4* __restrict__ tnrm, int planar,
-                                                     const Slot* __restrict__ table, uint32_t* __restrict__ cursor,
+                                                     Slot* __restrict__ table,
                                                      double4* __restrict__ pos, double4* __restrict__ nrm,
                                                      uint32_t* __restrict__ seg, uint32_t* __restrict__ rid) {
   const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
   if (rec >= nrec) return;
   const uint32_t s = rslot[rec];
   if (s == 0xFFFFFFFFu) return;
-  const uint32_t o = table[s].first + atomicAdd(&cursor[s], 1u);
+  const uint32_t o = atomicAdd(&table[s].first, 1u);
   pos[o] = tpos[rec];
   if (planar) nrm[o] = tnrm[rec];
   seg[o] = rseg[rec];
@@ -149,8 +151,10 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
                                                          int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
                                                          double4* __restrict__ m_pi, double4* __restrict__ m_ni,
                                                          uint8_t* __restrict__ m_ins, uint32_t* __restrict__ hist,
-                                                         uint32_t* __restrict__ work) {
+                                                         uint32_t* __restrict__ work, const IcpDev* __restrict__ icp) {
   extern __shared__ uint32_t s_hist[];  // [K]
+  if (icp && icp->icp_done) return;  // device ICP loop already converged
+  const double* Tj = icp ? icp->Tbefore : a.Tj;
   const bool planar = blockIdx.x < a.nb_pl;
   const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kQPB + threadIdx.x / kGroup;
   const int g = threadIdx.x % kGroup;
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   if (qi < nq) {
     const float4 lq = planar ? q_pl[qi] : q_pt[qi];
     double wq[3];
-    d_xform(a.Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
+    d_xform(Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
     const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
     // distances from the query to its voxel's faces (per-voxel lower bound)
     const double lo[3] = {wq[0] - bx * a.w, wq[1] - by * a.w, wq[2] - bz * a.w};
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         ++n_probe;
         const Slot sl = M.table[h];
         if (sl.key == key) {
-          first = sl.first;
+          first = sl.first - sl.count;
           count = sl.count;
           return;
         }
@@ -312,7 +316,8 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
 // offsets of each block within that pair, plus the pair total.  Grid (K, 2).
 __global__ __launch_bounds__(256) void k_pair_colscan(const uint32_t* __restrict__ hist, uint32_t nb_pl, uint32_t nb_pt,
                                                       int K, uint32_t* __restrict__ hist_off,
-                                                      uint32_t* __restrict__ pair_counts) {
+                                                      uint32_t* __restrict__ pair_counts, const IcpDev* __restrict__ icp) {
+  if (icp && icp->icp_done) return;
   __shared__ uint32_t ws[4];
   __shared__ uint32_t carry;
   const int k = blockIdx.x, t = blockIdx.y;
@@ -343,7 +348,10 @@ __global__ __launch_bounds__(256) void k_pair_colscan(const uint32_t* __restrict
 // chunk table (pair-major: plane chunks then point chunks of each pair).
 __global__ __launch_bounds__(1024) void k_pair_base(int K, const uint32_t* __restrict__ pair_counts,
                                                     uint32_t* __restrict__ pair_base, uint32_t* __restrict__ chunk_range,
-                                                    Chunk* __restrict__ chunks, uint32_t* __restrict__ n_chunks) {
+                                                    Chunk* __restrict__ chunks, uint32_t* __restrict__ n_chunks,
+                                                    const IcpDev* __restrict__ icp, uint32_t* __restrict__ host_counts) {
+  if (icp && icp->icp_done) return;
+  for (int i = threadIdx.x; i < 2 * K; i += 1024) host_counts[i] = pair_counts[i];  // mapped host memory
   __shared__ uint32_t ws[16];
   __shared__ uint32_t carry[3];
   if (threadIdx.x < 3) carry[threadIdx.x] = 0;
@@ -402,7 +410,9 @@ __global__ __launch_bounds__(64) void k_pair_scatter(uint32_t nq_pl, uint32_t nq
                                                      const uint32_t* __restrict__ hist_off,
                                                      const uint32_t* __restrict__ pair_base,
                                                      double* __restrict__ c_pl, size_t ld_pl,
-                                                     double* __restrict__ c_pt, size_t ld_pt) {
+                                                     double* __restrict__ c_pt, size_t ld_pt,
+                                                     const IcpDev* __restrict__ icp) {
+  if (icp && icp->icp_done) return;
   const bool planar = blockIdx.x < nb_pl;
   const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - nb_pl) * kQPB + threadIdx.x;
   const uint32_t nq = planar ? nq_pl : nq_pt;
@@ -476,54 +486,61 @@ uint64_t next_pow2(uint64_t v) {
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w) {
   hipStream_t st = c->stream;
   const int K = (int)scans.size();
+  const int Kc = std::max(K, 1);
   c->map_scans = scans;
   c->voxel_w = w;
   c->K = (uint32_t)K;
-  // poses and their inverses (GTSAM Pose3::inverse: (R^T, R^T (-t))), computed on the
-  // host with the same expression order as the device transforms.
-  c->h_mapposes.ensure(24 * (size_t)std::max(K, 1));
+  // one packed upload: poses [K][12], inverses [K][12] (GTSAM Pose3::inverse:
+  // (R^T, R^T(-t)), same expression order as the device transforms), segments of
+  // both feature types [2][K] (Seg = 16 B = 2 doubles)
+  const size_t n_d = 24 * (size_t)Kc + 2 * 2 * (size_t)Kc;
+  c->h_mapposes.ensure(n_d);
   double* hp = c->h_mapposes.p;
   for (int k = 0; k < K; ++k) {
     const double* T = poses34 + 12 * k;
     std::memcpy(hp + 12 * k, T, 12 * sizeof(double));
-    double* I = hp + 12 * (K + k);
+    double* I = hp + 12 * (Kc + k);
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) I[4 * i + j] = T[4 * j + i];
     const double nt[3] = {-T[3], -T[7], -T[11]};
     for (int i = 0; i < 3; ++i) I[4 * i + 3] = (I[4 * i] * nt[0] + I[4 * i + 1] * nt[1]) + I[4 * i + 2] * nt[2];
   }
-  c->map_poses.ensure(12 * (size_t)std::max(K, 1));
-  c->map_inv_poses.ensure(12 * (size_t)std::max(K, 1));
-  if (K > 0) {
-    FMX_HIP(hipMemcpyAsync(c->map_poses.p, hp, 12 * K * sizeof(double), hipMemcpyHostToDevice, st));
-    FMX_HIP(hipMemcpyAsync(c->map_inv_poses.p, hp + 12 * K, 12 * K * sizeof(double), hipMemcpyHostToDevice, st));
+  Seg* hseg = reinterpret_cast<Seg*>(hp + 24 * (size_t)Kc);
+  uint32_t nrec[2];
+  for (int t = 0; t < 2; ++t) {
+    Pool& pool = c->pool[t];
+    uint32_t n = 0;
+    for (int k = 0; k < Kc; ++k) {
+      uint32_t cnt = 0, po = 0;
+      if (k < K) {
+        auto it = pool.ranges.find(scans[k]);
+        if (it != pool.ranges.end()) {
+          cnt = it->second.second;
+          po = (uint32_t)it->second.first;
+        }
+      }
+      hseg[t * Kc + k] = Seg{n, cnt, po, 0};
+      n += cnt;
+    }
+    nrec[t] = n;
   }
+  c->map_blob.ensure(n_d);
+  FMX_HIP(hipMemcpyAsync(c->map_blob.p, hp, n_d * sizeof(double), hipMemcpyHostToDevice, st));
+  c->map_poses_p = c->map_blob.p;
+  c->map_inv_p = c->map_blob.p + 12 * (size_t)Kc;
+  const Seg* dseg = reinterpret_cast<const Seg*>(c->map_blob.p + 24 * (size_t)Kc);
   c->map_err.ensure(1);
-  FMX_HIP(hipMemsetAsync(c->map_err.p, 0, 4, st));
   for (int t = 0; t < 2; ++t) {
     Pool& pool = c->pool[t];
     VoxMap& M = c->map[t];
-    std::vector<Seg> hs(std::max(K, 1));
-    uint32_t n = 0;
-    for (int k = 0; k < K; ++k) {
-      auto it = pool.ranges.find(scans[k]);
-      const uint32_t cnt = it == pool.ranges.end() ? 0u : it->second.second;
-      const uint32_t po = it == pool.ranges.end() ? 0u : (uint32_t)it->second.first;
-      hs[k] = Seg{n, cnt, po, 0};
-      n += cnt;
-    }
+    const uint32_t n = nrec[t];
     M.n = n;
-    c->segs[t].ensure(std::max(K, 1));
-    // pinned staging owned by the map build (never reused before the next sync)
-    c->h_segs[t].ensure(std::max(K, 1));
-    std::memcpy(c->h_segs[t].p, hs.data(), sizeof(Seg) * std::max(K, 1));
-    FMX_HIP(hipMemcpyAsync(c->segs[t].p, c->h_segs[t].p, sizeof(Seg) * std::max(K, 1), hipMemcpyHostToDevice, st));
     const uint64_t use = next_pow2(std::max<uint64_t>(2ull * n, 1024));  // load factor <= 0.5
     M.table.ensure(use);
-    M.cursor.ensure(use);
     M.cap = use;
+    // zero the table (and, for t == 0, the range-error flag that follows the fill)
     FMX_HIP(hipMemsetAsync(M.table.p, 0, use * sizeof(Slot), st));
-    FMX_HIP(hipMemsetAsync(M.cursor.p, 0, use * sizeof(uint32_t), st));
+    if (t == 0) FMX_HIP(hipMemsetAsync(c->map_err.p, 0, 4, st));
     M.tpos.ensure(n + 1);
     M.rslot.ensure(n + 1);
     M.rseg.ensure(n + 1);
@@ -538,7 +555,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
     if (n > 0) {
       hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, pool.pos.p, pool.nrm.p, t == 0 ? 1 : 0,
-                         c->segs[t].p, K, c->map_poses.p, n, w, reinterpret_cast<Slot*>(M.table.p), use - 1,
+                         dseg + t * Kc, K, c->map_poses_p, n, w, reinterpret_cast<Slot*>(M.table.p), use - 1,
                          M.tpos.p, M.tnrm.p, M.rslot.p, M.rseg.p, c->map_err.p);
       FMX_HIP(hipGetLastError());
       c->scan_scratch.ensure(scan_scratch_size(use) + 4);
@@ -546,8 +563,8 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
       exclusive_scan(CountIn{reinterpret_cast<const Slot*>(M.table.p)}, FirstOut{reinterpret_cast<Slot*>(M.table.p)},
                      use, c->scan_scratch.p, c->dev_u32.p + 4, st);
       hipLaunchKernelGGL(k_map_scatter, dim3((n + 255) / 256), dim3(256), 0, st, n, M.rslot.p, M.rseg.p, M.tpos.p,
-                         M.tnrm.p, t == 0 ? 1 : 0, reinterpret_cast<const Slot*>(M.table.p), M.cursor.p, M.pos.p,
-                         M.nrm.p, M.seg.p, M.rid.p);
+                         M.tnrm.p, t == 0 ? 1 : 0, reinterpret_cast<Slot*>(M.table.p), M.pos.p, M.nrm.p, M.seg.p,
+                         M.rid.p);
       FMX_HIP(hipGetLastError());
     }
   }
@@ -555,11 +572,12 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   c->have_match = false;
 }
 
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map) {
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, const IcpDev* icp) {
   hipStream_t st = c->stream;
   const int K = std::max<int>((int)c->K, 1);
   MatchArgs a;
-  std::memcpy(a.Tj, pose_j34, sizeof(a.Tj));
+  if (pose_j34) std::memcpy(a.Tj, pose_j34, sizeof(a.Tj));
+  else std::memset(a.Tj, 0, sizeof(a.Tj));
   a.w = c->voxel_w;
   a.max_d2 = max_dist * max_dist;
   a.min_d2 = min_dist_map * min_dist_map;
@@ -580,6 +598,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->hist.ensure((size_t)(nb + 1) * K);
   c->hist_off.ensure((size_t)(nb + 1) * K);
   c->pair_counts.ensure(2 * (size_t)K);
+  c->h_counts.ensure(2 * (size_t)K + 4);
   c->pair_base.ensure(2 * (size_t)K);
   c->chunk_range.ensure(K + 1);
   const uint32_t maxch = c->n_qpl / kPlaneChunk + c->n_qpt / kPointChunk + 2 * K + 2;
@@ -604,33 +623,30 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   if (nb > 0) {
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
     hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
-                       c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_poses.p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
-                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p);
+                       c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
+                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, icp);
     FMX_HIP(hipGetLastError());
   }
   {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
     if (c->K > 0 && nb > 0) {
       hipLaunchKernelGGL(k_pair_colscan, dim3(c->K, 2), dim3(256), 0, st, c->hist.p, a.nb_pl, nb_pt, a.K,
-                         c->hist_off.p, c->pair_counts.p);
+                         c->hist_off.p, c->pair_counts.p, icp);
       FMX_HIP(hipGetLastError());
     } else if (c->K > 0) {
       FMX_HIP(hipMemsetAsync(c->pair_counts.p, 0, 2 * c->K * sizeof(uint32_t), st));
     }
     hipLaunchKernelGGL(k_pair_base, dim3(1), dim3(1024), 0, st, a.K, c->pair_counts.p, c->pair_base.p,
-                       c->chunk_range.p, c->chunks.p, c->n_chunks.p);
+                       c->chunk_range.p, c->chunks.p, c->n_chunks.p, icp, c->h_counts.d);
     FMX_HIP(hipGetLastError());
     if (nb > 0 && c->K > 0) {
       hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(64), 0, st, c->n_qpl, c->n_qpt, a.nb_pl, a.K, c->m_pair.p,
                          c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, c->pair_base.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt);
+                         c->ld_pl, c->c_pt.p, c->ld_pt, icp);
       FMX_HIP(hipGetLastError());
     }
   }
-  // per-pair counts + work counters to pinned host memory; consumed at the next sync
-  c->h_counts.ensure(2 * (size_t)K + 4);
-  if (c->K)
-    FMX_HIP(hipMemcpyAsync(c->h_counts.p, c->pair_counts.p, 2 * (size_t)c->K * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  // per-pair counts reach pinned host memory from k_pair_base; consumed at the next sync
   if (c->prof.on) {  // per-block work counters, only needed for the profile's byte model
     c->h_work.ensure(2 * (size_t)nb + 2);
     if (nb) FMX_HIP(hipMemcpyAsync(c->h_work.p, c->work.p, 2 * (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -643,7 +659,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
 // Consume the asynchronously copied match counts (caller has synchronized or will).
 void match_counts_fetch(fmx_ctx* c) {
   if (!c->counts_pending) return;
-  FMX_HIP(hipStreamSynchronize(c->stream));
+  stream_wait(c);
   const int K = std::max<int>((int)c->K, 1);
   c->cnt_pl.assign(c->h_counts.p, c->h_counts.p + c->K);
   c->cnt_pt.assign(c->h_counts.p + c->K, c->h_counts.p + 2 * c->K);
@@ -676,17 +692,17 @@ void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
     Pool& pool = c->pool[t];
     // worst case every query inserted
     if (pool.used + nq > pool.pos.cap) throw StatusError(FMX_E_OOM, "keypoint pool capacity exceeded");
-    c->scan_scratch.ensure(scan_scratch_size(nq) + 4);
+    c->scan_scratch_half = std::max<size_t>(scan_scratch_size(std::max(c->n_qpl, c->n_qpt)) + 4, 64);
+    c->scan_scratch.ensure(2 * c->scan_scratch_half);
     ProfScope ps(c->prof, PROF_INSERT, (t == 0 ? 33.0 : 17.0) * nq, st);
     if (t == 0)
       exclusive_scan(InsIn{f}, InsOutPl{f, c->q_pl_pos.p, c->q_pl_nrm.p, pool.pos.p + pool.used, pool.nrm.p + pool.used},
-                     nq, c->scan_scratch.p, c->dev_u32.p + t, st);
+                     nq, c->scan_scratch.p + t * c->scan_scratch_half, c->h_u32.d + t, st);
     else
-      exclusive_scan(InsIn{f}, InsOutPt{f, c->q_pt_pos.p, pool.pos.p + pool.used}, nq, c->scan_scratch.p,
-                     c->dev_u32.p + t, st);
+      exclusive_scan(InsIn{f}, InsOutPt{f, c->q_pt_pos.p, pool.pos.p + pool.used}, nq,
+                     c->scan_scratch.p + t * c->scan_scratch_half, c->h_u32.d + t, st);
   }
-  FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->dev_u32.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  FMX_HIP(hipStreamSynchronize(st));
+  stream_wait(c);
   for (int t = 0; t < 2; ++t) {
     tot[t] = (t == 0 ? c->n_qpl : c->n_qpt) ? c->h_u32.p[t] : 0u;
     Pool& pool = c->pool[t];
