@@ -339,6 +339,43 @@ void pool_add(fmx_ctx* c, int t, uint64_t scan, const float* f, uint32_t n) {
   pool.used += n;
 }
 
+// device float4 arrays -> pool under `scan`
+void pool_add_device(fmx_ctx* c, int t, uint64_t scan, const float* pos4, const float* nrm4, uint32_t n) {
+  if (n == 0) return;
+  ensure_pool_room(c, t, n);
+  Pool& pool = c->pool[t];
+  auto& rg = pool.ranges[scan];
+  if (rg.second == 0) rg.first = pool.used;
+  else if (rg.first + rg.second != pool.used) throw StatusError(FMX_E_STATE, "scan keypoints must be added contiguously");
+  FMX_HIP(hipMemcpyAsync(pool.pos.p + pool.used, pos4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+  if (t == 0)
+    FMX_HIP(hipMemcpyAsync(pool.nrm.p + pool.used, nrm4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+  rg.second += n;
+  pool.used += n;
+}
+
+void set_queries_device(fmx_ctx* c, uint64_t scan, const float* plp, const float* pln, uint32_t npl, const float* ptp,
+                        uint32_t npt) {
+  c->q_pl_pos.ensure(npl + 1);
+  c->q_pl_nrm.ensure(npl + 1);
+  c->q_pl_idx.ensure(npl + 1);
+  c->q_pt_pos.ensure(npt + 1);
+  c->q_pt_idx.ensure(npt + 1);
+  if (npl) {
+    FMX_HIP(hipMemcpyAsync(c->q_pl_pos.p, plp, npl * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    FMX_HIP(hipMemcpyAsync(c->q_pl_nrm.p, pln, npl * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (npt) FMX_HIP(hipMemcpyAsync(c->q_pt_pos.p, ptp, npt * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+  FMX_HIP(hipMemsetAsync(c->q_pl_idx.p, 0xFF, (npl + 1) * sizeof(uint32_t), c->stream));
+  FMX_HIP(hipMemsetAsync(c->q_pt_idx.p, 0xFF, (npt + 1) * sizeof(uint32_t), c->stream));
+  c->n_qpl = npl;
+  c->n_qpt = npt;
+  c->n_sel = npl;
+  c->q_scan = scan;
+  c->have_queries = true;
+  c->have_match = false;
+}
+
 void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const float* pt, uint32_t npt) {
   std::vector<float4> a(npl + 1), b(npl + 1), d(npt + 1);
   for (uint32_t i = 0; i < npl; ++i) {
@@ -855,6 +892,23 @@ fmx_status fmx_keypoints_add(fmx_ctx* c, uint64_t scan, const float* planar, uin
   });
 }
 
+fmx_status fmx_keypoints_add_device(fmx_ctx* c, uint64_t scan, const float* plp, const float* pln, uint32_t npl,
+                                    const float* ptp, uint32_t npt) {
+  return guard(c, [&] {
+    if ((npl && (!plp || !pln)) || (npt && !ptp)) throw StatusError(FMX_E_INVAL, "null features");
+    pool_add_device(c, 0, scan, plp, pln, npl);
+    pool_add_device(c, 1, scan, ptp, nullptr, npt);
+  });
+}
+
+fmx_status fmx_set_queries_device(fmx_ctx* c, uint64_t scan, const float* plp, const float* pln, uint32_t npl,
+                                  const float* ptp, uint32_t npt) {
+  return guard(c, [&] {
+    if ((npl && (!plp || !pln)) || (npt && !ptp)) throw StatusError(FMX_E_INVAL, "null features");
+    set_queries_device(c, scan, plp, pln, npl, ptp, npt);
+  });
+}
+
 fmx_status fmx_keypoints_remove(fmx_ctx* c, uint64_t scan) {
   return guard(c, [&] { remove_scan(c, scan); });
 }
@@ -966,6 +1020,15 @@ fmx_status fmx_current_pose(fmx_ctx* c, double pose[12]) {
 
 fmx_status fmx_last_stats(fmx_ctx* c, uint64_t stats[8]) {
   return guard(c, [&] { std::memcpy(stats, c->stats, sizeof(c->stats)); });
+}
+
+fmx_status fmx_match_work(fmx_ctx* c, double work[3]) {
+  return guard(c, [&] {
+    match_counts_fetch(c);
+    work[0] = (double)c->n_qpl + (double)c->n_qpt;
+    work[1] = c->last_probes;
+    work[2] = c->last_cands;
+  });
 }
 
 fmx_status fmx_profile_enable(fmx_ctx* c, int on) {

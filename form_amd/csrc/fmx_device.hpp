@@ -143,12 +143,56 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(In in, Out out, siz
   }
 }
 
+// One workgroup scans the whole array tile by tile (coalesced, carry in LDS): one
+// launch instead of three, for arrays up to kScanSingleMax.
+constexpr size_t kScanSingleMax = (size_t)kScanTile * 4;
+template <class In, class Out>
+__global__ __launch_bounds__(kScanThreads) void k_scan_single(In in, Out out, size_t n, uint32_t* total) {
+  __shared__ uint32_t ws[kScanThreads / kWave];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int w = threadIdx.x / kWave;
+  for (size_t t0 = 0; t0 < n; t0 += kScanTile) {
+    const size_t base = t0 + (size_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      v[j] = base + j < n ? in(base + j) : 0u;
+      s += v[j];
+    }
+    const uint32_t incl = wave_incl_scan(s);
+    if (lane_id() == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < kScanThreads / kWave; ++i) {
+      if (i < w) off += ws[i];
+      tot += ws[i];
+    }
+    uint32_t run = carry + off + incl - s;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      if (base + j < n) out(base + j, run);
+      run += v[j];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
 template <class In, class Out>
 inline void exclusive_scan(In in, Out out, size_t n, uint32_t* scratch /* >= nb */, uint32_t* total,
                            hipStream_t st) {
   const uint32_t nb = (uint32_t)((n + kScanTile - 1) / kScanTile);
   if (nb == 0) {
     (void)hipMemsetAsync(total, 0, sizeof(uint32_t), st);
+    return;
+  }
+  if (n <= kScanSingleMax) {
+    k_scan_single<In, Out><<<1, kScanThreads, 0, st>>>(in, out, n, total);
     return;
   }
   k_scan_reduce<In><<<nb, kScanThreads, 0, st>>>(in, n, scratch);

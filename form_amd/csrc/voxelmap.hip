@@ -131,7 +131,7 @@ struct MatchArgs {
   double w;
   double bound;  // prune bound on d^2 (+inf: no pruning)
   double max_d2, min_d2;
-  uint32_t nq_pl, nq_pt, nb_pl;  // queries; planar blocks
+  uint32_t nq_pl, nq_pt, nb_pl, nb_pt;  // queries; planar / point blocks
   int K;
 };
 
@@ -228,42 +228,48 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       for (uint32_t i = first + g; i < first + count; i += kGroup) test(i);
     }
     group_min();  // every lane now holds the own-voxel best: the bound for phase 2
-    // phase 2: the other 26 voxels.  Lane g bounds and probes shifts g+1, g+1+kGroup,
-    // ... (<= 4) in parallel; then the group walks every surviving voxel together
+    // phase 2: the other 26 voxels in two passes — the 6 face neighbours (shifts
+    // 1..6, the smallest lower bounds), then the 12 edges + 8 corners (7..26) pruned
+    // against the best found so far.  In each pass a lane bounds and probes its
+    // shifts in parallel, then the group walks every surviving voxel together
     // (records split over the lanes), re-checking each bound against the shared best.
-    constexpr int kPer = (26 + kGroup - 1) / kGroup;
-    uint32_t vf[kPer], vc[kPer];
-    double vlb[kPer];
+    auto pass = [&](int s_begin, int s_end) {
+      constexpr int kPer = (20 + kGroup - 1) / kGroup;
+      uint32_t vf[kPer], vc[kPer];
+      double vlb[kPer];
 #pragma unroll
-    for (int t = 0; t < kPer; ++t) {
-      vc[t] = 0;
-      vf[t] = 0;
-      vlb[t] = INFINITY;
-      const int s = 1 + g + t * kGroup;
-      if (!inr || s >= 27) continue;
-      const int sx = c_shift[s][0], sy = c_shift[s][1], sz = c_shift[s][2];
-      const double ex = sx < 0 ? lo[0] : (sx > 0 ? hi[0] : 0.0);
-      const double ey = sy < 0 ? lo[1] : (sy > 0 ? hi[1] : 0.0);
-      const double ez = sz < 0 ? lo[2] : (sz > 0 ? hi[2] : 0.0);
-      const double mx = fmax(ex - 1e-9, 0.0), my = fmax(ey - 1e-9, 0.0), mz = fmax(ez - 1e-9, 0.0);
-      const double lb = mx * mx + my * my + mz * mz;
-      if (lb > best) continue;  // conservative: no point inside can win
-      probe(sx, sy, sz, vf[t], vc[t]);
-      vlb[t] = lb;
-    }
-#pragma unroll
-    for (int t = 0; t < kPer; ++t) {
-      for (int l = 0; l < kGroup; ++l) {
-        const uint32_t cnt = __shfl(vc[t], l, kGroup);
-        if (cnt == 0) continue;
-        const double lb = __shfl(vlb[t], l, kGroup);
-        if (lb > best) continue;  // best is group-uniform here
-        const uint32_t first = __shfl(vf[t], l, kGroup);
-        n_cand += cnt / kGroup + (g < (int)(cnt % kGroup) ? 1 : 0);
-        for (uint32_t i = first + g; i < first + cnt; i += kGroup) test(i);
-        group_min();
+      for (int t = 0; t < kPer; ++t) {
+        vc[t] = 0;
+        vf[t] = 0;
+        vlb[t] = INFINITY;
+        const int s = s_begin + g + t * kGroup;
+        if (!inr || s >= s_end) continue;
+        const int sx = c_shift[s][0], sy = c_shift[s][1], sz = c_shift[s][2];
+        const double ex = sx < 0 ? lo[0] : (sx > 0 ? hi[0] : 0.0);
+        const double ey = sy < 0 ? lo[1] : (sy > 0 ? hi[1] : 0.0);
+        const double ez = sz < 0 ? lo[2] : (sz > 0 ? hi[2] : 0.0);
+        const double mx = fmax(ex - 1e-9, 0.0), my = fmax(ey - 1e-9, 0.0), mz = fmax(ez - 1e-9, 0.0);
+        const double lb = mx * mx + my * my + mz * mz;
+        if (lb > best) continue;  // conservative: no point inside can win
+        probe(sx, sy, sz, vf[t], vc[t]);
+        vlb[t] = lb;
       }
-    }
+#pragma unroll
+      for (int t = 0; t < kPer; ++t) {
+        for (int l = 0; l < kGroup; ++l) {
+          const uint32_t cnt = __shfl(vc[t], l, kGroup);
+          if (cnt == 0) continue;
+          const double lb = __shfl(vlb[t], l, kGroup);
+          if (lb > best) continue;  // best is group-uniform here
+          const uint32_t first = __shfl(vf[t], l, kGroup);
+          n_cand += cnt / kGroup + (g < (int)(cnt % kGroup) ? 1 : 0);
+          for (uint32_t i = first + g; i < first + cnt; i += kGroup) test(i);
+          group_min();
+        }
+      }
+    };
+    pass(1, 7);
+    pass(7, 27);
     if (g == 0) {
       const bool found = best_i != 0xFFFFFFFFu;
       int32_t pair = -1;
@@ -309,94 +315,102 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     work[2 * blockIdx.x] = tp;
     work[2 * blockIdx.x + 1] = tc;
   }
-  for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[(size_t)blockIdx.x * a.K + k] = s_hist[k];
+  // pair-major layout [type][pair][block]: one exclusive scan gives every block's
+  // destination offset (k_pair_base / k_pair_scatter)
+  const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.nb_pl;
+  const uint32_t nbt = planar ? a.nb_pl : a.nb_pt;
+  const uint32_t bt = planar ? blockIdx.x : blockIdx.x - a.nb_pl;
+  for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[hbase + (size_t)k * nbt + bt] = s_hist[k];
 }
 
-// Per (pair, type): exclusive scan of the block histograms over blocks -> rank
-// offsets of each block within that pair, plus the pair total.  Grid (K, 2).
-__global__ __launch_bounds__(256) void k_pair_colscan(const uint32_t* __restrict__ hist, uint32_t nb_pl, uint32_t nb_pt,
-                                                      int K, uint32_t* __restrict__ hist_off,
-                                                      uint32_t* __restrict__ pair_counts, const IcpDev* __restrict__ icp) {
-  if (icp && icp->icp_done) return;
-  __shared__ uint32_t ws[4];
+struct HistIn {
+  const uint32_t* h;
+  __device__ uint32_t operator()(size_t i) const { return h[i]; }
+};
+struct HistOut {
+  uint32_t* o;
+  __device__ void operator()(size_t i, uint32_t v) const { o[i] = v; }
+};
+
+// One block: from the scanned pair-major histogram, per-pair counts and first rows
+// (per type), host copy of the counts, and the linearize chunk table (pair-major:
+// plane chunks then point chunks of each pair).
+__global__ __launch_bounds__(1024) void k_pair_base(int K, uint32_t nb_pl, uint32_t nb_pt,
+                                                    const uint32_t* __restrict__ hoff, const uint32_t* __restrict__ total,
+                                                    uint32_t* __restrict__ pair_counts, uint32_t* __restrict__ pair_base,
+                                                    uint32_t* __restrict__ chunk_range, Chunk* __restrict__ chunks,
+                                                    uint32_t* __restrict__ n_chunks, const IcpDev* __restrict__ icp,
+                                                    uint32_t* __restrict__ host_counts) {
+  __shared__ uint32_t ws[16];
   __shared__ uint32_t carry;
-  const int k = blockIdx.x, t = blockIdx.y;
-  const uint32_t b0 = t == 0 ? 0 : nb_pl, nb = t == 0 ? nb_pl : nb_pt;
+  if (icp && icp->icp_done) return;
+  const size_t npl_all = (size_t)K * nb_pl, n_all = npl_all + (size_t)K * nb_pt;
+  // start offset of section (t, k) in the scanned array; sections of empty types
+  // (nb = 0) start where the next section starts
+  auto sec = [&](int t, int k) -> uint32_t {
+    const size_t i = t == 0 ? (size_t)k * nb_pl : npl_all + (size_t)k * nb_pt;
+    return i < n_all ? hoff[i] : *total;
+  };
+  const uint32_t tot_pl = K > 0 ? sec(1, 0) : 0u;  // planar total = start of the point part
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
-  for (uint32_t c0 = 0; c0 < nb; c0 += 256) {
-    const uint32_t b = c0 + threadIdx.x;
-    const uint32_t v = b < nb ? hist[(size_t)(b0 + b) * K + k] : 0u;
-    const uint32_t incl = wave_incl_scan(v);
+  for (int k0 = 0; k0 < K; k0 += 1024) {
+    const int k = k0 + threadIdx.x;
+    uint32_t npl = 0, npt = 0, b_pl = 0, b_pt = 0;
+    if (k < K) {
+      b_pl = sec(0, k);
+      const uint32_t e_pl = k + 1 < K ? sec(0, k + 1) : tot_pl;
+      b_pt = sec(1, k);
+      const uint32_t e_pt = k + 1 < K ? sec(1, k + 1) : *total;
+      npl = e_pl - b_pl;
+      npt = e_pt - b_pt;
+      b_pt -= tot_pl;
+      pair_counts[k] = npl;
+      pair_counts[K + k] = npt;
+      host_counts[k] = npl;  // mapped host memory
+      host_counts[K + k] = npt;
+      pair_base[k] = b_pl;
+      pair_base[K + k] = b_pt;
+    }
+    const uint32_t nch = (npl + kPlaneChunk - 1) / kPlaneChunk + (npt + kPointChunk - 1) / kPointChunk;
+    const uint32_t incl = wave_incl_scan(nch);
     const int w = threadIdx.x / kWave;
     if (lane_id() == 63) ws[w] = incl;
     __syncthreads();
     uint32_t off = 0, tot = 0;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 16; ++i) {
       if (i < w) off += ws[i];
       tot += ws[i];
     }
-    if (b < nb) hist_off[(size_t)(b0 + b) * K + k] = carry + off + incl - v;
+    if (k < K) chunk_range[k] = carry + off + incl - nch;
     __syncthreads();
     if (threadIdx.x == 0) carry += tot;
     __syncthreads();
   }
-  if (threadIdx.x == 0) pair_counts[t * K + k] = carry;
-}
-
-// One block: pair bases (exclusive scan of the totals per type) and the linearize
-// chunk table (pair-major: plane chunks then point chunks of each pair).
-__global__ __launch_bounds__(1024) void k_pair_base(int K, const uint32_t* __restrict__ pair_counts,
-                                                    uint32_t* __restrict__ pair_base, uint32_t* __restrict__ chunk_range,
-                                                    Chunk* __restrict__ chunks, uint32_t* __restrict__ n_chunks,
-                                                    const IcpDev* __restrict__ icp, uint32_t* __restrict__ host_counts) {
-  if (icp && icp->icp_done) return;
-  for (int i = threadIdx.x; i < 2 * K; i += 1024) host_counts[i] = pair_counts[i];  // mapped host memory
-  __shared__ uint32_t ws[16];
-  __shared__ uint32_t carry[3];
-  if (threadIdx.x < 3) carry[threadIdx.x] = 0;
+  if (threadIdx.x == 0) chunk_range[K] = carry;
   __syncthreads();
-  for (int k0 = 0; k0 < K; k0 += 1024) {
-    const int k = k0 + threadIdx.x;
-    uint32_t npl = 0, npt = 0;
-    if (k < K) {
-      npl = pair_counts[k];
-      npt = pair_counts[K + k];
+  // descriptors, every thread a strided share: chunk -> pair by binary search
+  const uint32_t nch_all = carry;
+  for (uint32_t ci = threadIdx.x; ci < nch_all; ci += 1024) {
+    int lo = 0, hi = K - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (chunk_range[mid] <= ci) lo = mid;
+      else hi = mid - 1;
     }
-    const uint32_t nch = (npl + kPlaneChunk - 1) / kPlaneChunk + (npt + kPointChunk - 1) / kPointChunk;
-    uint32_t ex[3];
-    const uint32_t vals[3] = {npl, npt, nch};
-    const int w = threadIdx.x / kWave;
-    for (int t = 0; t < 3; ++t) {
-      const uint32_t incl = wave_incl_scan(vals[t]);
-      if (lane_id() == 63) ws[w] = incl;
-      __syncthreads();
-      uint32_t off = 0, tot = 0;
-      for (int i = 0; i < 16; ++i) {
-        if (i < w) off += ws[i];
-        tot += ws[i];
-      }
-      ex[t] = carry[t] + off + incl - vals[t];
-      __syncthreads();
-      if (threadIdx.x == 0) carry[t] += tot;
-      __syncthreads();
-    }
-    if (k < K) {
-      pair_base[k] = ex[0];
-      pair_base[K + k] = ex[1];
-      uint32_t cb = ex[2];
-      chunk_range[k] = cb;
-      for (uint32_t r = 0; r < npl; r += kPlaneChunk)
-        chunks[cb++] = Chunk{0, (uint32_t)k, ex[0] + r, ex[0] + min(npl, r + kPlaneChunk)};
-      for (uint32_t r = 0; r < npt; r += kPointChunk)
-        chunks[cb++] = Chunk{1, (uint32_t)k, ex[1] + r, ex[1] + min(npt, r + kPointChunk)};
+    const int k = lo;
+    const uint32_t j = ci - chunk_range[k];
+    const uint32_t npl = pair_counts[k], npt = pair_counts[K + k];
+    const uint32_t ncpl = (npl + kPlaneChunk - 1) / kPlaneChunk;
+    if (j < ncpl) {
+      const uint32_t r = j * kPlaneChunk, b_pl = pair_base[k];
+      chunks[ci] = Chunk{0, (uint32_t)k, b_pl + r, b_pl + min(npl, r + kPlaneChunk)};
+    } else {
+      const uint32_t r = (j - ncpl) * kPointChunk, b_pt = pair_base[K + k];
+      chunks[ci] = Chunk{1, (uint32_t)k, b_pt + r, b_pt + min(npt, r + kPointChunk)};
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    chunk_range[K] = carry[2];
-    *n_chunks = carry[2];
-  }
+  if (threadIdx.x == 0) *n_chunks = nch_all;
 }
 
 // Stable scatter of accepted matches into pair-major SoA correspondences:
@@ -408,7 +422,7 @@ __global__ __launch_bounds__(64) void k_pair_scatter(uint32_t nq_pl, uint32_t nq
                                                      const float4* __restrict__ q_pl,
                                                      const float4* __restrict__ q_pt,
                                                      const uint32_t* __restrict__ hist_off,
-                                                     const uint32_t* __restrict__ pair_base,
+                                                     uint32_t nb_pt, const uint32_t* __restrict__ pair_base,
                                                      double* __restrict__ c_pl, size_t ld_pl,
                                                      double* __restrict__ c_pt, size_t ld_pt,
                                                      const IcpDev* __restrict__ icp) {
@@ -430,7 +444,13 @@ __global__ __launch_bounds__(64) void k_pair_scatter(uint32_t nq_pl, uint32_t nq
   }
   if (pair < 0) return;
   const int t = planar ? 0 : 1;
-  const uint32_t dst = pair_base[t * K + pair] + hist_off[(size_t)blockIdx.x * K + pair] + rank;
+  // pair-major scanned histogram; the point part is relative to the planar total
+  const size_t npl_all = (size_t)K * nb_pl;
+  const uint32_t tot_pl = nb_pt ? hist_off[npl_all] : 0u;  // exclusive prefix at the point section = planar total
+  const uint32_t dst = planar ? hist_off[(size_t)pair * nb_pl + blockIdx.x] + rank
+                              : hist_off[npl_all + (size_t)pair * nb_pt + (blockIdx.x - nb_pl)] - tot_pl + rank;
+  (void)pair_base;
+  (void)t;
   const size_t gq = planar ? qi : nq_pl + qi;
   const double4 pi = m_pi[gq];
   if (planar) {
@@ -587,6 +607,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
   const uint32_t nb_pt = (c->n_qpt + kQPB - 1) / kQPB;
+  a.nb_pt = nb_pt;
   a.K = (int)c->K;
   const uint32_t nq = c->n_qpl + c->n_qpt;
   c->m_pair.ensure(nq + 1);
@@ -629,20 +650,19 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   }
   {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
-    if (c->K > 0 && nb > 0) {
-      hipLaunchKernelGGL(k_pair_colscan, dim3(c->K, 2), dim3(256), 0, st, c->hist.p, a.nb_pl, nb_pt, a.K,
-                         c->hist_off.p, c->pair_counts.p, icp);
-      FMX_HIP(hipGetLastError());
-    } else if (c->K > 0) {
-      FMX_HIP(hipMemsetAsync(c->pair_counts.p, 0, 2 * c->K * sizeof(uint32_t), st));
-    }
-    hipLaunchKernelGGL(k_pair_base, dim3(1), dim3(1024), 0, st, a.K, c->pair_counts.p, c->pair_base.p,
-                       c->chunk_range.p, c->chunks.p, c->n_chunks.p, icp, c->h_counts.d);
+    const size_t nh = (size_t)a.K * nb;
+    c->scan_scratch.ensure(scan_scratch_size(nh) + 4);
+    c->dev_u32.ensure(8);
+    if (nh > 0) exclusive_scan(HistIn{c->hist.p}, HistOut{c->hist_off.p}, nh, c->scan_scratch.p, c->dev_u32.p + 5, st);
+    else FMX_HIP(hipMemsetAsync(c->dev_u32.p + 5, 0, 4, st));
+    hipLaunchKernelGGL(k_pair_base, dim3(1), dim3(1024), 0, st, a.K, a.nb_pl, nb_pt, c->hist_off.p, c->dev_u32.p + 5,
+                       c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p, icp,
+                       c->h_counts.d);
     FMX_HIP(hipGetLastError());
     if (nb > 0 && c->K > 0) {
       hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(64), 0, st, c->n_qpl, c->n_qpt, a.nb_pl, a.K, c->m_pair.p,
-                         c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, c->pair_base.p, c->c_pl.p,
-                         c->ld_pl, c->c_pt.p, c->ld_pt, icp);
+                         c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, nb_pt, c->pair_base.p,
+                         c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt, icp);
       FMX_HIP(hipGetLastError());
     }
   }

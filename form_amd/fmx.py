@@ -75,10 +75,11 @@ def lib():
 
 EXPORTED = [
     "fmx_abi_version", "fmx_default_params", "fmx_create", "fmx_destroy", "fmx_last_error",
-    "fmx_extract", "fmx_extract_download", "fmx_set_queries", "fmx_keypoints_add",
+    "fmx_extract", "fmx_extract_download", "fmx_set_queries", "fmx_set_queries_device", "fmx_keypoints_add",
+    "fmx_keypoints_add_device",
     "fmx_keypoints_remove", "fmx_map_build", "fmx_match", "fmx_match_download", "fmx_map_insert",
     "fmx_corr_set", "fmx_linearize", "fmx_error", "fmx_register_scan", "fmx_current_pose",
-    "fmx_last_stats", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
+    "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
     "fmx_profile_name", "fmx_profile_read", "fmx_sync",
 ]
 
@@ -203,7 +204,23 @@ class Context:
                                           _p(point), C.c_uint32(len(point))))
         self.n_planar, self.n_point = len(planar), len(point)
 
+    def set_queries_device(self, planar_pos4, planar_nrm4, point_pos4=None, scan_idx: int = 0):
+        """Device-resident queries: (N,4) float32 CUDA tensors."""
+        npt = 0 if point_pos4 is None else point_pos4.shape[0]
+        pp = C.c_void_p(point_pos4.data_ptr()) if npt else None
+        self._chk(self._L.fmx_set_queries_device(self.h, C.c_uint64(scan_idx), C.c_void_p(planar_pos4.data_ptr()),
+                                                 C.c_void_p(planar_nrm4.data_ptr()), C.c_uint32(planar_pos4.shape[0]),
+                                                 pp, C.c_uint32(npt)))
+        self.n_planar, self.n_point = planar_pos4.shape[0], npt
+
     # ---------------------------------------------------------------- stage 2
+    def keypoints_add_device(self, scan_idx: int, planar_pos4, planar_nrm4, point_pos4=None):
+        npt = 0 if point_pos4 is None else point_pos4.shape[0]
+        pp = C.c_void_p(point_pos4.data_ptr()) if npt else None
+        self._chk(self._L.fmx_keypoints_add_device(self.h, C.c_uint64(scan_idx), C.c_void_p(planar_pos4.data_ptr()),
+                                                   C.c_void_p(planar_nrm4.data_ptr()), C.c_uint32(planar_pos4.shape[0]),
+                                                   pp, C.c_uint32(npt)))
+
     def keypoints_add(self, scan_idx: int, planar: np.ndarray, point: np.ndarray):
         planar = np.ascontiguousarray(planar, np.float32).reshape(-1, 6)
         point = np.ascontiguousarray(point, np.float32).reshape(-1, 3)
@@ -288,6 +305,11 @@ class Context:
         keys = ["icp_iters", "lm_iters", "matched_planar", "matched_point", "map_planar", "map_point",
                 "linearizations", "map_scans"]
         return {k: int(v) for k, v in zip(keys, s)}
+
+    def match_work(self) -> dict:
+        w = np.zeros(3)
+        self._chk(self._L.fmx_match_work(self.h, _p(w)))
+        return dict(queries=float(w[0]), probes=float(w[1]), candidates=float(w[2]))
 
     # ---------------------------------------------------------------- profiling
     def profile(self, on: bool = True):

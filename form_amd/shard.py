@@ -107,7 +107,9 @@ def make_queries(pos4, nrm4, n_query: int, offset: np.ndarray, noise: float, see
     sensor offset by `offset` (3x4): q_local = offset^-1 * (p + e)."""
     dev = pos4.device
     g = torch.Generator(device="cpu").manual_seed(seed)
-    sel = torch.randperm(pos4.shape[0], generator=g)[:n_query].to(dev)
+    # a random subset of the map features, kept in map (grid) order: a LiDAR scan's
+    # points arrive spatially coherent, not shuffled
+    sel = torch.randperm(pos4.shape[0], generator=g)[:n_query].sort().values.to(dev)
     p = pos4[sel, :3].double() + noise * torch.randn((n_query, 3), generator=g, dtype=torch.float64).to(dev)
     R = torch.as_tensor(offset[:, :3], dtype=torch.float64, device=dev)
     t = torch.as_tensor(offset[:, 3], dtype=torch.float64, device=dev)

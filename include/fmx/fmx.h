@@ -107,11 +107,21 @@ fmx_status fmx_extract_download(fmx_ctx* ctx, float* planar, uint32_t* planar_in
 fmx_status fmx_set_queries(fmx_ctx* ctx, uint64_t scan_idx, const float* planar, uint32_t n_planar,
                            const float* point, uint32_t n_point);
 
+/* Device-resident variants (no host round trip): float4 arrays (x, y, z, pad) that
+ * already live on the context's device; normals likewise.  Same semantics as
+ * fmx_set_queries / fmx_keypoints_add. */
+fmx_status fmx_set_queries_device(fmx_ctx* ctx, uint64_t scan_idx, const float* planar_pos4,
+                                  const float* planar_nrm4, uint32_t n_planar, const float* point_pos4,
+                                  uint32_t n_point);
+
 /* ---------------- stage 2: KeypointMap / VoxelMap / Matcher ---------------
  * Window keypoint store: KeypointMap::get(scan).push_back / insert_matches /
  * remove (map.tpp:95-126, 148-165).  Features are in the scan's local frame. */
 fmx_status fmx_keypoints_add(fmx_ctx* ctx, uint64_t scan_idx, const float* planar,
                              uint32_t n_planar, const float* point, uint32_t n_point);
+fmx_status fmx_keypoints_add_device(fmx_ctx* ctx, uint64_t scan_idx, const float* planar_pos4,
+                                    const float* planar_nrm4, uint32_t n_planar, const float* point_pos4,
+                                    uint32_t n_point);
 fmx_status fmx_keypoints_remove(fmx_ctx* ctx, uint64_t scan_idx);
 /* KeypointMap::to_voxel_map for both feature types (map.tpp:128-146, form.cpp:61-65):
  * builds the device voxel hash of every stored keypoint of scans[0..n) at the given
@@ -161,8 +171,11 @@ fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, i
 fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
 
 /* Statistics of the last register_scan: {icp_iters, lm_iters, matched_planar,
- * matched_point, map_planar, map_point, voxels_planar, voxels_point}. */
+ * matched_point, map_planar, map_point, linearizations, map_scans}. */
 fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t stats[8]);
+/* Work of the last fmx_match (counted by the kernel, available while profiling is
+ * enabled): queries, hash probes, candidate records distance-tested. */
+fmx_status fmx_match_work(fmx_ctx* ctx, double work[3]);
 
 /* ---------------- profiling (bench.py roofline) ----------------------------
  * When enabled, each kernel launch is bracketed by HIP events on the context
