@@ -47,6 +47,7 @@ def parse():
                     help="extra steps, after the timed ones, with per-kernel HIP-event timing (roofline); "
                          "default = --steps.  The timed region itself runs without event overhead.")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--subdiv", type=int, default=None, help="override voxel_subdivision (device map cells per voxel edge)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     return ap.parse_args()
@@ -126,7 +127,7 @@ def run_c5(a, rank, world, local):
     q4, n4 = shard.make_queries(pos4, nrm4, a.c5_queries, Ttrue, 0.05, synth.SEED + 1)
     b, e = shard.shard_bounds(a.c5_queries, rank, world)
     n_map = pos4.shape[0]
-    prm = fmx.EstimatorParams(keypoint_pool_capacity=n_map + 1024)
+    prm = fmx.EstimatorParams(keypoint_pool_capacity=n_map + 1024, voxel_subdivision=a.subdiv or 1)  # one record per voxel
     ctx = fmx.Context(prm, device=local)
     ctx.keypoints_add_device(0, pos4, nrm4)
     I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
@@ -214,7 +215,8 @@ def main():
     scans = [synth.raycast(world_obj, synth.trajectory_pose(k0 + k), geo, synth.SEED + 7919 * (k0 + k + 1), dev)
              for k in range(total)]
     torch.cuda.synchronize()
-    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params)), device=local)
+    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params),
+                                          voxel_subdivision=a.subdiv or 0), device=local)
     for k in range(a.warmup):
         ctx.register_scan(scans[k])
     ctx.sync()

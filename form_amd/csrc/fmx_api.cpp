@@ -775,6 +775,7 @@ void fmx_default_params(fmx_params* p) {
   p->min_dist_map = 0.1;  // map.hpp:97-100
   p->keypoint_pool_capacity = 4u << 20;
   p->max_pairs = 1024;
+  p->voxel_subdivision = 1;
 }
 
 fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {

@@ -193,7 +193,9 @@ struct fmx_ctx {
   fmx::DBuf<double> map_blob;                  // poses [K][12], inverses [K][12], segments
   const double* map_poses_p = nullptr;
   const double* map_inv_p = nullptr;
-  double voxel_w = 0;
+  double voxel_w = 0;   // reference voxel width (max_dist_matching)
+  double cell_w = 0;    // internal cell width of the built map
+  int cell_m = 1;       // subdivision: rings searched
   bool have_map = false;
   fmx::DBuf<uint32_t> map_err;
 

@@ -27,6 +27,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 namespace fmx {
 namespace {
@@ -120,15 +121,35 @@ struct MapView {
   const uint32_t* rid;
 };
 
-__device__ __constant__ int c_shift[27][3] = {
-    {0, 0, 0},   {1, 0, 0},   {-1, 0, 0},  {0, 1, 0},   {0, -1, 0},  {0, 0, 1},  {0, 0, -1},
-    {1, 1, 0},   {1, -1, 0},  {-1, 1, 0},  {-1, -1, 0}, {1, 0, 1},   {1, 0, -1}, {-1, 0, 1},
-    {-1, 0, -1}, {0, 1, 1},   {0, 1, -1},  {0, -1, 1},  {0, -1, -1}, {1, 1, 1},  {1, 1, -1},
-    {1, -1, 1},  {1, -1, -1}, {-1, 1, 1},  {-1, 1, -1}, {-1, -1, 1}, {-1, -1, -1}};
+// Cell shifts searched around the query's cell: [0] own cell, [1,7) the 6 face
+// neighbours and [7,27) the 12 edges + 8 corners — the first 27 in the reference's
+// fixed order (map.tpp:54-68) — then [27,125) the 98 cells of ring 2, used when the
+// map is built on cells of w/2 (ring 2 is then still within the bound w).
+__device__ __constant__ int c_shift[125][3] = {
+    {0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1},
+    {1, 1, 0}, {1, -1, 0}, {-1, 1, 0}, {-1, -1, 0}, {1, 0, 1}, {1, 0, -1}, {-1, 0, 1},
+    {-1, 0, -1}, {0, 1, 1}, {0, 1, -1}, {0, -1, 1}, {0, -1, -1}, {1, 1, 1}, {1, 1, -1},
+    {1, -1, 1}, {1, -1, -1}, {-1, 1, 1}, {-1, 1, -1}, {-1, -1, 1}, {-1, -1, -1}, {-2, 0, 0},
+    {0, -2, 0}, {0, 0, -2}, {0, 0, 2}, {0, 2, 0}, {2, 0, 0}, {-2, -1, 0}, {-2, 0, -1},
+    {-2, 0, 1}, {-2, 1, 0}, {-1, -2, 0}, {-1, 0, -2}, {-1, 0, 2}, {-1, 2, 0}, {0, -2, -1},
+    {0, -2, 1}, {0, -1, -2}, {0, -1, 2}, {0, 1, -2}, {0, 1, 2}, {0, 2, -1}, {0, 2, 1},
+    {1, -2, 0}, {1, 0, -2}, {1, 0, 2}, {1, 2, 0}, {2, -1, 0}, {2, 0, -1}, {2, 0, 1},
+    {2, 1, 0}, {-2, -1, -1}, {-2, -1, 1}, {-2, 1, -1}, {-2, 1, 1}, {-1, -2, -1}, {-1, -2, 1},
+    {-1, -1, -2}, {-1, -1, 2}, {-1, 1, -2}, {-1, 1, 2}, {-1, 2, -1}, {-1, 2, 1}, {1, -2, -1},
+    {1, -2, 1}, {1, -1, -2}, {1, -1, 2}, {1, 1, -2}, {1, 1, 2}, {1, 2, -1}, {1, 2, 1},
+    {2, -1, -1}, {2, -1, 1}, {2, 1, -1}, {2, 1, 1}, {-2, -2, 0}, {-2, 0, -2}, {-2, 0, 2},
+    {-2, 2, 0}, {0, -2, -2}, {0, -2, 2}, {0, 2, -2}, {0, 2, 2}, {2, -2, 0}, {2, 0, -2},
+    {2, 0, 2}, {2, 2, 0}, {-2, -2, -1}, {-2, -2, 1}, {-2, -1, -2}, {-2, -1, 2}, {-2, 1, -2},
+    {-2, 1, 2}, {-2, 2, -1}, {-2, 2, 1}, {-1, -2, -2}, {-1, -2, 2}, {-1, 2, -2}, {-1, 2, 2},
+    {1, -2, -2}, {1, -2, 2}, {1, 2, -2}, {1, 2, 2}, {2, -2, -1}, {2, -2, 1}, {2, -1, -2},
+    {2, -1, 2}, {2, 1, -2}, {2, 1, 2}, {2, 2, -1}, {2, 2, 1}, {-2, -2, -2}, {-2, -2, 2},
+    {-2, 2, -2}, {-2, 2, 2}, {2, -2, -2}, {2, -2, 2}, {2, 2, -2}, {2, 2, 2},
+};
 
 struct MatchArgs {
   double Tj[12];
-  double w;
+  double w;       // cell width of the built map (voxel width / subdivision)
+  int rings;      // neighbour rings to search (= subdivision)
   double bound;  // prune bound on d^2 (+inf: no pruning)
   double max_d2, min_d2;
   uint32_t nq_pl, nq_pt, nb_pl, nb_pt;  // queries; planar / point blocks
@@ -228,40 +249,40 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       for (uint32_t i = first + g; i < first + count; i += kGroup) test(i);
     }
     group_min();  // every lane now holds the own-voxel best: the bound for phase 2
-    // phase 2: the other 26 voxels in two passes — the 6 face neighbours (shifts
-    // 1..6, the smallest lower bounds), then the 12 edges + 8 corners (7..26) pruned
-    // against the best found so far.  In each pass a lane bounds and probes its
-    // shifts in parallel, then the group walks every surviving voxel together
-    // (records split over the lanes), re-checking each bound against the shared best.
+    // phase 2: the neighbour cells in passes of increasing lower bound — ring-1 faces
+    // (shifts 1..6), ring-1 edges + corners (7..26), then ring 2 (27..124) when the
+    // map uses half-width cells — each pass pruned against the best found so far.  In
+    // a pass a lane bounds and probes its shifts in parallel, then the group walks
+    // every surviving cell together (records split over the lanes), re-checking each
+    // bound against the shared best.
     auto pass = [&](int s_begin, int s_end) {
-      constexpr int kPer = (20 + kGroup - 1) / kGroup;
-      uint32_t vf[kPer], vc[kPer];
-      double vlb[kPer];
+      for (int s0 = s_begin; s0 < s_end; s0 += kGroup) {  // one shift per lane per chunk
+        uint32_t vf = 0, vc = 0;
+        double vlb = INFINITY;
+        const int s = s0 + g;
+        if (inr && s < s_end) {
+          const int sh[3] = {c_shift[s][0], c_shift[s][1], c_shift[s][2]};
+          double lb = 0.0;
 #pragma unroll
-      for (int t = 0; t < kPer; ++t) {
-        vc[t] = 0;
-        vf[t] = 0;
-        vlb[t] = INFINITY;
-        const int s = s_begin + g + t * kGroup;
-        if (!inr || s >= s_end) continue;
-        const int sx = c_shift[s][0], sy = c_shift[s][1], sz = c_shift[s][2];
-        const double ex = sx < 0 ? lo[0] : (sx > 0 ? hi[0] : 0.0);
-        const double ey = sy < 0 ? lo[1] : (sy > 0 ? hi[1] : 0.0);
-        const double ez = sz < 0 ? lo[2] : (sz > 0 ? hi[2] : 0.0);
-        const double mx = fmax(ex - 1e-9, 0.0), my = fmax(ey - 1e-9, 0.0), mz = fmax(ez - 1e-9, 0.0);
-        const double lb = mx * mx + my * my + mz * mz;
-        if (lb > best) continue;  // conservative: no point inside can win
-        probe(sx, sy, sz, vf[t], vc[t]);
-        vlb[t] = lb;
-      }
-#pragma unroll
-      for (int t = 0; t < kPer; ++t) {
-        for (int l = 0; l < kGroup; ++l) {
-          const uint32_t cnt = __shfl(vc[t], l, kGroup);
-          if (cnt == 0) continue;
-          const double lb = __shfl(vlb[t], l, kGroup);
+          for (int ax = 0; ax < 3; ++ax) {
+            const double e = sh[ax] > 0 ? hi[ax] + (sh[ax] - 1) * a.w : (sh[ax] < 0 ? lo[ax] + (-sh[ax] - 1) * a.w : 0.0);
+            const double m = fmax(e - 1e-9, 0.0);
+            lb += m * m;
+          }
+          if (lb <= best) {  // else conservative: no point inside can win
+            probe(sh[0], sh[1], sh[2], vf, vc);
+            vlb = lb;
+          }
+        }
+        uint64_t live = __ballot(vc != 0);  // wave-wide mask; this group's lanes
+        live = (live >> ((lane_id() / kGroup) * kGroup)) & ((1ull << kGroup) - 1);
+        while (live) {
+          const int l = __ffsll((unsigned long long)live) - 1;
+          live &= live - 1;
+          const double lb = __shfl(vlb, l, kGroup);
           if (lb > best) continue;  // best is group-uniform here
-          const uint32_t first = __shfl(vf[t], l, kGroup);
+          const uint32_t cnt = __shfl(vc, l, kGroup);
+          const uint32_t first = __shfl(vf, l, kGroup);
           n_cand += cnt / kGroup + (g < (int)(cnt % kGroup) ? 1 : 0);
           for (uint32_t i = first + g; i < first + cnt; i += kGroup) test(i);
           group_min();
@@ -270,6 +291,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     };
     pass(1, 7);
     pass(7, 27);
+    if (a.rings >= 2) pass(27, 125);
     if (g == 0) {
       const bool found = best_i != 0xFFFFFFFFu;
       int32_t pair = -1;
@@ -510,6 +532,13 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   c->map_scans = scans;
   c->voxel_w = w;
   c->K = (uint32_t)K;
+  // internal cell = w / subdivision (<= 2).  Searching +-subdivision cells covers the
+  // ball of radius w, so decisions bounded by w are unchanged; when min_dist_map > w the
+  // reference's exact 27 voxels of width w are needed (subdivision 1).
+  int m = c->P.voxel_subdivision == 0 ? 1 : (int)std::min<uint32_t>(c->P.voxel_subdivision, 2u);
+  if (c->P.min_dist_map > w) m = 1;
+  c->cell_m = m;
+  c->cell_w = w / m;
   // one packed upload: poses [K][12], inverses [K][12] (GTSAM Pose3::inverse:
   // (R^T, R^T(-t)), same expression order as the device transforms), segments of
   // both feature types [2][K] (Seg = 16 B = 2 doubles)
@@ -575,7 +604,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
     if (n > 0) {
       hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, pool.pos.p, pool.nrm.p, t == 0 ? 1 : 0,
-                         dseg + t * Kc, K, c->map_poses_p, n, w, reinterpret_cast<Slot*>(M.table.p), use - 1,
+                         dseg + t * Kc, K, c->map_poses_p, n, c->cell_w, reinterpret_cast<Slot*>(M.table.p), use - 1,
                          M.tpos.p, M.tnrm.p, M.rslot.p, M.rseg.p, c->map_err.p);
       FMX_HIP(hipGetLastError());
       c->scan_scratch.ensure(scan_scratch_size(use) + 4);
@@ -598,11 +627,15 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   MatchArgs a;
   if (pose_j34) std::memcpy(a.Tj, pose_j34, sizeof(a.Tj));
   else std::memset(a.Tj, 0, sizeof(a.Tj));
-  a.w = c->voxel_w;
+  a.w = c->cell_w;
+  a.rings = c->cell_m;
   a.max_d2 = max_dist * max_dist;
   a.min_d2 = min_dist_map * min_dist_map;
   const double obs = std::max(a.max_d2, a.min_d2);
-  a.bound = obs <= a.w * a.w ? obs : INFINITY;
+  const double reach = c->cell_m * c->cell_w;  // = the map's voxel width
+  if (obs > reach * reach && c->cell_m > 1)
+    throw StatusError(FMX_E_INVAL, "max_dist / min_dist_map exceed the voxel width of a subdivided map");
+  a.bound = obs <= reach * reach ? obs : INFINITY;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;

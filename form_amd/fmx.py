@@ -52,7 +52,7 @@ class _Params(C.Structure):
         ("max_num_keyscans", C.c_int64), ("max_steps_unused_keyscan", C.c_int64),
         ("max_num_recent_scans", C.c_uint32), ("keyscan_match_ratio", C.c_double),
         ("min_dist_map", C.c_double), ("keypoint_pool_capacity", C.c_uint64),
-        ("max_pairs", C.c_uint32),
+        ("max_pairs", C.c_uint32), ("voxel_subdivision", C.c_uint32),
     ]
 
 
@@ -125,6 +125,7 @@ class EstimatorParams:
     min_dist_map: float = 0.1
     keypoint_pool_capacity: int = 4 << 20
     max_pairs: int = 1024
+    voxel_subdivision: int = 1
 
     def __post_init__(self):
         if self.extraction is None:

@@ -72,6 +72,9 @@ typedef struct fmx_params {
   /* device capacities (not in the reference: it allocates on demand) */
   uint64_t keypoint_pool_capacity; /* records per feature type kept in the window store */
   uint32_t max_pairs;              /* scans per submap (window size bound) */
+  uint32_t voxel_subdivision;      /* device map cells = voxel width / this (1 or 2; 0 = 1):
+                                      same matches; 2 tests fewer candidates per query but
+                                      probes more cells (slower on C4/C5) */
 } fmx_params;
 
 typedef struct fmx_ctx fmx_ctx;

@@ -73,11 +73,12 @@ def test_extract_edge_cases(fmx_mod, oracle):
     assert np.array_equal(got["point_index"], ref["point_idx"])
 
 
-@pytest.mark.parametrize("config", ["tiny", "c2"])
-def test_match_matches_oracle(fmx_mod, oracle, config):
+@pytest.mark.parametrize("config,subdiv", [("tiny", 2), ("c2", 2), ("c2", 1)])
+def test_match_matches_oracle(fmx_mod, oracle, config, subdiv):
     feats = stream_features(oracle, config, 6)
     p = feats[0]["params"]
-    ctx = _ctx(fmx_mod, p)
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p),
+                                                  voxel_subdivision=subdiv))
     w = 0.8
     omaps = [oracle.VoxelMap(w, 0), oracle.VoxelMap(w, 1)]
     scans, poses = [], []
