@@ -14,12 +14,14 @@
 //
 // Greedy planar selection.  The reference sorts each sector by curvature and
 // accepts, in that order, every still-unused point under the threshold, clearing
-// +-(k-1) columns around it, until planar_feats_per_sector+1 are accepted.  With a
-// strict total order on (curvature, column) that greedy result equals the greedy
-// maximal independent set computed in parallel rounds (a candidate that is the
-// minimum of its undecided +-(k-1) neighbourhood is accepted, its neighbours are
-// removed), truncated to the P+1 smallest keys.  Sectors stay sequential: the
-// suppression of sector s spills into sector s+1 (parity hazard 5).
+// +-(k-1) columns around it, until planar_feats_per_sector+1 are accepted.  Here
+// the block ranks the candidates by the strict key (curvature, column), then one
+// wave walks them in key order 64 at a time: conflicts with accepted points of
+// earlier chunks are read from LDS, conflicts inside the chunk are a 64-bit mask
+// per lane resolved by ballot rounds.  (Parallel MIS rounds over the whole sector
+// were exact too, but curvature is monotone along smooth surfaces, so the rounds
+// chained ~pps/k deep.)  Sectors stay sequential: the suppression of sector s
+// spills into sector s+1 (parity hazard 5).
 #include "fmx_device.hpp"
 #include "fmx_internal.hpp"
 
@@ -28,7 +30,7 @@
 namespace fmx {
 namespace {
 
-constexpr int kRowThreads = 256;
+constexpr int kRowThreads = 1024;  // 16 waves: the row phases are LDS-latency bound
 
 struct ExArgs {
   int R, C, k, S, P, Ppt;
@@ -36,12 +38,6 @@ struct ExArgs {
   double thr, min2, max2, radius2;
   int min_points;
 };
-
-// key order for the greedy: (curvature, column)
-__device__ __forceinline__ bool key_less(const float* curv, int a, int b) {
-  const float ca = curv[a], cb = curv[b];
-  return ca < cb || (ca == cb && a < b);
-}
 
 // Ordered (stable) block compaction of flag(c) for c in [b, e) into list[0..n).
 // Returns n (uniform).  Uses ws[kRowThreads/64 + 1].
@@ -66,27 +62,39 @@ __device__ int block_compact(int b, int e, F flag, int* list, int* ws) {
   return base;
 }
 
+// KC > 0: neighbor_points fixed at compile time (the default 5), so every +-k loop
+// unrolls and its LDS reads issue together; KC = 0 reads it from the arguments.
+template <int KC>
 __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __restrict__ scan, ExArgs a,
                                                               uint8_t* __restrict__ planar_mask,
                                                               uint32_t* __restrict__ sel_slots,
                                                               uint32_t* __restrict__ pt_slots,
                                                               uint32_t* __restrict__ row_counts) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int C = a.C, r = blockIdx.x, tid = threadIdx.x, k = a.k;
+  const int C = a.C, r = blockIdx.x, tid = threadIdx.x, k = KC > 0 ? KC : a.k;
   float4* pts = reinterpret_cast<float4*>(smem);
-  float* curv = reinterpret_cast<float*>(pts + C);
-  int* list = reinterpret_cast<int*>(curv + C);
-  int* rk = list + C;                                      // ranks of accepted planar points
-  uint8_t* flg = reinterpret_cast<uint8_t*>(rk + C);  // bit0 point-valid, bit1 out-of-range, bit2 planar-valid
+  uint64_t* keys = reinterpret_cast<uint64_t*>(pts + C);  // accepted planar keys (curv bits, column)
+  int* list = reinterpret_cast<int*>(keys);                // point phase: compacted columns (aliases keys)
+  float* curv = reinterpret_cast<float*>(keys + C);
+  uint8_t* flg = reinterpret_cast<uint8_t*>(curv + C);  // bit0 point-valid, bit1 out-of-range, bit2 planar-valid
   uint8_t* used = flg + C;                               // used_points (planar) then point mask
   uint8_t* state = used + C;
   uint8_t* win = state + C;
   __shared__ int ws[kRowThreads / kWave + 1];
   __shared__ int s_cnt;
 
+#ifdef FMX_EXTRACT_TIMING
+  uint64_t tstamp[40];
+  int nts = 0;
+#define TSTAMP() (tstamp[nts < 40 ? nts++ : 39] = wall_clock64())
+#else
+#define TSTAMP() ((void)0)
+#endif
+  TSTAMP();
   const float4* row = scan + (size_t)r * C;
   for (int c = tid; c < C; c += kRowThreads) pts[c] = row[c];
   __syncthreads();
+  TSTAMP();
 
   // compute_valid_points / compute_point_valid_points (extraction.tpp:136-222)
   for (int c = tid; c < C; c += kRowThreads) {
@@ -100,15 +108,16 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     flg[c] = f;
   }
   __syncthreads();
+  TSTAMP();
   // planar validity: neighbour invalidation of +-k around out-of-range points
   // (scatter at :170-173, evaluated here as a gather), then the curvature (:226-261).
   for (int c = tid; c < C; c += kRowThreads) {
     bool plv = (flg[c] & 1) != 0;
-    if (plv) {
-      for (int d = 1; d <= k; ++d) {
-        if (c - d >= 0 && (flg[c - d] & 2)) plv = false;
-        if (c + d < C && (flg[c + d] & 2)) plv = false;
-      }
+    if (plv) {  // valid => k <= c < C-k: the neighbour reads stay in the row (no branches, loads batch)
+      uint32_t any = 0;
+#pragma unroll
+      for (int d = 1; d <= k; ++d) any |= (uint32_t)(flg[c - d] | flg[c + d]);
+      plv = (any & 2) == 0;
     }
     float cv = FLT_MAX;
     if (plv) {
@@ -116,6 +125,7 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
       double dx = -(2.0 * k) * (double)p.x;
       double dy = -(2.0 * k) * (double)p.y;
       double dz = -(2.0 * k) * (double)p.z;
+#pragma unroll
       for (int n = 1; n <= k; ++n) {
         const float4 qm = pts[c - n], qp = pts[c + n];
         dx = dx + (double)qm.x + (double)qp.x;
@@ -129,78 +139,126 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     planar_mask[(size_t)r * C + c] = plv ? 1 : 0;
   }
   __syncthreads();
+  TSTAMP();
   for (int c = tid; c < C; c += kRowThreads) {
     if (win[c]) flg[c] |= 4;
     used[c] = win[c];
   }
   __syncthreads();
+  TSTAMP();
 
   // ---------------- planar features: sectors in order (extraction.tpp:44-68)
+  // pts[] is dead from here on; its 16C bytes hold the key-sorted candidates srt[C],
+  // the chunk-lane map pos[C] ((stamp << 6) | lane) and the accepted bitmap accb.
+  int* srt = reinterpret_cast<int*>(pts);
+  uint32_t* pos = reinterpret_cast<uint32_t*>(srt + C);
+  uint64_t* accb = reinterpret_cast<uint64_t*>(pts) + C;  // byte offset 8C
+  for (int c = tid; c < C; c += kRowThreads) pos[c] = 0xFFFFFFFFu;
   const int pps = C / a.S;
   int pl_count = 0;  // uniform
+  uint32_t stamp = 0;  // chunk id within the row (uniform)
   for (int s = 0; s < a.S; ++s) {
     const int b = s * pps;
     const int e = (s == a.S - 1) ? C : b + pps;
-    for (int c = b + tid; c < e; c += kRowThreads) {
-      state[c] = (used[c] && (double)curv[c] < a.thr) ? 1 : 0;  // 1 = undecided candidate
-      win[c] = 0;
-    }
-    __syncthreads();
-    // parallel greedy MIS in (curvature, column) order, conflict radius k-1
-    for (;;) {
-      for (int c = b + tid; c < e; c += kRowThreads) {
-        if (state[c] != 1) continue;
-        bool w = true;
-        for (int d = 1; d < k && w; ++d) {
-          const int cl = c - d, cr = c + d;
-          if (cl >= b && state[cl] == 1 && key_less(curv, cl, c)) w = false;
-          if (cr < e && state[cr] == 1 && key_less(curv, cr, c)) w = false;
-        }
-        win[c] = w ? 1 : 0;
-      }
-      __syncthreads();
-      int undecided = 0;
-      for (int c = b + tid; c < e; c += kRowThreads) {
-        if (state[c] != 1) continue;
-        if (win[c]) {
-          state[c] = 2;  // accepted
-        } else {
-          bool rm = false;
-          for (int d = 1; d < k && !rm; ++d) {
-            if (c - d >= b && win[c - d]) rm = true;
-            if (c + d < e && win[c + d]) rm = true;
-          }
-          if (rm) state[c] = 3;
-          else undecided = 1;
-        }
-      }
-      if (!__syncthreads_or(undecided)) break;
-      for (int c = b + tid; c < e; c += kRowThreads) win[c] = 0;
-      __syncthreads();
-    }
-    // accepted set -> ranks in key order; keep the P+1 smallest (break at :354)
+    // candidates (used && curvature < threshold, :340-342) as packed keys
+    // (curvature bits, column): curvature >= 0, so the u64 order is (curv, column).
     if (tid == 0) s_cnt = 0;
+    for (int c = b + tid; c < e; c += kRowThreads) state[c] = 0;
+    for (int w = (b >> 6) + tid; w <= ((e - 1) >> 6); w += kRowThreads) accb[w] = 0;
     __syncthreads();
     for (int c = b + tid; c < e; c += kRowThreads)
-      if (state[c] == 2) list[atomicAdd(&s_cnt, 1)] = c;
+      if (used[c] && (double)curv[c] < a.thr)
+        keys[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(curv[c]) << 32) | (uint32_t)c;
     __syncthreads();
-    const int n_acc = s_cnt;
-    const int keep = n_acc < a.P + 1 ? n_acc : a.P + 1;
-    for (int i = tid; i < n_acc; i += kRowThreads) rk[i] = 0;
+    const int n_c = s_cnt;
+    if (s < 2) TSTAMP();
+    // sort by counting: rank of each key, `sub` adjacent lanes per candidate
+    // (each part scans a contiguous, even-aligned range two keys per 16-B read)
+    int sub = 1;
+    while (sub < 8 && sub * 2 * n_c <= kRowThreads) sub *= 2;
+    if (tid == 0 && (n_c & 1)) keys[n_c] = ~0ull;  // pad: never < a key
     __syncthreads();
-    for (int idx = tid; idx < n_acc * n_acc; idx += kRowThreads) {  // rank by pair counting
-      const int i = idx / n_acc, j = idx - i * n_acc;
-      if (key_less(curv, list[j], list[i])) atomicAdd(&rk[i], 1);
-    }
-    __syncthreads();
-    for (int i = tid; i < n_acc; i += kRowThreads) {
-      const int c = list[i], rank = rk[i];
-      if (rank < keep) {
-        sel_slots[(size_t)r * a.cap_pl + pl_count + rank] = (uint32_t)c;
-        state[c] = 4;
+    for (int t = tid; t < n_c * sub; t += kRowThreads) {
+      const int i = t / sub, part = t % sub;
+      const uint64_t ki = keys[i];
+      const int npair = (n_c + 1) >> 1, per = (npair + sub - 1) / sub;
+      const int p0 = part * per, p1 = min(npair, p0 + per);
+      const ulonglong2* kp = reinterpret_cast<const ulonglong2*>(keys);
+      int rank = 0;
+      int j = p0;
+      for (; j + 3 < p1; j += 4) {
+        const ulonglong2 q0 = kp[j], q1 = kp[j + 1], q2 = kp[j + 2], q3 = kp[j + 3];
+        rank += (q0.x < ki) + (q0.y < ki) + (q1.x < ki) + (q1.y < ki) + (q2.x < ki) + (q2.y < ki) +
+                (q3.x < ki) + (q3.y < ki);
       }
+      for (; j < p1; ++j) {
+        const ulonglong2 q = kp[j];
+        rank += (q.x < ki) + (q.y < ki);
+      }
+      for (int o = 1; o < sub; o <<= 1) rank += __shfl_xor(rank, o, 64);
+      if (part == 0) srt[rank] = (int)(uint32_t)ki;
     }
     __syncthreads();
+    if (s < 2) TSTAMP();
+    // Greedy in key order (:343-355), one wave, 64 candidates per chunk: a candidate
+    // is accepted iff no accepted candidate of lower key lies within k-1 columns.
+    // Earlier chunks: accepted bitmap.  Inside the chunk: each lane maps its column
+    // to (stamp, lane) in pos[], reads its +-(k-1) neighbours' lanes into a conflict
+    // mask of lower-key lanes, and ballot rounds resolve the chunk.
+    if (tid < kWave) {
+      const int lane = tid;
+      int kept = 0;  // wave-uniform
+      for (int base = 0; base < n_c && kept < a.P + 1; base += kWave, ++stamp) {
+        const int idx = base + lane;
+        const bool in = idx < n_c;
+        const int c = in ? srt[idx] : b;
+        const int lo = c - (k - 1) < b ? b : c - (k - 1), hi = c + (k - 1) >= e ? e - 1 : c + (k - 1);
+        bool und = in;
+        if (in) {
+          pos[c] = (stamp << 6) | (uint32_t)lane;
+          const int w0 = lo >> 6, w1 = hi >> 6;
+          for (int w = w0; w <= w1; ++w) {
+            uint64_t m = accb[w];
+            if (w == w0) m &= ~0ull << (lo & 63);
+            if (w == w1) m &= ~0ull >> (63 - (hi & 63));
+            if (m) und = false;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint64_t conf = 0;
+        if (und) {
+#pragma unroll
+          for (int j = lo; j <= hi; ++j) {
+            const uint32_t q = pos[j];
+            if ((q >> 6) == stamp && (int)(q & 63) < lane) conf |= 1ull << (q & 63);
+          }
+        }
+        uint64_t A = 0;
+        for (;;) {
+          const uint64_t U = __ballot(und);
+          if (U == 0) break;
+          const bool acc = und && (conf & U) == 0;
+          A |= __ballot(acc);
+          if (acc || (conf & A) != 0) und = false;
+        }
+        if ((A >> lane) & 1) {
+          const int rank = kept + __popcll(A & lanemask_lt());
+          if (rank < a.P + 1) {
+            sel_slots[(size_t)r * a.cap_pl + pl_count + rank] = (uint32_t)c;
+            state[c] = 4;
+          }
+          atomicOr(reinterpret_cast<unsigned long long*>(&accb[c >> 6]), 1ull << (c & 63));
+        }
+        kept += __popcll(A);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (tid == 0) s_cnt = kept < a.P + 1 ? kept : a.P + 1;
+    }
+    __syncthreads();
+    if (s < 2) TSTAMP();
+    const int keep = s_cnt;
     // suppression used[c +- n], n in [0, k) (:347-350)
     for (int c = b + tid; c < e; c += kRowThreads) {
       if (state[c] != 4) continue;
@@ -211,6 +269,7 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     }
     pl_count += keep;
     __syncthreads();
+    TSTAMP();
   }
 
   // ---------------- point features (extraction.tpp:70-96)
@@ -225,6 +284,7 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     const int b = s * pps;
     const int e = (s == a.S - 1) ? C : b + pps;
     const int nu = block_compact(b, e, [&](int c) { return win[c] != 0; }, list, ws);
+    if (s < 1) TSTAMP();
     if (tid < kWave) {
       // extract_point (:360-399).  Phase A, literal, lane 0: passes off = 0, 1, ...
       // over U[off], U[off+factor], ... until the (Ppt+1)-th accept; the break at
@@ -285,6 +345,7 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
       if (tid == 0) s_cnt = pt_count + nf;
     }
     __syncthreads();
+    if (s < 1) TSTAMP();
     // apply phase-B suppression from the written slots (phase A already applied)
     {
       const int n0 = pt_count, n1 = s_cnt;
@@ -299,11 +360,21 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     __syncthreads();
     pt_count = s_cnt;
     __syncthreads();
+    TSTAMP();
   }
   if (tid == 0) {
     row_counts[2 * r] = (uint32_t)pl_count;
     row_counts[2 * r + 1] = (uint32_t)pt_count;
   }
+#ifdef FMX_EXTRACT_TIMING
+  if (tid == 0 && (r == 5 || r == 64 || r == 120)) {
+    int d[24] = {0};
+    for (int i = 1; i < nts && i < 24; ++i) d[i - 1] = (int)(tstamp[i] - tstamp[i - 1]);
+    printf("row %d ticks: %d %d %d %d | %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d\n", r, d[0], d[1],
+           d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], d[16], d[17],
+           d[18], d[19], d[20], d[21], d[22], d[23]);
+  }
+#endif
 }
 
 // Per-row 64-column block AABBs of the planar-valid points (one wave per block),
@@ -666,14 +737,20 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   c->cols = C;
   const size_t lds = (size_t)C * (16 + 4 + 4 + 4 + 4);
   if (!c->lds_attr_set) {
-    FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extract_rows),
+    FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extract_rows<5>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * (16 + 4 + 4 + 4 + 4)));
+    FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extract_rows<0>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * (16 + 4 + 4 + 4 + 4)));
     c->lds_attr_set = true;
   }
   {
     ProfScope ps(c->prof, PROF_EXTRACT_ROWS, 16.0 * N + N, st);
-    hipLaunchKernelGGL(k_extract_rows, dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
-                       c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+    if (a.k == 5)
+      hipLaunchKernelGGL(k_extract_rows<5>, dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+    else
+      hipLaunchKernelGGL(k_extract_rows<0>, dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
   }
   FMX_HIP(hipGetLastError());
   FMX_HIP(hipMemsetAsync(c->row_ok.p, 0, R * sizeof(uint32_t), st));

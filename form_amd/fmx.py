@@ -20,7 +20,7 @@ from dataclasses import dataclass, fields
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfmx.so")
+LIB_PATH = os.environ.get("FMX_LIB", os.path.join(_HERE, "libfmx.so"))  # FMX_LIB: A/B of two builds
 _LIB = None
 
 FMX_OK = 0
