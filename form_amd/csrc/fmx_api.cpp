@@ -486,25 +486,21 @@ struct DeviceLM {
     }
     c2 = 0;
     if (K == 0) return 0.0;
-    e.G.resize(28 * (size_t)K);
-    e.err.resize(K);
-    // window poses = the built map's poses (unchanged during the scan); Tj by value
-    run_linearize_mapj(c, Tj.m, sigma, 1, e.G.data(), e.err.data());
+    // window poses = the built map's poses (unchanged during the scan); Tj by value;
+    // one fused launch sums the system over all pairs
+    double S[29];
+    run_linearize_total(c, Tj.m, sigma, S);
     ++linearizations;
-    double er = 0;
-    for (uint32_t k = 0; k < K; ++k) {
-      const double* Gk = &e.G[28 * (size_t)k];
-      double full[7][7];
-      int o = 0;
-      for (int i = 0; i < 7; ++i)
-        for (int j = i; j < 7; ++j) full[i][j] = full[j][i] = Gk[o++];
-      for (int i = 0; i < 6; ++i) {
-        for (int j = 0; j < 6; ++j) H[i][j] += full[i][j];
-        gg[i] += full[i][6];
-      }
-      c2 += full[6][6];
-      er += e.err[k];
+    double full[7][7];
+    int o = 0;
+    for (int i = 0; i < 7; ++i)
+      for (int j = i; j < 7; ++j) full[i][j] = full[j][i] = S[o++];
+    for (int i = 0; i < 6; ++i) {
+      for (int j = 0; j < 6; ++j) H[i][j] = full[i][j];
+      gg[i] = full[i][6];
     }
+    c2 = full[6][6];
+    const double er = S[28];
     return er;
   }
   // one LevenbergMarquardtOptimizer::iterate() from the cached system at T
@@ -596,6 +592,7 @@ void remove_scan(fmx_ctx* c, uint64_t s) {  // KeypointMap::remove (map.tpp:112-
 }
 
 void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
+  HostScope hs_all(0);
   if (!c->est) {
     c->est = new fmx_ctx::Est();
     c->est->ks.P = &c->P;
@@ -615,17 +612,34 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   auto& cj = e.cons[j];
   for (auto& [i, T] : e.values)
     if (i != j) cj[i] = {0, 0};
-  // extract (form.cpp:51)
-  fmx_feature_counts fc{};
-  do_extract(c, xyzw, n, j, on_dev, &fc);
-  // to_voxel_map x2, voxel width = max_dist_matching (form.cpp:61-65)
+  // to_voxel_map x2, voxel width = max_dist_matching (form.cpp:61-65).  The map holds
+  // only earlier scans at their current estimates, so it does not depend on this
+  // scan's features: FMX_MAP_SIDE builds it on the side stream next to extraction
+  // (measured neutral: host launch cost already serializes the two).
   std::set<uint64_t> sset;
   for (int t = 0; t < 2; ++t)
     for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
   std::vector<uint64_t> scans(sset.begin(), sset.end());
   std::vector<double> poses(12 * scans.size());
   for (size_t k = 0; k < scans.size(); ++k) std::memcpy(&poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double));
-  run_map_build(c, scans, poses.data(), P.max_dist_matching);
+  static const bool side = std::getenv("FMX_MAP_SIDE") != nullptr;  // A/B switch, default off
+  if (side) {
+    FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
+    FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
+    FMX_HIP(hipEventRecord(c->ev_join, c->side));
+  } else {
+    HostScope hs_map(3);
+    run_map_build(c, scans, poses.data(), P.max_dist_matching);
+  }
+  // extract (form.cpp:51)
+  fmx_feature_counts fc{};
+  {
+    HostScope hs_ex(2);
+    do_extract(c, xyzw, n, j, on_dev, &fc);
+  }
+  HostScope* hs_icp = new HostScope(4);
+  if (side) FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   uint64_t icp = 0, lm_it = 0, lins = 0;
   static const bool host_lm = std::getenv("FMX_DEVICE_LM") == nullptr;  // default: host LM
   if (host_lm) {
@@ -686,7 +700,11 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       lm_rounds(c, kRounds);
       icp_launch(c, 1);
       readback();
-      while (!hs.icp_done && hs.phase != 2) {  // LM needs more rounds
+      for (int more = 0; !hs.icp_done && hs.phase != 2; ++more) {  // LM needs more rounds
+        if (more > 40)  // 160 rounds > GTSAM's 100 LM iterations: the state machine is stuck
+          throw StatusError(FMX_E_STATE, "device LM made no progress (phase " + std::to_string(hs.phase) +
+                                             ", lins " + std::to_string(hs.lins) + ", lm_iters " +
+                                             std::to_string(hs.lm_iters) + ")");
         lm_rounds(c, kRounds);
         icp_launch(c, 1);
         readback();
@@ -695,10 +713,11 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     }
     if (!hs.icp_done) {  // optimize(false) from the last updated pose
       icp_launch(c, 2);
-      do {
+      for (int more = 0; hs.phase != 2; ++more) {
+        if (more > 40) throw StatusError(FMX_E_STATE, "device LM made no progress (final optimize)");
         lm_rounds(c, kRounds);
         readback();
-      } while (hs.phase != 2);
+      }
       hs.lm_total += hs.lm_iters;
     }
     Pose Tf;
@@ -708,6 +727,8 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     lm_it = (uint64_t)hs.lm_total;
     lins = (uint64_t)hs.lins;
   }
+  delete hs_icp;
+  HostScope hs_tail(5);
   match_counts_fetch(c);
   uint64_t mpl = 0, mpt = 0;
   for (uint32_t k = 0; k < c->K; ++k) {
@@ -790,6 +811,9 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
   c->device = device;
   fmx_status st = guard(c, [&] {
     FMX_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    FMX_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    FMX_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    FMX_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     const uint64_t cap = p->keypoint_pool_capacity ? p->keypoint_pool_capacity : (4u << 20);
     c->pool[0].planar = true;
     c->pool[1].planar = false;
@@ -809,6 +833,7 @@ void fmx_destroy(fmx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->side) (void)hipStreamSynchronize(c->side);
   for (auto& e : c->prof.free_events) (void)hipEventDestroy(e);
   for (auto& pe : c->prof.pending) {
     (void)hipEventDestroy(pe.second.first);
@@ -833,9 +858,12 @@ void fmx_destroy(fmx_ctx* c) {
   c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();
   c->hist.release(); c->hist_off.release(); c->c_pl.release(); c->c_pt.release(); c->pair_counts.release();
   c->chunk_range.release(); c->chunks.release(); c->n_chunks.release(); c->poses_ij.release();
-  c->partials.release(); c->G.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
+  c->partials.release(); c->G.release(); c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   delete c;
 }
 

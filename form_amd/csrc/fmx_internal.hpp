@@ -5,6 +5,9 @@
 
 #include <map>
 #include <stdexcept>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -162,6 +165,8 @@ struct fmx_ctx {
   fmx_params P{};
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;                    // map build, overlapped with extraction
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // stream -> side -> stream ordering
   std::string err;
   fmx::Prof prof;
 
@@ -230,7 +235,8 @@ struct fmx_ctx {
   bool lds_attr_set = false;
 
   // ---- linearize
-  fmx::DBuf<double> poses_ij, partials, G;
+  fmx::DBuf<double> poses_ij, partials, G, bpart;  // bpart: k_linearize_total block partials
+  fmx::DBuf<uint32_t> ticket;                     // its last-block ticket
   fmx::HBuf<double> h_poses, h_G;
   fmx::HBuf<int32_t> h_i32;
 
@@ -247,7 +253,55 @@ struct fmx_ctx {
 namespace fmx {
 // Wait for the context stream by polling (hipStreamSynchronize's blocking wake-up
 // costs tens of microseconds; the ICP loop waits ~5-15 times per scan).
+// Host-side timing (env FMX_HOST_TIMING): accumulated seconds / counts per site,
+// printed to stderr at exit.  Diagnostic only.
+struct HostTiming {
+  bool on = std::getenv("FMX_HOST_TIMING") != nullptr;
+  double t[8] = {0};
+  uint64_t n[8] = {0};
+  ~HostTiming() {
+    if (!on) return;
+    static const char* names[8] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop", "insert+tail",
+                                   "lm_host_math", "launch"};
+    for (int i = 0; i < 8; ++i)
+      if (n[i]) fprintf(stderr, "host %-14s %10.1f us total %8llu calls %8.2f us/call\n", names[i], t[i] * 1e6,
+                        (unsigned long long)n[i], t[i] * 1e6 / n[i]);
+  }
+};
+inline HostTiming& host_timing() {
+  static HostTiming h;
+  return h;
+}
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+struct HostScope {
+  int id;
+  double t0;
+  explicit HostScope(int i) : id(i), t0(host_timing().on ? now_s() : 0.0) {}
+  ~HostScope() {
+    if (host_timing().on) {
+      host_timing().t[id] += now_s() - t0;
+      host_timing().n[id]++;
+    }
+  }
+};
+
+// Wait for the context stream: hipStreamQuery spin (default) or, FMX_SYNC=sync,
+// hipStreamSynchronize.  An isolated empty-kernel round trip favours the latter
+// (11.5 vs 52 us, tools/apibench), but register_scan measures 4-5 % faster with the
+// spin (best of 3, C4), so the spin stays the default.
 inline void stream_wait(fmx_ctx* c) {
+  HostScope hs(1);
+  static const bool query = [] {
+    const char* s = std::getenv("FMX_SYNC");
+    return !(s && std::string(s) == "sync");
+  }();
+  if (!query) {
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) throw HipError(std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+    return;
+  }
   for (;;) {
     const hipError_t e = hipStreamQuery(c->stream);
     if (e == hipSuccess) return;
@@ -256,7 +310,10 @@ inline void stream_wait(fmx_ctx* c) {
 }
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out);
-void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w);
+// st: stream to build on (default the context stream; register_scan uses the side
+// stream so the build overlaps extraction)
+void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w,
+                   hipStream_t st = nullptr);
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,
                const IcpDev* icp = nullptr);  // icp != null: pose from the device ICP state
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
@@ -267,6 +324,8 @@ void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34,
                    double* G_out, double* err_out);
 // single-pose fast path: Ti = the built map's poses (device), Tj by value (no upload)
 void run_linearize_mapj(fmx_ctx* c, const double* pose_j34, double sigma, int mode, double* G_out, double* err_out);
+// out[0..27]: summed single-pose system over all pairs at pose_j; out[28]: error
+void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, double* out);
 void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
                  const double* ppj, const uint32_t* nt, const double* tpi, const double* tpj);
 constexpr int kPlaneChunk = 64;  // plane rows per linearize chunk (one wave, one row per lane)

@@ -42,9 +42,9 @@ struct LinShape<2> {  // error only
   static constexpr int M = 0, NG = 1;
 };
 
-template <int MODE>
-__device__ __forceinline__ void accum_row(const double (&H)[12], double r, double inv,
-                                          double (&acc)[LinShape<MODE>::NG]) {
+template <int MODE, int N>
+__device__ __forceinline__ void accum_row(const double (&H)[12], double r, double inv, double (&acc)[N]) {
+  static_assert(N >= LinShape<MODE>::NG, "accumulator too small");
   if constexpr (MODE == 2) {
     const double w = r * inv;
     acc[0] += w * w;
@@ -398,31 +398,9 @@ __device__ __forceinline__ void lm_advance(LmReg& s, bool end_first) {
   s.phase = 2;
 }
 
-constexpr int kStepThreads = 256;  // 256: leaves the deciding lane enough VGPRs (no scratch)
-
-// Reduce the chunk partials of every pair (fixed order: 8 interleaved accumulators
-// per item, combined in order) and take one LM decision on a register copy.
-__global__ __launch_bounds__(kStepThreads) void k_lm_step(const uint32_t* __restrict__ chunk_range,
-                                                          const double* __restrict__ partials, size_t ldp, int K,
-                                                          double* __restrict__ Gs, IcpDev* __restrict__ s) {
-  extern __shared__ double sG[];  // [K * 28]
-  if (s->icp_done || s->phase == 2) return;
-  constexpr int NG = 28;
-  for (int it = threadIdx.x; it < K * NG; it += kStepThreads) {
-    const int k = it / NG, e = it % NG;
-    const uint32_t b = chunk_range[k], en = chunk_range[k + 1];
-    const double* p = partials + (size_t)e * ldp;
-    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t ch = b;
-    for (; ch + 8 <= en; ch += 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] += p[ch + u];
-    }
-    for (int u = 0; ch < en; ++ch, ++u) a[u] += p[ch];
-    sG[it] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
+// One LM decision (GTSAM LevenbergMarquardtOptimizer, see lm_advance) on a register
+// copy of the state, from the summed 7 x 7 system S (packed upper) and error e.
+__device__ __forceinline__ void lm_decide(IcpDev* __restrict__ s, const double* S /* LDS */, double e) {
   LmReg r;
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
@@ -440,29 +418,23 @@ __global__ __launch_bounds__(kStepThreads) void k_lm_step(const uint32_t* __rest
   r.linchg = s->linchg;
   r.phase = s->phase;
   r.lm_iters = s->lm_iters;
-  double H[36], g[6], c = 0, e = 0;
-#pragma unroll
-  for (int i = 0; i < 36; ++i) H[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) g[i] = 0;
-  for (int k = 0; k < K; ++k) {
-    const double* G = sG + NG * k;
+  double H[36], g[6], c = 0;
+  {
     int o = 0;
 #pragma unroll
     for (int i = 0; i < 7; ++i)
 #pragma unroll
       for (int j = i; j < 7; ++j) {
-        const double v = G[o++];
+        const double v = S[o++];
         if (i < 6 && j < 6) {
-          H[6 * i + j] += v;
-          if (i != j) H[6 * j + i] += v;
+          H[6 * i + j] = v;
+          H[6 * j + i] = v;
         } else if (i < 6) {
-          g[i] += v;
+          g[i] = v;
         } else {
-          c += v;
+          c = v;
         }
       }
-    e += 0.5 * G[NG - 1];
   }
   if (r.phase == 0) {  // initial linearization at T
 #pragma unroll
@@ -518,6 +490,140 @@ __global__ __launch_bounds__(kStepThreads) void k_lm_step(const uint32_t* __rest
   s->phase = r.phase;
   s->lm_iters = r.lm_iters;
   s->lins++;
+}
+
+// ---------------------------------------------------------------- fused total
+// register_scan's linearization (single pose): the sum over ALL pairs of
+// [H_j b]^T [H_j b] (28 doubles) and the error, in one launch.  16 waves per block,
+// one 64-row chunk each.  Each wave reduce-scatters its 28 (+4 pad) sums across the
+// lanes (5 halving steps + 1: 32 shuffles instead of 28 butterflies), the block adds
+// its waves in order, the block partial goes out with sc1 (write-through) stores,
+// each block takes an agent-scope ticket, and the last block sums the block partials
+// with sc1 loads in a fixed order (MI355X_MICROARCH.md, inter-workgroup hand-off,
+// row 1: no fences needed).  Host mode writes G and err to mapped memory; device mode
+// (DEVLM) takes the LM decision in the same block.
+// Host mode: 16 waves per block.  Device-LM mode: 4 waves, so the inlined LM
+// decision gets 256 VGPRs without spilling (the grid is < 1 block per CU anyway).
+constexpr int kTotWavesHost = 16, kTotWavesDev = 4;
+constexpr int kTotLd = 32;  // doubles per block partial (28 used)
+template <bool DEVLM>
+constexpr int tot_waves() { return DEVLM ? kTotWavesDev : kTotWavesHost; }
+
+// v[0..31] summed over the wave; afterwards lanes 2i and 2i+1 hold entry i in v[0].
+__device__ __forceinline__ double wave_reduce_scatter32(double (&v)[32]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int half = 16 >> k;
+    const bool hi = (lane >> (5 - k)) & 1;
+#pragma unroll
+    for (int j = 0; j < half; ++j) {
+      const double a = v[j], b = v[j + half];
+      const double send = hi ? a : b;
+      const double keep = hi ? b : a;
+      v[j] = keep + __shfl_xor(send, 32 >> k, 64);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
+template <bool DEVLM>
+__global__ __launch_bounds__(tot_waves<DEVLM>() * kWave) void k_linearize_total(
+    const Chunk* __restrict__ chunks, const uint32_t* __restrict__ n_chunks, const double* __restrict__ c_pl,
+    size_t ld_pl, const double* __restrict__ c_pt, size_t ld_pt, const double* __restrict__ poses, double inv,
+    double* __restrict__ bpart, uint32_t* __restrict__ ticket, double* __restrict__ out, IcpDev* __restrict__ icp,
+    Pose34 tjv) {
+  constexpr int NG = 28;
+  constexpr int kTotWaves = tot_waves<DEVLM>();
+  constexpr int kTotGroups = kTotWaves * kWave / NG;  // final reduction: lane groups x 28 entries
+  if (icp && (icp->icp_done || icp->phase == 2)) return;  // uniform: device LM finished
+  const int w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t ch = blockIdx.x * kTotWaves + w;
+  double acc[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) acc[i] = 0.0;
+  if (n_chunks && ch < *n_chunks) {  // n_chunks null: no correspondences (K = 0)
+    const Chunk d = chunks[ch];
+    const double* Ti = poses + 12 * d.pair;
+    const double* Tj = icp ? (icp->phase == 0 ? icp->T : icp->Tn) : tjv.m;
+    double H[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) H[i] = 0.0;
+    const uint32_t row = d.begin + lane;
+    if (row < d.end) {
+      if (d.type == 0) {
+        const double pi[3] = {c_pl[row], c_pl[ld_pl + row], c_pl[2 * ld_pl + row]};
+        const double ni[3] = {c_pl[3 * ld_pl + row], c_pl[4 * ld_pl + row], c_pl[5 * ld_pl + row]};
+        const double pj[3] = {c_pl[6 * ld_pl + row], c_pl[7 * ld_pl + row], c_pl[8 * ld_pl + row]};
+        double r;
+        plane_row<1>(Ti, Tj, pi, ni, pj, r, H);
+        accum_row<1>(H, r, inv, acc);
+      } else {
+        const double pi[3] = {c_pt[row], c_pt[ld_pt + row], c_pt[2 * ld_pt + row]};
+        const double pj[3] = {c_pt[3 * ld_pt + row], c_pt[4 * ld_pt + row], c_pt[5 * ld_pt + row]};
+        double wpi[3], wpj[3];
+        d_xform(Ti, pi[0], pi[1], pi[2], wpi);
+        d_xform(Tj, pj[0], pj[1], pj[2], wpj);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          double r;
+          point_row<1>(Ti, Tj, pi, pj, wpi, wpj, a, r, H);
+          accum_row<1>(H, r, inv, acc);
+        }
+      }
+    }
+  }
+  __shared__ double sw[kTotWaves][NG];
+  __shared__ double sq[kTotGroups][NG];
+  __shared__ double sS[NG + 1];
+  __shared__ int s_last;
+  const double mine = wave_reduce_scatter32(acc);  // entry lane / 2
+  if ((lane & 1) == 0 && (lane >> 1) < NG) sw[w][lane >> 1] = mine;
+  __syncthreads();
+  if (threadIdx.x < NG) {
+    const int t = threadIdx.x;
+    double bp = sw[0][t];
+#pragma unroll
+    for (int i = 1; i < kTotWaves; ++i) bp += sw[i][t];
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(bpart + (size_t)blockIdx.x * kTotLd + t),
+                       (unsigned long long)__double_as_longlong(bp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  // last block: lane group j (36 of them) sums entry e of blocks j, j + 36, ...;
+  // then the 36 group sums in order
+  const int nblk = gridDim.x;
+  if (threadIdx.x < kTotGroups * NG) {
+    const int e = threadIdx.x % NG, j = threadIdx.x / NG;
+    double s = 0.0;
+    for (int b = j; b < nblk; b += kTotGroups)
+      s += __longlong_as_double((long long)__hip_atomic_load(
+          reinterpret_cast<const unsigned long long*>(bpart + (size_t)b * kTotLd + e), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT));
+    sq[j][e] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NG) {
+    const int e = threadIdx.x;
+    double s = sq[0][e];
+#pragma unroll
+    for (int j = 1; j < kTotGroups; ++j) s += sq[j][e];
+    sS[e] = s;
+    if (!icp) out[e] = s;
+    if (e == NG - 1) {
+      sS[NG] = 0.5 * s;
+      if (!icp) out[NG] = 0.5 * s;
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if constexpr (DEVLM) {
+    if (threadIdx.x == 0) lm_decide(icp, sS, sS[NG]);
+  }
 }
 
 // form.cpp:71-72: before = current pose; LM restarts (lambda0) from it.
@@ -702,6 +808,18 @@ void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, 
 
 namespace fmx {
 
+// blocks of k_linearize_total for the current chunk table (+ the partial / ticket
+// buffers it needs; the ticket starts at 0 and the last block resets it)
+static uint32_t tot_blocks(fmx_ctx* c, int waves) {
+  const uint32_t nblk = std::max<uint32_t>((c->max_chunks + waves - 1) / waves, 1);
+  c->bpart.ensure((size_t)nblk * kTotLd);
+  if (!c->ticket.p) {
+    c->ticket.ensure(1);
+    FMX_HIP(hipMemsetAsync(c->ticket.p, 0, sizeof(uint32_t), c->stream));
+  }
+  return nblk;
+}
+
 void icp_launch(fmx_ctx* c, int what) {
   hipStream_t st = c->stream;
   if (what == 0) hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, st, c->icp.p);
@@ -710,30 +828,45 @@ void icp_launch(fmx_ctx* c, int what) {
   FMX_HIP(hipGetLastError());
 }
 
-// `rounds` x (linearize at the state's pose, reduce + LM decision); no host sync.
+// `rounds` x (fused linearize + reduce + LM decision); no host sync.
 void lm_rounds(fmx_ctx* c, int rounds) {
   hipStream_t st = c->stream;
   const int K = (int)c->K;
-  const uint32_t nb = std::max<uint32_t>(c->max_chunks, 1);
-  const size_t ldp = nb;
-  c->partials.ensure((size_t)nb * 91 + 1);
-  c->G.ensure((size_t)std::max(K, 1) * 92 + 1);
+  const uint32_t nblk = tot_blocks(c, kTotWavesDev);
   const double inv = 1.0 / c->P.planar_constraint_sigma;
   for (int r = 0; r < rounds; ++r) {
-    {
-      ProfScope ps(c->prof, PROF_LINEARIZE, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * 28 * K, st);
-      if (K > 0)
-        hipLaunchKernelGGL(k_linearize<1>, dim3(nb), dim3(kLinThreads), 0, st, c->chunks.p, c->n_chunks.p, c->c_pl.p,
-                           c->ld_pl, c->c_pt.p, c->ld_pt, c->map_poses_p, inv, c->partials.p, ldp, c->icp.p,
-                           Pose34{}, 0);
-    }
-    {
-      ProfScope ps(c->prof, PROF_LIN_FINAL, 8.0 * 28 * (double)nb, st);
-      hipLaunchKernelGGL(k_lm_step, dim3(1), dim3(kStepThreads), (size_t)std::max(K, 1) * 28 * sizeof(double), st,
-                         c->chunk_range.p, c->partials.p, ldp, K, c->G.p, c->icp.p);
-    }
+    ProfScope ps(c->prof, PROF_LINEARIZE, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kTotLd * nblk, st);
+    // K = 0 still launches: the LM decides on the empty system (error 0 -> done)
+    hipLaunchKernelGGL(k_linearize_total<true>, dim3(K > 0 ? nblk : 1), dim3(kTotWavesDev * kWave), 0, st, c->chunks.p,
+                       K > 0 ? c->n_chunks.p : nullptr, c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt, c->map_poses_p,
+                       inv, c->bpart.p, c->ticket.p, (double*)nullptr, c->icp.p, Pose34{});
     FMX_HIP(hipGetLastError());
   }
+}
+
+// register_scan's host-LM linearization: out[0..27] = sum over pairs of the packed
+// 7 x 7 [H_j b]^T [H_j b] at pose_j, out[28] = error.  One launch, one wait.
+void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, double* out) {
+  if (!c->have_map) throw StatusError(FMX_E_STATE, "no map");
+  if (!c->have_corr) throw StatusError(FMX_E_STATE, "no correspondences");
+  hipStream_t st = c->stream;
+  for (int i = 0; i < 29; ++i) out[i] = 0.0;
+  if (c->K == 0) return;
+  const uint32_t nblk = tot_blocks(c, kTotWavesHost);
+  Pose34 tjv;
+  std::memcpy(tjv.m, pose_j34, sizeof(tjv.m));
+  c->h_G.ensure(32);
+  if (c->counts_pending && c->prof.on) match_counts_fetch(c);  // exact byte model for the profile
+  {
+    ProfScope ps(c->prof, PROF_LINEARIZE, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kTotLd * nblk, st);
+    hipLaunchKernelGGL(k_linearize_total<false>, dim3(nblk), dim3(kTotWavesHost * kWave), 0, st, c->chunks.p, c->n_chunks.p,
+                       c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt, c->map_poses_p, 1.0 / sigma, c->bpart.p,
+                       c->ticket.p, c->h_G.d, (IcpDev*)nullptr, tjv);
+    FMX_HIP(hipGetLastError());
+  }
+  stream_wait(c);
+  match_counts_fetch(c);  // already copied; no extra wait
+  std::memcpy(out, c->h_G.p, 29 * sizeof(double));
 }
 
 }  // namespace fmx

@@ -525,8 +525,9 @@ uint64_t next_pow2(uint64_t v) {
 }  // namespace
 
 // ---------------------------------------------------------------------------- host
-void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w) {
-  hipStream_t st = c->stream;
+void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w,
+                   hipStream_t stream) {
+  hipStream_t st = stream ? stream : c->stream;
   const int K = (int)scans.size();
   const int Kc = std::max(K, 1);
   c->map_scans = scans;

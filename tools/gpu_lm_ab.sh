@@ -1,0 +1,13 @@
+#!/bin/bash
+# Host LM vs device LM (FMX_DEVICE_LM=1) on one box: register parity test under the
+# device path, then interleaved C4 bench lines.
+mkdir -p gpurun_out
+FMX_DEVICE_LM=1 timeout -k 10 300 python -m pytest tests -m gpu -q -p no:cacheprovider -k register > gpurun_out/pytest_devlm.log 2>&1 || { tail -30 gpurun_out/pytest_devlm.log; exit 1; }
+tail -1 gpurun_out/pytest_devlm.log
+for rep in $(seq 1 ${REPS:-2}); do
+  for tag in host dev; do
+    if [ $tag = dev ]; then export FMX_DEVICE_LM=1; else unset FMX_DEVICE_LM; fi
+    timeout -k 10 400 python bench.py --steps ${STEPS:-30} --warmup 10 --no-cpu-baseline > gpurun_out/lm_$tag$rep.json 2> gpurun_out/lm_$tag$rep.err || { tail -20 gpurun_out/lm_$tag$rep.err; exit 1; }
+    python -c "import json; d=json.load(open('gpurun_out/lm_$tag$rep.json')); print('$tag', d['value'], d['ms_per_step'], {k: v for k, v in d['kernels_ms_per_step'].items() if v}, d['counters']['linearizations'])"
+  done
+done

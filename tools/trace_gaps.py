@@ -1,0 +1,35 @@
+"""Summarise a rocprofv3 kernel_trace.csv: busy vs idle time over the last steps and
+the per-kernel launch sequence of one register_scan (bench.py C4 run)."""
+import csv
+import sys
+from collections import defaultdict
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+print("kernels:", len(ev))
+# steps start at the extraction kernel
+starts = [i for i, e in enumerate(ev) if "k_extract_rows" in e[2]]
+print("steps seen:", len(starts))
+if len(starts) >= 3:
+    a, b = starts[-3], starts[-2]
+    seg = ev[a:b]
+    t0 = seg[0][0]
+    span = ev[b][0] - t0
+    busy = 0
+    last_end = t0
+    for s, e, n in seg:
+        busy += e - max(s, last_end) if e > last_end else 0
+        last_end = max(last_end, e)
+    print(f"one step: span {span/1e3:.1f} us, kernel-busy {busy/1e3:.1f} us, launches {len(seg)}")
+    prev_end = t0
+    for s, e, n in seg:
+        short = n.split("(")[0].replace("void ", "")[:60]
+        print(f"  +{(s - t0)/1e3:8.1f}  gap {(s - prev_end)/1e3:7.1f}  dur {(e - s)/1e3:7.1f}  {short}")
+        prev_end = max(prev_end, e)
+    tot = defaultdict(float)
+    for s, e, n in ev[starts[1]:starts[-1]]:
+        tot[n.split("(")[0][:60]] += (e - s) / 1e3
+    nsteps = len(starts) - 2
+    print("per-step kernel time (us):")
+    for k, v in sorted(tot.items(), key=lambda x: -x[1]):
+        print(f"  {v / nsteps:8.1f}  {k}")
