@@ -28,7 +28,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from form_amd import fmx, synth  # noqa: E402
+from form_amd import fmx, metrics, synth  # noqa: E402
 
 METRIC = "scans/sec + Mpts/sec scan-to-submap ICP (128-beam); ATE delta vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
@@ -96,10 +96,12 @@ def cpu_baseline(scans_host, params, budget_s):
     est = O.Estimator(O.default_params(params), threads)
     times = []
     t_all = time.perf_counter()
+    poses = []
     for s in scans_host:
         t0 = time.perf_counter()
-        est.register_scan(s)
+        T, _, _ = est.register_scan(s)
         times.append(time.perf_counter() - t0)
+        poses.append(T)
         if time.perf_counter() - t_all > budget_s:
             break
     # steady state: skip the first (empty-map) scan when there is more than one
@@ -109,7 +111,25 @@ def cpu_baseline(scans_host, params, budget_s):
                 sample=f"oracle register_scan (C++ restatement, std::thread at the reference's two TBB sites) "
                        f"over the first {len(times)} scans of the same synthetic stream; median of "
                        f"{len(steady)} steady-state scans = {per * 1e3:.1f} ms/scan",
-                ms_per_scan=per * 1e3)
+                ms_per_scan=per * 1e3), poses
+
+
+def ate_block(scans_host, oracle_poses, params, k0, device):
+    """ATE of the GPU path and of the CPU oracle path over the same scans against the
+    synthetic ground truth (the newer_college ATE is unavailable
+    offline).  Untimed; a fresh context replays the sample."""
+    n = len(oracle_poses)
+    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params)), device=device)
+    gpu = []
+    for s in scans_host[:n]:
+        ctx.register_scan(s)
+        gpu.append(ctx.current_pose())
+    gt = [synth.trajectory_pose(k0 + k) for k in range(n)]
+    a_gpu, a_cpu = metrics.ate_rmse(gpu, gt), metrics.ate_rmse(oracle_poses, gt)
+    return {"gpu_m": round(a_gpu, 6), "cpu_port_m": round(a_cpu, 6), "delta_m": round(a_gpu - a_cpu, 9),
+            "max_pose_diff_m": round(float(max(np.abs(np.asarray(g)[:, 3] - np.asarray(o)[:, 3]).max()
+                                               for g, o in zip(gpu, oracle_poses))), 9),
+            "scans": n, "truth": "synthetic trajectory (synth.trajectory_pose)"}
 
 
 def run_c5(a, rank, world, local):
@@ -292,7 +312,8 @@ def main():
     }
     if not a.no_cpu_baseline and world == 1:
         host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
-        out["cpu_baseline"] = cpu_baseline(host, params, a.cpu_sample_s)
+        out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s)
+        out["ate"] = ate_block(host, opos, params, k0, local)
     print(json.dumps(out))
     if world > 1:
         import torch.distributed as dist

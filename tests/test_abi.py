@@ -4,6 +4,7 @@ import ctypes as C
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -60,3 +61,20 @@ def test_null_context_is_rejected():
     L = fmx.lib()
     assert L.fmx_sync(None) == 1  # FMX_E_INVAL
     assert L.fmx_last_error(None) == b"null context"
+
+
+def test_ate_rmse_alignment():
+    """ATE helper (form_amd.metrics): relative to the first pose, so a constant frame
+    offset costs nothing and a translation error shows up exactly."""
+    from form_amd import metrics, synth
+    gt = [synth.trajectory_pose(k) for k in range(10)]
+    off = np.eye(3, 4)
+    off[:, 3] = [5.0, -2.0, 1.0]
+    shifted = [metrics._mul(off, G) for G in gt]  # same trajectory, other world frame
+    assert metrics.ate_rmse(shifted, gt) < 1e-12
+    est = [metrics._mul(metrics._inv(gt[0]), G) for G in gt]  # estimator frame: identity at scan 0
+    assert metrics.ate_rmse(est, gt) < 1e-12
+    bad = [E.copy() for E in est]
+    for E in bad[1:]:
+        E[0, 3] += 0.01
+    assert abs(metrics.ate_rmse(bad, gt) - 0.01 * np.sqrt(9 / 10)) < 1e-12

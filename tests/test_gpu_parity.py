@@ -142,3 +142,25 @@ def test_register_stream_matches_oracle(fmx_mod, oracle):
         Tg = ctx.current_pose()
         To, st, _ = oest.register_scan(s.numpy())
         assert np.abs(Tg - To).max() < 1e-6, (k, np.abs(Tg - To).max())
+
+
+def test_ate_gpu_vs_oracle(fmx_mod, oracle):
+    """ATE stand-in: over a C2 stream the GPU path's ATE against the
+    synthetic ground truth is within 1 mm of the CPU oracle path's (the north star's
+    bar for the reference)."""
+    from form_amd import metrics
+    geo = synth.GEOMETRIES["c2"]
+    p = synth.default_params(geo)
+    world = synth.World()
+    ctx = _ctx(fmx_mod, p)
+    oest = oracle.Estimator(oracle.default_params(p))
+    gpu, cpu, gt = [], [], []
+    for k in range(20):
+        s, T, _ = synth.make_scan("c2", k, world=world)
+        ctx.register_scan(s.to("cuda:0"))
+        gpu.append(ctx.current_pose())
+        cpu.append(oest.register_scan(s.numpy())[0])
+        gt.append(T)
+    a_gpu, a_cpu = metrics.ate_rmse(gpu, gt), metrics.ate_rmse(cpu, gt)
+    assert abs(a_gpu - a_cpu) < 1e-3, (a_gpu, a_cpu)
+    assert a_gpu < 0.05, a_gpu  # the registration tracks the synthetic trajectory
