@@ -374,6 +374,7 @@ void set_queries_device(fmx_ctx* c, uint64_t scan, const float* plp, const float
   c->q_scan = scan;
   c->have_queries = true;
   c->have_match = false;
+  c->have_qo = false;
 }
 
 void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const float* pt, uint32_t npt) {
@@ -399,6 +400,7 @@ void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const
   c->q_scan = scan;
   c->have_queries = true;
   c->have_match = false;
+  c->have_qo = false;
 }
 
 void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out) {
@@ -422,6 +424,7 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
   c->q_scan = scan;
   c->have_queries = true;
   c->have_match = false;
+  c->have_qo = false;
 }
 
 }  // namespace
@@ -650,7 +653,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
       ++icp;
       const Pose before = e.values.at(j);
-      run_match(c, before.m, P.max_dist_matching, P.min_dist_map);
+      run_match(c, before.m, P.max_dist_matching, P.min_dist_map, nullptr, false);  // query order
       int li = 0;
       const Pose after = lm.optimize(before, &li);
       lm_it += li;
@@ -696,7 +699,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     };
     for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
       icp_launch(c, 0);
-      run_match(c, nullptr, P.max_dist_matching, P.min_dist_map, c->icp.p);
+      run_match(c, nullptr, P.max_dist_matching, P.min_dist_map, c->icp.p, false);
       lm_rounds(c, kRounds);
       icp_launch(c, 1);
       readback();

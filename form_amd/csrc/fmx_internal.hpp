@@ -49,6 +49,14 @@ struct DBuf {
     cap = 0;
   }
 };
+// Grow b to >= n elements; new storage is zeroed on stream st (for self-resetting
+// device counters).
+template <class T>
+void ensure_zeroed(DBuf<T>& b, size_t n, hipStream_t st) {
+  if (n <= b.cap) return;
+  b.ensure(n);
+  FMX_HIP(hipMemsetAsync(b.p, 0, b.cap * sizeof(T), st));
+}
 template <class T>
 struct HBuf {  // pinned host memory, also mapped into the device address space
   T* p = nullptr;
@@ -237,6 +245,9 @@ struct fmx_ctx {
   // ---- linearize
   fmx::DBuf<double> poses_ij, partials, G, bpart;  // bpart: k_linearize_total block partials
   fmx::DBuf<uint32_t> ticket;                     // its last-block ticket
+  fmx::DBuf<uint32_t> mcnt, mticket;              // query-order match: per-pair counters + ticket
+  uint32_t n_qo = 0;                              // queries of the last query-order match
+  bool have_qo = false;
   fmx::HBuf<double> h_poses, h_G;
   fmx::HBuf<int32_t> h_i32;
 
@@ -314,8 +325,11 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
 // stream so the build overlaps extraction)
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w,
                    hipStream_t st = nullptr);
+// icp != null: pose from the device ICP state.  sorted: bucket the accepted matches
+// pair-major into SoA correspondences (fmx_match / fmx_linearize); otherwise only the
+// per-pair counts are produced and register_scan linearizes in query order.
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,
-               const IcpDev* icp = nullptr);  // icp != null: pose from the device ICP state
+               const IcpDev* icp = nullptr, bool sorted = true);
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
 void match_counts_fetch(fmx_ctx* c);
 void icp_launch(fmx_ctx* c, int what);  // 0 begin ICP iteration, 1 end ICP iteration, 2 begin final LM

@@ -527,12 +527,22 @@ __device__ __forceinline__ double wave_reduce_scatter32(double (&v)[32]) {
   return v[0] + __shfl_xor(v[0], 1, 64);
 }
 
+// Rows in query order (the match outputs, no pair sort): query gq < nq_pl is a plane
+// row (p_i = m_pi, n_i = m_ni, p_j = q_pl), else a point pair (p_i = m_pi, p_j =
+// q_pt); m_pair < 0 (not accepted) contributes nothing; T_i = poses[m_pair].
+struct QoRows {
+  const int32_t* pair;
+  const double4* pi;
+  const double4* ni;
+  const float4* q_pl;
+  const float4* q_pt;
+  uint32_t nq_pl, nq;
+};
+
 template <bool DEVLM>
 __global__ __launch_bounds__(tot_waves<DEVLM>() * kWave) void k_linearize_total(
-    const Chunk* __restrict__ chunks, const uint32_t* __restrict__ n_chunks, const double* __restrict__ c_pl,
-    size_t ld_pl, const double* __restrict__ c_pt, size_t ld_pt, const double* __restrict__ poses, double inv,
-    double* __restrict__ bpart, uint32_t* __restrict__ ticket, double* __restrict__ out, IcpDev* __restrict__ icp,
-    Pose34 tjv) {
+    QoRows qo, const double* __restrict__ poses, double inv, double* __restrict__ bpart, uint32_t* __restrict__ ticket,
+    double* __restrict__ out, IcpDev* __restrict__ icp, Pose34 tjv) {
   constexpr int NG = 28;
   constexpr int kTotWaves = tot_waves<DEVLM>();
   constexpr int kTotGroups = kTotWaves * kWave / NG;  // final reduction: lane groups x 28 entries
@@ -542,25 +552,28 @@ __global__ __launch_bounds__(tot_waves<DEVLM>() * kWave) void k_linearize_total(
   double acc[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) acc[i] = 0.0;
-  if (n_chunks && ch < *n_chunks) {  // n_chunks null: no correspondences (K = 0)
-    const Chunk d = chunks[ch];
-    const double* Ti = poses + 12 * d.pair;
+  const uint32_t gq = ch * kWave + lane;
+  const int32_t pair = gq < qo.nq ? qo.pair[gq] : -1;
+  if (pair >= 0) {
+    const double* Ti = poses + 12 * pair;
     const double* Tj = icp ? (icp->phase == 0 ? icp->T : icp->Tn) : tjv.m;
     double H[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) H[i] = 0.0;
-    const uint32_t row = d.begin + lane;
-    if (row < d.end) {
-      if (d.type == 0) {
-        const double pi[3] = {c_pl[row], c_pl[ld_pl + row], c_pl[2 * ld_pl + row]};
-        const double ni[3] = {c_pl[3 * ld_pl + row], c_pl[4 * ld_pl + row], c_pl[5 * ld_pl + row]};
-        const double pj[3] = {c_pl[6 * ld_pl + row], c_pl[7 * ld_pl + row], c_pl[8 * ld_pl + row]};
+    const double4 p4 = qo.pi[gq];
+    const double pi[3] = {p4.x, p4.y, p4.z};
+    {
+      if (gq < qo.nq_pl) {
+        const double4 n4 = qo.ni[gq];
+        const float4 q = qo.q_pl[gq];
+        const double ni[3] = {n4.x, n4.y, n4.z};
+        const double pj[3] = {(double)q.x, (double)q.y, (double)q.z};
         double r;
         plane_row<1>(Ti, Tj, pi, ni, pj, r, H);
         accum_row<1>(H, r, inv, acc);
       } else {
-        const double pi[3] = {c_pt[row], c_pt[ld_pt + row], c_pt[2 * ld_pt + row]};
-        const double pj[3] = {c_pt[3 * ld_pt + row], c_pt[4 * ld_pt + row], c_pt[5 * ld_pt + row]};
+        const float4 q = qo.q_pt[gq - qo.nq_pl];
+        const double pj[3] = {(double)q.x, (double)q.y, (double)q.z};
         double wpi[3], wpj[3];
         d_xform(Ti, pi[0], pi[1], pi[2], wpi);
         d_xform(Tj, pj[0], pj[1], pj[2], wpj);
@@ -808,16 +821,19 @@ void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, 
 
 namespace fmx {
 
-// blocks of k_linearize_total for the current chunk table (+ the partial / ticket
-// buffers it needs; the ticket starts at 0 and the last block resets it)
+// blocks of k_linearize_total over the last query-order match (64 queries per wave)
+// (+ the partial / ticket buffers it needs; the ticket starts at 0 and the last block
+// resets it)
 static uint32_t tot_blocks(fmx_ctx* c, int waves) {
-  const uint32_t nblk = std::max<uint32_t>((c->max_chunks + waves - 1) / waves, 1);
+  const uint32_t nch = (c->n_qo + kWave - 1) / kWave;
+  const uint32_t nblk = std::max<uint32_t>((nch + waves - 1) / waves, 1);
   c->bpart.ensure((size_t)nblk * kTotLd);
-  if (!c->ticket.p) {
-    c->ticket.ensure(1);
-    FMX_HIP(hipMemsetAsync(c->ticket.p, 0, sizeof(uint32_t), c->stream));
-  }
+  ensure_zeroed(c->ticket, 1, c->stream);
   return nblk;
+}
+static QoRows qo_rows(fmx_ctx* c) {
+  return QoRows{c->m_pair.p, reinterpret_cast<const double4*>(c->m_pi.p), reinterpret_cast<const double4*>(c->m_ni.p),
+                c->q_pl_pos.p, c->q_pt_pos.p, c->n_qpl, c->n_qo};
 }
 
 void icp_launch(fmx_ctx* c, int what) {
@@ -831,14 +847,13 @@ void icp_launch(fmx_ctx* c, int what) {
 // `rounds` x (fused linearize + reduce + LM decision); no host sync.
 void lm_rounds(fmx_ctx* c, int rounds) {
   hipStream_t st = c->stream;
-  const int K = (int)c->K;
   const uint32_t nblk = tot_blocks(c, kTotWavesDev);
   const double inv = 1.0 / c->P.planar_constraint_sigma;
+  const QoRows qo = qo_rows(c);
   for (int r = 0; r < rounds; ++r) {
-    ProfScope ps(c->prof, PROF_LINEARIZE, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kTotLd * nblk, st);
-    // K = 0 still launches: the LM decides on the empty system (error 0 -> done)
-    hipLaunchKernelGGL(k_linearize_total<true>, dim3(K > 0 ? nblk : 1), dim3(kTotWavesDev * kWave), 0, st, c->chunks.p,
-                       K > 0 ? c->n_chunks.p : nullptr, c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt, c->map_poses_p,
+    ProfScope ps(c->prof, PROF_LINEARIZE, 4.0 * c->n_qo + 80.0 * c->rows_pl + 48.0 * c->rows_pt, st);
+    // K = 0 or no queries still launches: the LM decides on the empty system
+    hipLaunchKernelGGL(k_linearize_total<true>, dim3(nblk), dim3(kTotWavesDev * kWave), 0, st, qo, c->map_poses_p,
                        inv, c->bpart.p, c->ticket.p, (double*)nullptr, c->icp.p, Pose34{});
     FMX_HIP(hipGetLastError());
   }
@@ -848,20 +863,21 @@ void lm_rounds(fmx_ctx* c, int rounds) {
 // 7 x 7 [H_j b]^T [H_j b] at pose_j, out[28] = error.  One launch, one wait.
 void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, double* out) {
   if (!c->have_map) throw StatusError(FMX_E_STATE, "no map");
-  if (!c->have_corr) throw StatusError(FMX_E_STATE, "no correspondences");
+  if (!c->have_qo) throw StatusError(FMX_E_STATE, "no query-order match");
   hipStream_t st = c->stream;
   for (int i = 0; i < 29; ++i) out[i] = 0.0;
-  if (c->K == 0) return;
+  if (c->K == 0 || c->n_qo == 0) return;
   const uint32_t nblk = tot_blocks(c, kTotWavesHost);
   Pose34 tjv;
   std::memcpy(tjv.m, pose_j34, sizeof(tjv.m));
   c->h_G.ensure(32);
   if (c->counts_pending && c->prof.on) match_counts_fetch(c);  // exact byte model for the profile
   {
-    ProfScope ps(c->prof, PROF_LINEARIZE, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kTotLd * nblk, st);
-    hipLaunchKernelGGL(k_linearize_total<false>, dim3(nblk), dim3(kTotWavesHost * kWave), 0, st, c->chunks.p, c->n_chunks.p,
-                       c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt, c->map_poses_p, 1.0 / sigma, c->bpart.p,
-                       c->ticket.p, c->h_G.d, (IcpDev*)nullptr, tjv);
+    // bytes: pair id per query + (p_i, n_i 32 B each, p_j 16 B) per accepted plane row,
+    // (p_i 32 B, p_j 16 B) per accepted point pair
+    ProfScope ps(c->prof, PROF_LINEARIZE, 4.0 * c->n_qo + 80.0 * c->rows_pl + 48.0 * c->rows_pt, st);
+    hipLaunchKernelGGL(k_linearize_total<false>, dim3(nblk), dim3(kTotWavesHost * kWave), 0, st, qo_rows(c),
+                       c->map_poses_p, 1.0 / sigma, c->bpart.p, c->ticket.p, c->h_G.d, (IcpDev*)nullptr, tjv);
     FMX_HIP(hipGetLastError());
   }
   stream_wait(c);

@@ -154,6 +154,7 @@ struct MatchArgs {
   double max_d2, min_d2;
   uint32_t nq_pl, nq_pt, nb_pl, nb_pt;  // queries; planar / point blocks
   int K;
+  int sorted;  // 1: per-block pair histogram for the pair sort; 0: per-pair counts only
 };
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
@@ -172,7 +173,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
                                                          int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
                                                          double4* __restrict__ m_pi, double4* __restrict__ m_ni,
                                                          uint8_t* __restrict__ m_ins, uint32_t* __restrict__ hist,
-                                                         uint32_t* __restrict__ work, const IcpDev* __restrict__ icp) {
+                                                         uint32_t* __restrict__ work, const IcpDev* __restrict__ icp,
+                                                         uint32_t* __restrict__ mcnt, uint32_t* __restrict__ mticket,
+                                                         uint32_t* __restrict__ host_counts) {
   extern __shared__ uint32_t s_hist[];  // [K]
   if (icp && icp->icp_done) return;  // device ICP loop already converged
   const double* Tj = icp ? icp->Tbefore : a.Tj;
@@ -337,12 +340,31 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     work[2 * blockIdx.x] = tp;
     work[2 * blockIdx.x + 1] = tc;
   }
-  // pair-major layout [type][pair][block]: one exclusive scan gives every block's
-  // destination offset (k_pair_base / k_pair_scatter)
-  const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.nb_pl;
-  const uint32_t nbt = planar ? a.nb_pl : a.nb_pt;
-  const uint32_t bt = planar ? blockIdx.x : blockIdx.x - a.nb_pl;
-  for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[hbase + (size_t)k * nbt + bt] = s_hist[k];
+  if (a.sorted) {
+    // pair-major layout [type][pair][block]: one exclusive scan gives every block's
+    // destination offset (k_pair_base / k_pair_scatter)
+    const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.nb_pl;
+    const uint32_t nbt = planar ? a.nb_pl : a.nb_pt;
+    const uint32_t bt = planar ? blockIdx.x : blockIdx.x - a.nb_pl;
+    for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[hbase + (size_t)k * nbt + bt] = s_hist[k];
+    return;
+  }
+  // counts only: agent-scope adds into mcnt[type][pair], a ticket per block, and the
+  // last block moves the totals to pinned host memory and zeroes mcnt for the next
+  // launch (the adds are complete before each ticket: vmcnt(0) + barrier)
+  const int t = planar ? 0 : 1;
+  for (int k = threadIdx.x; k < a.K; k += kMatchThreads)
+    if (s_hist[k]) __hip_atomic_fetch_add(mcnt + (size_t)t * a.K + k, s_hist[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int s_last;
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(mticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
+    host_counts[i] = __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct HistIn {
@@ -620,9 +642,11 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   }
   c->have_map = true;
   c->have_match = false;
+  c->have_qo = false;
 }
 
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, const IcpDev* icp) {
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, const IcpDev* icp,
+               bool sorted) {
   hipStream_t st = c->stream;
   const int K = std::max<int>((int)c->K, 1);
   MatchArgs a;
@@ -643,6 +667,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   const uint32_t nb_pt = (c->n_qpt + kQPB - 1) / kQPB;
   a.nb_pt = nb_pt;
   a.K = (int)c->K;
+  a.sorted = sorted ? 1 : 0;
   const uint32_t nq = c->n_qpl + c->n_qpt;
   c->m_pair.ensure(nq + 1);
   c->m_d2.ensure(nq + 1);
@@ -666,6 +691,8 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->c_pt.ensure(6 * c->ld_pt);
   c->work.ensure(2 * (size_t)nb + 2);
   c->work_blocks = nb;
+  ensure_zeroed(c->mcnt, 2 * (size_t)K, st);
+  ensure_zeroed(c->mticket, 1, st);
   auto view = [&](int t) {
     VoxMap& M = c->map[t];
     return MapView{reinterpret_cast<const Slot*>(M.table.p), M.cap ? M.cap - 1 : 0, M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
@@ -679,10 +706,13 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
     hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
                        c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
-                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, icp);
+                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, icp, c->mcnt.p, c->mticket.p, c->h_counts.d);
     FMX_HIP(hipGetLastError());
   }
-  {
+  if (!sorted) {  // counts come from the match kernel's last block (none without queries)
+    if (nb == 0 && c->K > 0) FMX_HIP(hipMemsetAsync(c->h_counts.d, 0, 2 * c->K * sizeof(uint32_t), st));
+    c->n_qo = nq;
+  } else {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
     const size_t nh = (size_t)a.K * nb;
     c->scan_scratch.ensure(scan_scratch_size(nh) + 4);
@@ -707,7 +737,8 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   }
   c->counts_pending = true;
   c->have_match = true;
-  c->have_corr = true;
+  c->have_corr = sorted;  // pair-major correspondences for fmx_linearize
+  c->have_qo = true;      // query-order correspondences for register_scan
 }
 
 // Consume the asynchronously copied match counts (caller has synchronized or will).
