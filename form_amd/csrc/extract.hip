@@ -626,7 +626,8 @@ __device__ int fit_one(const float4* __restrict__ scan, const uint32_t* __restri
 
 // per-row offsets of {planar with normal, points, planar selected}: one block
 __global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, const uint32_t* row_ok, int R,
-                                                   uint32_t* row_off /* [3][R+1] */, uint32_t* host_totals) {
+                                                   uint32_t* row_off /* [3][R+1] */, uint32_t* host_totals,
+                                                   uint32_t* flag, uint32_t seq) {
   __shared__ uint32_t ws[16];
   __shared__ uint32_t carry[3];
   if (threadIdx.x < 3) carry[threadIdx.x] = 0;
@@ -655,6 +656,7 @@ __global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, c
     row_off[threadIdx.x * (R + 1) + R] = carry[threadIdx.x];
     host_totals[threadIdx.x] = carry[threadIdx.x];  // mapped host memory: no copy op
   }
+  if (threadIdx.x == 0) publish_flag(flag, seq);  // lanes 0-2 of this wave stored the totals
 }
 
 // ordered compaction of row slots into the query arrays (block per row)
@@ -770,14 +772,16 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
     hipLaunchKernelGGL(k_fit, dim3((a.cap_pl + 255) / 256, R), dim3(256), 0, st, d_scan, c->sel_slots.p,
                        c->row_counts.p, c->closest.p, a, c->nrm_slots.p, c->row_ok.p);
   }
+  uint32_t seq = 0;
   {
     ProfScope ps(c->prof, PROF_COMPACT, 0.0, st);
+    seq = next_flag(c);
     hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, st, c->row_counts.p, c->row_ok.p, R, c->row_off.p,
-                       c->h_u32.d);
+                       c->h_u32.d, c->h_flag.d, seq);
   }
   FMX_HIP(hipGetLastError());
   // totals (planar-with-normal, points, selected) were written to mapped host memory
-  stream_wait(c);
+  wait_flag(c, c->h_flag.p, seq);
   const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
   c->q_pl_pos.ensure(npl + 1);
   c->q_pl_nrm.ensure(npl + 1);

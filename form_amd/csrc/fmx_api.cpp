@@ -693,24 +693,20 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     hs.ended = -1;
     hs.K = (int32_t)c->K;
     FMX_HIP(hipMemcpyAsync(c->icp.p, &hs, sizeof(IcpDev), hipMemcpyHostToDevice, c->stream));
-    auto readback = [&]() {
-      FMX_HIP(hipMemcpyAsync(&hs, c->icp.p, sizeof(IcpDev), hipMemcpyDeviceToHost, c->stream));
-      stream_wait(c);
-    };
+    // the state comes back through pinned mapped memory (h_icp) behind a flag
+    auto readback = [&](bool end) { icp_launch(c, end ? 1 : 3); };
     for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
       icp_launch(c, 0);
       run_match(c, nullptr, P.max_dist_matching, P.min_dist_map, c->icp.p, false);
       lm_rounds(c, kRounds);
-      icp_launch(c, 1);
-      readback();
+      readback(true);
       for (int more = 0; !hs.icp_done && hs.phase != 2; ++more) {  // LM needs more rounds
         if (more > 40)  // 160 rounds > GTSAM's 100 LM iterations: the state machine is stuck
           throw StatusError(FMX_E_STATE, "device LM made no progress (phase " + std::to_string(hs.phase) +
                                              ", lins " + std::to_string(hs.lins) + ", lm_iters " +
                                              std::to_string(hs.lm_iters) + ")");
         lm_rounds(c, kRounds);
-        icp_launch(c, 1);
-        readback();
+        readback(true);
       }
       if (hs.icp_done) break;
     }
@@ -719,7 +715,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       for (int more = 0; hs.phase != 2; ++more) {
         if (more > 40) throw StatusError(FMX_E_STATE, "device LM made no progress (final optimize)");
         lm_rounds(c, kRounds);
-        readback();
+        readback(false);
       }
       hs.lm_total += hs.lm_iters;
     }
@@ -862,7 +858,8 @@ void fmx_destroy(fmx_ctx* c) {
   c->hist.release(); c->hist_off.release(); c->c_pl.release(); c->c_pt.release(); c->pair_counts.release();
   c->chunk_range.release(); c->chunks.release(); c->n_chunks.release(); c->poses_ij.release();
   c->partials.release(); c->G.release(); c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
-  c->h_corr.release(); c->h_meta.release(); c->h_counts.release();
+  c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
+  c->mcnt.release(); c->mticket.release(); c->iticket.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);

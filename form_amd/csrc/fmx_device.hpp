@@ -65,6 +65,18 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// ---------------------------------------------------------------- host completion word
+// Publish seq at the mapped host word `flag` after this wave's earlier stores (to
+// mapped host memory or device memory) are complete and released to the system
+// (host side: wait_flag in fmx_internal.hpp).  Call from ONE lane of the wave that
+// made the stores (other waves: drain + barrier before).
+__device__ __forceinline__ void publish_flag(uint32_t* flag, uint32_t seq) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------- device-wide scan
 // Exclusive scan of n uint32 values produced by in(i) into out(i, v); *total = sum.
 // Three launches (tile reduce, block-sum scan, tile scan): deterministic.

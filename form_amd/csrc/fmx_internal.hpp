@@ -246,7 +246,10 @@ struct fmx_ctx {
   fmx::DBuf<double> poses_ij, partials, G, bpart;  // bpart: k_linearize_total block partials
   fmx::DBuf<uint32_t> ticket;                     // its last-block ticket
   fmx::DBuf<uint32_t> mcnt, mticket;              // query-order match: per-pair counters + ticket
+  fmx::DBuf<uint32_t> iticket;                    // k_insert ticket
   uint32_t n_qo = 0;                              // queries of the last query-order match
+  fmx::HBuf<uint32_t> h_flag;                     // mapped completion word (wait_flag)
+  uint32_t flag_seq = 0;
   bool have_qo = false;
   fmx::HBuf<double> h_poses, h_G;
   fmx::HBuf<int32_t> h_i32;
@@ -319,6 +322,33 @@ inline void stream_wait(fmx_ctx* c) {
     if (e != hipErrorNotReady) throw HipError(std::string("hipStreamQuery: ") + hipGetErrorString(e));
   }
 }
+// Wait until a kernel has published sequence number seq at the mapped host word f
+// (its last block stores results, drains, releases at system scope, then stores
+// seq).  Cheaper than a stream round trip: the host resumes as soon as the word
+// lands, before the kernel retires.  A stream that went idle without the word, or a
+// stream error, throws (no silent hang).
+inline void wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq) {
+  HostScope hs(1);
+  for (uint32_t spins = 1;; ++spins) {
+    if (*f == seq) break;
+    if ((spins & 0x3FFF) == 0) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e == hipSuccess) {
+        if (*f == seq) break;
+        throw HipError("kernel completed without publishing its result flag");
+      }
+      if (e != hipErrorNotReady) throw HipError(std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+inline uint32_t next_flag(fmx_ctx* c) {
+  if (!c->h_flag.p) {
+    c->h_flag.ensure(1);
+    c->h_flag.p[0] = 0;
+  }
+  return ++c->flag_seq;
+}
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out);
 // st: stream to build on (default the context stream; register_scan uses the side
@@ -331,8 +361,12 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,
                const IcpDev* icp = nullptr, bool sorted = true);
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
-void match_counts_fetch(fmx_ctx* c);
-void icp_launch(fmx_ctx* c, int what);  // 0 begin ICP iteration, 1 end ICP iteration, 2 begin final LM
+// wait = false: the caller knows the match kernel has completed (a later kernel in
+// stream order published a flag)
+void match_counts_fetch(fmx_ctx* c, bool wait = true);
+// 0 begin ICP iteration, 1 end ICP iteration + state to host (waits), 2 begin final LM,
+// 3 state to host (waits)
+void icp_launch(fmx_ctx* c, int what);
 void lm_rounds(fmx_ctx* c, int rounds);
 void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
                    double* G_out, double* err_out);

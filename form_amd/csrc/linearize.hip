@@ -542,7 +542,7 @@ struct QoRows {
 template <bool DEVLM>
 __global__ __launch_bounds__(tot_waves<DEVLM>() * kWave) void k_linearize_total(
     QoRows qo, const double* __restrict__ poses, double inv, double* __restrict__ bpart, uint32_t* __restrict__ ticket,
-    double* __restrict__ out, IcpDev* __restrict__ icp, Pose34 tjv) {
+    double* __restrict__ out, IcpDev* __restrict__ icp, Pose34 tjv, uint32_t* __restrict__ flag, uint32_t seq) {
   constexpr int NG = 28;
   constexpr int kTotWaves = tot_waves<DEVLM>();
   constexpr int kTotGroups = kTotWaves * kWave / NG;  // final reduction: lane groups x 28 entries
@@ -632,7 +632,10 @@ __global__ __launch_bounds__(tot_waves<DEVLM>() * kWave) void k_linearize_total(
       if (!icp) out[NG] = 0.5 * s;
     }
   }
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (flag) publish_flag(flag, seq);  // out[] was stored by this wave
+  }
   __syncthreads();
   if constexpr (DEVLM) {
     if (threadIdx.x == 0) lm_decide(icp, sS, sS[NG]);
@@ -648,18 +651,27 @@ __global__ void k_icp_begin(IcpDev* s) {
   s->lm_iters = 0;
   s->icp_iters++;
 }
-// form.cpp:83-88: stop if ||before.localCoordinates(after)|| < threshold, else
-// update_current_pose(after).
-__global__ void k_icp_end(IcpDev* s, double thr) {
-  if (s->icp_done || s->phase != 2 || s->ended == s->icp_iters) return;
-  s->ended = s->icp_iters;
-  s->lm_total += s->lm_iters;
-  double Bi[12], D[12];
-  dpose_inverse(s->Tbefore, Bi);
-  dpose_compose(Bi, s->T, D);
-  if (dpose_lognorm(D) < thr) s->icp_done = 1;
-  else
-    for (int i = 0; i < 12; ++i) s->Tcur[i] = s->T[i];
+// form.cpp:83-88 (end != 0): stop if ||before.localCoordinates(after)|| < threshold,
+// else update_current_pose(after).  Then one wave copies the state to pinned host
+// memory and publishes the completion word (the host's once-per-ICP-iteration read).
+__global__ __launch_bounds__(64) void k_icp_end(IcpDev* s, int end, double thr, IcpDev* host, uint32_t* flag,
+                                                uint32_t seq) {
+  if (threadIdx.x == 0 && end && !(s->icp_done || s->phase != 2 || s->ended == s->icp_iters)) {
+    s->ended = s->icp_iters;
+    s->lm_total += s->lm_iters;
+    double Bi[12], D[12];
+    dpose_inverse(s->Tbefore, Bi);
+    dpose_compose(Bi, s->T, D);
+    if (dpose_lognorm(D) < thr) s->icp_done = 1;
+    else
+      for (int i = 0; i < 12; ++i) s->Tcur[i] = s->T[i];
+  }
+  __syncthreads();
+  static_assert(sizeof(IcpDev) % 4 == 0, "IcpDev copied as words");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(s);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(host);
+  for (int i = threadIdx.x; i < (int)(sizeof(IcpDev) / 4); i += 64) dst[i] = src[i];
+  if (threadIdx.x == 0) publish_flag(flag, seq);  // the single wave made every store
 }
 // optimize(false) after an unconverged loop: LM from the current pose.
 __global__ void k_lm_begin(IcpDev* s) {
@@ -839,8 +851,14 @@ static QoRows qo_rows(fmx_ctx* c) {
 void icp_launch(fmx_ctx* c, int what) {
   hipStream_t st = c->stream;
   if (what == 0) hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, st, c->icp.p);
-  else if (what == 1) hipLaunchKernelGGL(k_icp_end, dim3(1), dim3(1), 0, st, c->icp.p, c->P.new_pose_threshold);
-  else hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(1), 0, st, c->icp.p);
+  else if (what == 1 || what == 3) {  // 1: end the ICP iteration + read back; 3: read back only
+    const uint32_t seq = next_flag(c);
+    hipLaunchKernelGGL(k_icp_end, dim3(1), dim3(64), 0, st, c->icp.p, what == 1 ? 1 : 0, c->P.new_pose_threshold,
+                       c->h_icp.d, c->h_flag.d, seq);
+    FMX_HIP(hipGetLastError());
+    wait_flag(c, c->h_flag.p, seq);
+    return;
+  } else hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(1), 0, st, c->icp.p);
   FMX_HIP(hipGetLastError());
 }
 
@@ -854,7 +872,7 @@ void lm_rounds(fmx_ctx* c, int rounds) {
     ProfScope ps(c->prof, PROF_LINEARIZE, 4.0 * c->n_qo + 80.0 * c->rows_pl + 48.0 * c->rows_pt, st);
     // K = 0 or no queries still launches: the LM decides on the empty system
     hipLaunchKernelGGL(k_linearize_total<true>, dim3(nblk), dim3(kTotWavesDev * kWave), 0, st, qo, c->map_poses_p,
-                       inv, c->bpart.p, c->ticket.p, (double*)nullptr, c->icp.p, Pose34{});
+                       inv, c->bpart.p, c->ticket.p, (double*)nullptr, c->icp.p, Pose34{}, (uint32_t*)nullptr, 0u);
     FMX_HIP(hipGetLastError());
   }
 }
@@ -871,17 +889,19 @@ void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, doubl
   Pose34 tjv;
   std::memcpy(tjv.m, pose_j34, sizeof(tjv.m));
   c->h_G.ensure(32);
+  const uint32_t seq = next_flag(c);
   if (c->counts_pending && c->prof.on) match_counts_fetch(c);  // exact byte model for the profile
   {
     // bytes: pair id per query + (p_i, n_i 32 B each, p_j 16 B) per accepted plane row,
     // (p_i 32 B, p_j 16 B) per accepted point pair
     ProfScope ps(c->prof, PROF_LINEARIZE, 4.0 * c->n_qo + 80.0 * c->rows_pl + 48.0 * c->rows_pt, st);
     hipLaunchKernelGGL(k_linearize_total<false>, dim3(nblk), dim3(kTotWavesHost * kWave), 0, st, qo_rows(c),
-                       c->map_poses_p, 1.0 / sigma, c->bpart.p, c->ticket.p, c->h_G.d, (IcpDev*)nullptr, tjv);
+                       c->map_poses_p, 1.0 / sigma, c->bpart.p, c->ticket.p, c->h_G.d, (IcpDev*)nullptr, tjv,
+                       c->h_flag.d, seq);
     FMX_HIP(hipGetLastError());
   }
-  stream_wait(c);
-  match_counts_fetch(c);  // already copied; no extra wait
+  wait_flag(c, c->h_flag.p, seq);
+  match_counts_fetch(c, false);  // the match kernel finished before this one started
   std::memcpy(out, c->h_G.p, 29 * sizeof(double));
 }
 

@@ -512,31 +512,79 @@ __global__ __launch_bounds__(64) void k_pair_scatter(uint32_t nq_pl, uint32_t nq
   }
 }
 
-struct InsIn {
-  const uint8_t* f;
-  __device__ uint32_t operator()(size_t i) const { return f[i]; }
+// KeypointMap::insert_matches for both feature types in one launch (map.tpp:148-165):
+// block t stably compacts the queries of type t whose NN distance exceeded
+// min_dist_map (m_ins) onto the end of the type's keypoint store, tile by tile
+// (carry in LDS); it stores its count to pinned host memory and releases it; the
+// last block by ticket publishes the completion word.
+struct InsArgs {
+  uint32_t nq_pl, nq_pt;
+  const uint8_t* ins;  // [nq_pl + nq_pt]
+  const float4* q_pl;
+  const float4* q_pl_nrm;
+  const float4* q_pt;
+  float4* d_pl_pos;  // pool ends
+  float4* d_pl_nrm;
+  float4* d_pt_pos;
+  uint32_t* host_tot;  // [2], mapped
+  uint32_t* ticket;
+  uint32_t* flag;
+  uint32_t seq;
 };
-struct InsOutPl {
-  const uint8_t* f;
-  const float4* pos;
-  const float4* nrm;
-  float4* dpos;
-  float4* dnrm;
-  __device__ void operator()(size_t i, uint32_t o) const {
-    if (f[i]) {
-      dpos[o] = pos[i];
-      dnrm[o] = nrm[i];
+__global__ __launch_bounds__(kScanThreads) void k_insert(InsArgs a) {
+  __shared__ uint32_t ws[kScanThreads / kWave];
+  __shared__ uint32_t carry;
+  const int t = blockIdx.x;
+  const uint32_t n = t == 0 ? a.nq_pl : a.nq_pt;
+  const uint8_t* f = a.ins + (t == 0 ? 0 : a.nq_pl);
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int w = threadIdx.x / kWave;
+  for (uint32_t t0 = 0; t0 < n; t0 += kScanTile) {
+    const uint32_t base = t0 + threadIdx.x * kScanItems;
+    uint32_t fl[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      fl[j] = base + j < n ? f[base + j] : 0u;
+      s += fl[j];
+    }
+    const uint32_t incl = wave_incl_scan(s);
+    if (lane_id() == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < kScanThreads / kWave; ++i) {
+      if (i < w) off += ws[i];
+      tot += ws[i];
+    }
+    uint32_t o = carry + off + incl - s;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      if (fl[j]) {
+        const uint32_t i = base + j;
+        if (t == 0) {
+          a.d_pl_pos[o] = a.q_pl[i];
+          a.d_pl_nrm[o] = a.q_pl_nrm[i];
+        } else {
+          a.d_pt_pos[o] = a.q_pt[i];
+        }
+        ++o;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.host_tot[t] = carry;
+    publish_flag(a.host_tot + 2 + t, 1u);  // drain + system release of this block's count (word unused)
+    const bool last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
+    if (last) {
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      publish_flag(a.flag, a.seq);
     }
   }
-};
-struct InsOutPt {
-  const uint8_t* f;
-  const float4* pos;
-  float4* dpos;
-  __device__ void operator()(size_t i, uint32_t o) const {
-    if (f[i]) dpos[o] = pos[i];
-  }
-};
+}
 
 uint64_t next_pow2(uint64_t v) {
   uint64_t p = 1;
@@ -742,9 +790,9 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
 }
 
 // Consume the asynchronously copied match counts (caller has synchronized or will).
-void match_counts_fetch(fmx_ctx* c) {
+void match_counts_fetch(fmx_ctx* c, bool wait) {
   if (!c->counts_pending) return;
-  stream_wait(c);
+  if (wait) stream_wait(c);
   const int K = std::max<int>((int)c->K, 1);
   c->cnt_pl.assign(c->h_counts.p, c->h_counts.p + c->K);
   c->cnt_pt.assign(c->h_counts.p + c->K, c->h_counts.p + 2 * c->K);
@@ -769,27 +817,34 @@ void match_counts_fetch(fmx_ctx* c) {
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
   hipStream_t st = c->stream;
   uint32_t tot[2] = {0, 0};
-  c->dev_u32.ensure(8);
   c->h_u32.ensure(8);
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < 2; ++t) {  // worst case every query inserted
     const uint32_t nq = t == 0 ? c->n_qpl : c->n_qpt;
-    const uint8_t* f = c->m_ins.p + (t == 0 ? 0 : c->n_qpl);
-    Pool& pool = c->pool[t];
-    // worst case every query inserted
-    if (pool.used + nq > pool.pos.cap) throw StatusError(FMX_E_OOM, "keypoint pool capacity exceeded");
-    c->scan_scratch_half = std::max<size_t>(scan_scratch_size(std::max(c->n_qpl, c->n_qpt)) + 4, 64);
-    c->scan_scratch.ensure(2 * c->scan_scratch_half);
-    ProfScope ps(c->prof, PROF_INSERT, (t == 0 ? 33.0 : 17.0) * nq, st);
-    if (t == 0)
-      exclusive_scan(InsIn{f}, InsOutPl{f, c->q_pl_pos.p, c->q_pl_nrm.p, pool.pos.p + pool.used, pool.nrm.p + pool.used},
-                     nq, c->scan_scratch.p + t * c->scan_scratch_half, c->h_u32.d + t, st);
-    else
-      exclusive_scan(InsIn{f}, InsOutPt{f, c->q_pt_pos.p, pool.pos.p + pool.used}, nq,
-                     c->scan_scratch.p + t * c->scan_scratch_half, c->h_u32.d + t, st);
+    if (c->pool[t].used + nq > c->pool[t].pos.cap) throw StatusError(FMX_E_OOM, "keypoint pool capacity exceeded");
   }
-  stream_wait(c);
+  ensure_zeroed(c->iticket, 1, st);
+  InsArgs ia;
+  ia.nq_pl = c->n_qpl;
+  ia.nq_pt = c->n_qpt;
+  ia.ins = c->m_ins.p;
+  ia.q_pl = c->q_pl_pos.p;
+  ia.q_pl_nrm = c->q_pl_nrm.p;
+  ia.q_pt = c->q_pt_pos.p;
+  ia.d_pl_pos = c->pool[0].pos.p + c->pool[0].used;
+  ia.d_pl_nrm = c->pool[0].nrm.p + c->pool[0].used;
+  ia.d_pt_pos = c->pool[1].pos.p + c->pool[1].used;
+  ia.host_tot = c->h_u32.d + 4;
+  ia.ticket = c->iticket.p;
+  ia.seq = next_flag(c);
+  ia.flag = c->h_flag.d;
+  {
+    ProfScope ps(c->prof, PROF_INSERT, 33.0 * c->n_qpl + 17.0 * c->n_qpt, st);
+    hipLaunchKernelGGL(k_insert, dim3(2), dim3(kScanThreads), 0, st, ia);
+    FMX_HIP(hipGetLastError());
+  }
+  wait_flag(c, c->h_flag.p, ia.seq);
   for (int t = 0; t < 2; ++t) {
-    tot[t] = (t == 0 ? c->n_qpl : c->n_qpt) ? c->h_u32.p[t] : 0u;
+    tot[t] = c->h_u32.p[4 + t];
     Pool& pool = c->pool[t];
     auto& rg = pool.ranges[scan];
     if (rg.second == 0) rg.first = pool.used;
