@@ -654,7 +654,7 @@ __global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, c
   }
   if (threadIdx.x < 3) {
     row_off[threadIdx.x * (R + 1) + R] = carry[threadIdx.x];
-    host_totals[threadIdx.x] = carry[threadIdx.x];  // mapped host memory: no copy op
+    host_store(host_totals + threadIdx.x, carry[threadIdx.x]);  // mapped host memory: no copy op
   }
   if (threadIdx.x == 0) publish_flag(flag, seq);  // lanes 0-2 of this wave stored the totals
 }
@@ -783,11 +783,15 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   // totals (planar-with-normal, points, selected) were written to mapped host memory
   wait_flag(c, c->h_flag.p, seq);
   const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
-  c->q_pl_pos.ensure(npl + 1);
-  c->q_pl_nrm.ensure(npl + 1);
-  c->q_pl_idx.ensure(npl + 1);
-  c->q_pt_pos.ensure(npt + 1);
-  c->q_pt_idx.ensure(npt + 1);
+  // sized for the worst case, not the totals just read: a wrong total can then never
+  // turn into an out-of-bounds write
+  const size_t max_pl = (size_t)R * a.cap_pl, max_pt = (size_t)R * a.cap_pt;
+  if (npl > max_pl || npt > max_pt || nsel > max_pl) throw StatusError(FMX_E_HIP, "implausible feature totals");
+  c->q_pl_pos.ensure(max_pl + 1);
+  c->q_pl_nrm.ensure(max_pl + 1);
+  c->q_pl_idx.ensure(max_pl + 1);
+  c->q_pt_pos.ensure(max_pt + 1);
+  c->q_pt_idx.ensure(max_pt + 1);
   {
     ProfScope ps(c->prof, PROF_COMPACT, 32.0 * npl + 16.0 * npt, st);
     hipLaunchKernelGGL(k_write_features, dim3(R), dim3(256), 0, st, d_scan, a, c->row_counts.p, c->row_off.p,

@@ -66,13 +66,23 @@ __device__ __forceinline__ T wave_sum(T v) {
 }
 
 // ---------------------------------------------------------------- host completion word
-// Publish seq at the mapped host word `flag` after this wave's earlier stores (to
-// mapped host memory or device memory) are complete and released to the system
-// (host side: wait_flag in fmx_internal.hpp).  Call from ONE lane of the wave that
-// made the stores (other waves: drain + barrier before).
+// Results the host polls for go to pinned host memory with SYSTEM-scope stores
+// (host_store: sc0 sc1, written through, never left dirty in the GPU L2); the wave
+// that made them drains (vmcnt 0) and then stores the completion word the same way
+// (publish_flag; host side: wait_flag in fmx_internal.hpp).  MI355X_MICROARCH.md
+// lists this write-through form as valid without a release fence; a system release
+// (buffer_wbl2) would write back every dirty L2 line of the XCD instead.  Plain
+// stores to host memory CAN sit in L2: with plain payload stores and no fence the
+// host once read stale totals behind a fresh word.  Call publish_flag from ONE lane
+// of the wave that made every host_store it covers.
+__device__ __forceinline__ void host_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void host_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void publish_flag(uint32_t* flag, uint32_t seq) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

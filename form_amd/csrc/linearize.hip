@@ -626,10 +626,10 @@ __global__ __launch_bounds__(tot_waves<DEVLM>() * kWave) void k_linearize_total(
 #pragma unroll
     for (int j = 1; j < kTotGroups; ++j) s += sq[j][e];
     sS[e] = s;
-    if (!icp) out[e] = s;
+    if (!icp) host_store(out + e, s);
     if (e == NG - 1) {
       sS[NG] = 0.5 * s;
-      if (!icp) out[NG] = 0.5 * s;
+      if (!icp) host_store(out + NG, 0.5 * s);
     }
   }
   if (threadIdx.x == 0) {
@@ -670,7 +670,7 @@ __global__ __launch_bounds__(64) void k_icp_end(IcpDev* s, int end, double thr, 
   static_assert(sizeof(IcpDev) % 4 == 0, "IcpDev copied as words");
   const uint32_t* src = reinterpret_cast<const uint32_t*>(s);
   uint32_t* dst = reinterpret_cast<uint32_t*>(host);
-  for (int i = threadIdx.x; i < (int)(sizeof(IcpDev) / 4); i += 64) dst[i] = src[i];
+  for (int i = threadIdx.x; i < (int)(sizeof(IcpDev) / 4); i += 64) host_store(dst + i, src[i]);
   if (threadIdx.x == 0) publish_flag(flag, seq);  // the single wave made every store
 }
 // optimize(false) after an unconverged loop: LM from the current pose.

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   __syncthreads();
   if (!s_last) return;
   for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
-    host_counts[i] = __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -411,8 +411,8 @@ __global__ __launch_bounds__(1024) void k_pair_base(int K, uint32_t nb_pl, uint3
       b_pt -= tot_pl;
       pair_counts[k] = npl;
       pair_counts[K + k] = npt;
-      host_counts[k] = npl;  // mapped host memory
-      host_counts[K + k] = npt;
+      host_store(host_counts + k, npl);  // mapped host memory
+      host_store(host_counts + K + k, npt);
       pair_base[k] = b_pl;
       pair_base[K + k] = b_pt;
     }
@@ -576,8 +576,8 @@ __global__ __launch_bounds__(kScanThreads) void k_insert(InsArgs a) {
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    a.host_tot[t] = carry;
-    publish_flag(a.host_tot + 2 + t, 1u);  // drain + system release of this block's count (word unused)
+    host_store(a.host_tot + t, carry);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // complete before the ticket
     const bool last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
     if (last) {
       __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
