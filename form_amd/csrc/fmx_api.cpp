@@ -859,7 +859,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->chunk_range.release(); c->chunks.release(); c->n_chunks.release(); c->poses_ij.release();
   c->partials.release(); c->G.release(); c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
-  c->mcnt.release(); c->mticket.release(); c->iticket.release();
+  c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);

@@ -246,7 +246,9 @@ struct fmx_ctx {
   fmx::DBuf<double> poses_ij, partials, G, bpart;  // bpart: k_linearize_total block partials
   fmx::DBuf<uint32_t> ticket;                     // its last-block ticket
   fmx::DBuf<uint32_t> mcnt, mticket;              // query-order match: per-pair counters + ticket
-  fmx::DBuf<uint32_t> iticket;                    // k_insert ticket
+  fmx::DBuf<uint32_t> ins_blk, ins_off;           // per match block insert counts / offsets
+  uint32_t ins_tot[2] = {0, 0};                   // insert totals of the last match
+  uint32_t match_nb_pl = 0, match_nb = 0;         // blocks of the last match
   uint32_t n_qo = 0;                              // queries of the last query-order match
   fmx::HBuf<uint32_t> h_flag;                     // mapped completion word (wait_flag)
   uint32_t flag_seq = 0;

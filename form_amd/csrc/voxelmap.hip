@@ -175,7 +175,8 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
                                                          uint8_t* __restrict__ m_ins, uint32_t* __restrict__ hist,
                                                          uint32_t* __restrict__ work, const IcpDev* __restrict__ icp,
                                                          uint32_t* __restrict__ mcnt, uint32_t* __restrict__ mticket,
-                                                         uint32_t* __restrict__ host_counts) {
+                                                         uint32_t* __restrict__ host_counts,
+                                                         uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off) {
   extern __shared__ uint32_t s_hist[];  // [K]
   if (icp && icp->icp_done) return;  // device ICP loop already converged
   const double* Tj = icp ? icp->Tbefore : a.Tj;
@@ -184,7 +185,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   const int g = threadIdx.x % kGroup;
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
   const MapView& M = planar ? mp : mt;
+  __shared__ uint32_t s_ins;
   for (int k = threadIdx.x; k < a.K; k += kMatchThreads) s_hist[k] = 0;
+  if (threadIdx.x == 0) s_ins = 0;
   __syncthreads();
   uint32_t n_probe = 0, n_cand = 0;
   if (qi < nq) {
@@ -318,7 +321,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       m_d2[gq] = found ? best : DBL_MAX;
       m_pi[gq] = pi;
       if (planar) m_ni[qi] = ni;
-      m_ins[gq] = (!found || best > a.min_d2) ? 1 : 0;
+      const bool ins = !found || best > a.min_d2;
+      m_ins[gq] = ins ? 1 : 0;
+      if (ins) atomicAdd(&s_ins, 1u);
       if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
     }
   }
@@ -340,6 +345,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     work[2 * blockIdx.x] = tp;
     work[2 * blockIdx.x + 1] = tc;
   }
+  if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
+    __hip_atomic_store(ins_blk + blockIdx.x, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int t = planar ? 0 : 1;
   if (a.sorted) {
     // pair-major layout [type][pair][block]: one exclusive scan gives every block's
     // destination offset (k_pair_base / k_pair_scatter)
@@ -347,14 +355,15 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     const uint32_t nbt = planar ? a.nb_pl : a.nb_pt;
     const uint32_t bt = planar ? blockIdx.x : blockIdx.x - a.nb_pl;
     for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[hbase + (size_t)k * nbt + bt] = s_hist[k];
-    return;
+  } else {
+    // counts only: agent-scope adds into mcnt[type][pair]
+    for (int k = threadIdx.x; k < a.K; k += kMatchThreads)
+      if (s_hist[k])
+        __hip_atomic_fetch_add(mcnt + (size_t)t * a.K + k, s_hist[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // counts only: agent-scope adds into mcnt[type][pair], a ticket per block, and the
-  // last block moves the totals to pinned host memory and zeroes mcnt for the next
-  // launch (the adds are complete before each ticket: vmcnt(0) + barrier)
-  const int t = planar ? 0 : 1;
-  for (int k = threadIdx.x; k < a.K; k += kMatchThreads)
-    if (s_hist[k]) __hip_atomic_fetch_add(mcnt + (size_t)t * a.K + k, s_hist[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // a ticket per block (its agent-scope stores / adds are complete first: vmcnt(0) +
+  // barrier); the last block publishes the pair counts (counts mode, zeroing mcnt
+  // for the next launch) and scans the per-block insert counts into offsets + totals
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ int s_last;
@@ -362,8 +371,35 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     s_last = __hip_atomic_fetch_add(mticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
-    host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (!a.sorted)
+    for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
+      host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  __shared__ uint32_t ws[kMatchThreads / kWave];
+  __shared__ uint32_t carry;
+  for (int tt = 0; tt < 2; ++tt) {  // planar blocks [0, nb_pl), point blocks [nb_pl, nb)
+    const uint32_t b0 = tt == 0 ? 0u : a.nb_pl, b1 = tt == 0 ? a.nb_pl : a.nb_pl + a.nb_pt;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t s0 = b0; s0 < b1; s0 += kMatchThreads) {
+      const uint32_t b = s0 + threadIdx.x;
+      const uint32_t val =
+          b < b1 ? __hip_atomic_load(ins_blk + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const uint32_t incl = wave_incl_scan(val);
+      const int w = threadIdx.x / kWave;
+      if (lane_id() == 63) ws[w] = incl;
+      __syncthreads();
+      uint32_t off = 0, tot = 0;
+      for (int i = 0; i < kMatchThreads / kWave; ++i) {
+        if (i < w) off += ws[i];
+        tot += ws[i];
+      }
+      if (b < b1) ins_off[b] = carry + off + incl - val;
+      __syncthreads();
+      if (threadIdx.x == 0) carry += tot;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, carry);
+  }
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -512,77 +548,35 @@ __global__ __launch_bounds__(64) void k_pair_scatter(uint32_t nq_pl, uint32_t nq
   }
 }
 
-// KeypointMap::insert_matches for both feature types in one launch (map.tpp:148-165):
-// block t stably compacts the queries of type t whose NN distance exceeded
-// min_dist_map (m_ins) onto the end of the type's keypoint store, tile by tile
-// (carry in LDS); it stores its count to pinned host memory and releases it; the
-// last block by ticket publishes the completion word.
+// KeypointMap::insert_matches (map.tpp:148-165) for both feature types in one
+// launch: wave b covers the 64 queries of match block b and appends those whose NN
+// distance exceeded min_dist_map (m_ins) to the type's keypoint store, in query
+// order, at the block offset the match kernel's last block scanned (ins_off).
 struct InsArgs {
-  uint32_t nq_pl, nq_pt;
-  const uint8_t* ins;  // [nq_pl + nq_pt]
+  uint32_t nq_pl, nq_pt, nb_pl;
+  const uint8_t* ins;       // [nq_pl + nq_pt]
+  const uint32_t* ins_off;  // [nb] per match block, per type
   const float4* q_pl;
   const float4* q_pl_nrm;
   const float4* q_pt;
   float4* d_pl_pos;  // pool ends
   float4* d_pl_nrm;
   float4* d_pt_pos;
-  uint32_t* host_tot;  // [2], mapped
-  uint32_t* ticket;
-  uint32_t* flag;
-  uint32_t seq;
 };
-__global__ __launch_bounds__(kScanThreads) void k_insert(InsArgs a) {
-  __shared__ uint32_t ws[kScanThreads / kWave];
-  __shared__ uint32_t carry;
-  const int t = blockIdx.x;
-  const uint32_t n = t == 0 ? a.nq_pl : a.nq_pt;
-  const uint8_t* f = a.ins + (t == 0 ? 0 : a.nq_pl);
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  const int w = threadIdx.x / kWave;
-  for (uint32_t t0 = 0; t0 < n; t0 += kScanTile) {
-    const uint32_t base = t0 + threadIdx.x * kScanItems;
-    uint32_t fl[kScanItems];
-    uint32_t s = 0;
-#pragma unroll
-    for (int j = 0; j < kScanItems; ++j) {
-      fl[j] = base + j < n ? f[base + j] : 0u;
-      s += fl[j];
-    }
-    const uint32_t incl = wave_incl_scan(s);
-    if (lane_id() == 63) ws[w] = incl;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int i = 0; i < kScanThreads / kWave; ++i) {
-      if (i < w) off += ws[i];
-      tot += ws[i];
-    }
-    uint32_t o = carry + off + incl - s;
-#pragma unroll
-    for (int j = 0; j < kScanItems; ++j) {
-      if (fl[j]) {
-        const uint32_t i = base + j;
-        if (t == 0) {
-          a.d_pl_pos[o] = a.q_pl[i];
-          a.d_pl_nrm[o] = a.q_pl_nrm[i];
-        } else {
-          a.d_pt_pos[o] = a.q_pt[i];
-        }
-        ++o;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    host_store(a.host_tot + t, carry);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // complete before the ticket
-    const bool last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
-    if (last) {
-      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      publish_flag(a.flag, a.seq);
-    }
+__global__ __launch_bounds__(kQPB) void k_insert(InsArgs a) {
+  const uint32_t b = blockIdx.x;
+  const bool planar = b < a.nb_pl;
+  const uint32_t qi = (planar ? b : b - a.nb_pl) * kQPB + threadIdx.x;
+  const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
+  const bool f = qi < nq && a.ins[planar ? qi : a.nq_pl + qi] != 0;
+  const uint64_t m = __ballot(f);
+  if (!f) return;
+  const uint32_t o = a.ins_off[b] + (uint32_t)__popcll(m & lanemask_lt());
+  if (planar) {
+    a.d_pl_pos[o] = a.q_pl[qi];
+    a.d_pl_nrm[o] = a.q_pl_nrm[qi];
+  } else {
+    a.d_pt_pos[o] = a.q_pt[qi];
   }
 }
 
@@ -741,6 +735,9 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->work_blocks = nb;
   ensure_zeroed(c->mcnt, 2 * (size_t)K, st);
   ensure_zeroed(c->mticket, 1, st);
+  c->ins_blk.ensure(nb + 1);
+  c->ins_off.ensure(nb + 1);
+  c->h_counts.ensure(2 * (size_t)K + 4);
   auto view = [&](int t) {
     VoxMap& M = c->map[t];
     return MapView{reinterpret_cast<const Slot*>(M.table.p), M.cap ? M.cap - 1 : 0, M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
@@ -754,11 +751,15 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
     hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
                        c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
-                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, icp, c->mcnt.p, c->mticket.p, c->h_counts.d);
+                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, icp, c->mcnt.p, c->mticket.p, c->h_counts.d,
+                       c->ins_blk.p, c->ins_off.p);
     FMX_HIP(hipGetLastError());
   }
-  if (!sorted) {  // counts come from the match kernel's last block (none without queries)
-    if (nb == 0 && c->K > 0) FMX_HIP(hipMemsetAsync(c->h_counts.d, 0, 2 * c->K * sizeof(uint32_t), st));
+  // no queries: no launch, so zero the counts and insert totals the kernel would write
+  if (nb == 0) FMX_HIP(hipMemsetAsync(c->h_counts.d, 0, (2 * (size_t)c->K + 2) * sizeof(uint32_t), st));
+  c->match_nb_pl = a.nb_pl;
+  c->match_nb = nb;
+  if (!sorted) {  // counts come from the match kernel's last block
     c->n_qo = nq;
   } else {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
@@ -796,6 +797,8 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
   const int K = std::max<int>((int)c->K, 1);
   c->cnt_pl.assign(c->h_counts.p, c->h_counts.p + c->K);
   c->cnt_pt.assign(c->h_counts.p + c->K, c->h_counts.p + 2 * c->K);
+  c->ins_tot[0] = c->h_counts.p[2 * c->K];
+  c->ins_tot[1] = c->h_counts.p[2 * c->K + 1];
   c->rows_pl = c->rows_pt = 0;
   for (uint32_t k = 0; k < c->K; ++k) {
     c->rows_pl += c->cnt_pl[k];
@@ -815,36 +818,33 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
 }
 
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
+  if (!c->have_match) throw StatusError(FMX_E_STATE, "no match to insert from");
   hipStream_t st = c->stream;
-  uint32_t tot[2] = {0, 0};
-  c->h_u32.ensure(8);
-  for (int t = 0; t < 2; ++t) {  // worst case every query inserted
+  match_counts_fetch(c);  // insert totals of the last match (no wait if already fetched)
+  const uint32_t tot[2] = {c->ins_tot[0], c->ins_tot[1]};
+  for (int t = 0; t < 2; ++t) {
     const uint32_t nq = t == 0 ? c->n_qpl : c->n_qpt;
-    if (c->pool[t].used + nq > c->pool[t].pos.cap) throw StatusError(FMX_E_OOM, "keypoint pool capacity exceeded");
+    if (tot[t] > nq) throw StatusError(FMX_E_HIP, "implausible insert total");
+    if (c->pool[t].used + tot[t] > c->pool[t].pos.cap) throw StatusError(FMX_E_OOM, "keypoint pool capacity exceeded");
   }
-  ensure_zeroed(c->iticket, 1, st);
   InsArgs ia;
   ia.nq_pl = c->n_qpl;
   ia.nq_pt = c->n_qpt;
+  ia.nb_pl = c->match_nb_pl;
   ia.ins = c->m_ins.p;
+  ia.ins_off = c->ins_off.p;
   ia.q_pl = c->q_pl_pos.p;
   ia.q_pl_nrm = c->q_pl_nrm.p;
   ia.q_pt = c->q_pt_pos.p;
   ia.d_pl_pos = c->pool[0].pos.p + c->pool[0].used;
   ia.d_pl_nrm = c->pool[0].nrm.p + c->pool[0].used;
   ia.d_pt_pos = c->pool[1].pos.p + c->pool[1].used;
-  ia.host_tot = c->h_u32.d + 4;
-  ia.ticket = c->iticket.p;
-  ia.seq = next_flag(c);
-  ia.flag = c->h_flag.d;
-  {
+  if (c->match_nb > 0) {
     ProfScope ps(c->prof, PROF_INSERT, 33.0 * c->n_qpl + 17.0 * c->n_qpt, st);
-    hipLaunchKernelGGL(k_insert, dim3(2), dim3(kScanThreads), 0, st, ia);
+    hipLaunchKernelGGL(k_insert, dim3(c->match_nb), dim3(kQPB), 0, st, ia);
     FMX_HIP(hipGetLastError());
   }
-  wait_flag(c, c->h_flag.p, ia.seq);
   for (int t = 0; t < 2; ++t) {
-    tot[t] = c->h_u32.p[4 + t];
     Pool& pool = c->pool[t];
     auto& rg = pool.ranges[scan];
     if (rg.second == 0) rg.first = pool.used;
