@@ -754,8 +754,8 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[1] = lm_it;
   c->stats[2] = mpl;
   c->stats[3] = mpt;
-  c->stats[4] = c->map[0].n;
-  c->stats[5] = c->map[1].n;
+  c->stats[4] = c->map.n[0];
+  c->stats[5] = c->map.n[1];
   c->stats[6] = lins;
   c->stats[7] = scans.size();
   if (out) *out = fc;
@@ -846,12 +846,14 @@ void fmx_destroy(fmx_ctx* c) {
   c->q_pl_pos.release(); c->q_pl_nrm.release(); c->q_pt_pos.release(); c->q_pl_idx.release(); c->q_pt_idx.release();
   for (int t = 0; t < 2; ++t) {
     c->pool[t].pos.release(); c->pool[t].nrm.release();
-    auto& M = c->map[t];
-    M.table.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
-    M.rseg.release(); M.pos.release(); M.nrm.release(); M.seg.release(); M.rid.release();
     c->segs[t].release(); c->h_segs[t].release();
   }
-  c->h_mapposes.release(); c->map_blob.release(); c->map_err.release();
+  {
+    auto& M = c->map;
+    M.table.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
+    M.rseg.release(); M.pos.release(); M.nrm.release(); M.seg.release(); M.rid.release();
+  }
+  c->h_mapposes.release(); c->map_blob.release();
   c->blk_lo.release(); c->blk_hi.release(); c->icp.release(); c->h_icp.release(); c->h_work.release();
   c->work.release(); c->pair_base.release();
   c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();
@@ -959,7 +961,7 @@ fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint3
     run_match(c, pose_j, max_dist, c->P.min_dist_map);
     match_counts_fetch(c);
     c->h_u32.ensure(8);
-    FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->map_err.p, 4, hipMemcpyDeviceToHost, c->stream));
+    FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->map_err_p, 4, hipMemcpyDeviceToHost, c->stream));
     FMX_HIP(hipStreamSynchronize(c->stream));
     if (c->h_u32.p[0]) throw StatusError(FMX_E_RANGE, "voxel coordinate outside the packed-key range");
     if (cpl) std::memcpy(cpl, c->cnt_pl.data(), c->K * sizeof(uint32_t));

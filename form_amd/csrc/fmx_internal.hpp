@@ -125,15 +125,18 @@ struct Pool {
 };
 
 // One built voxel map (VoxelMap<P>, map.hpp:66-94) in HBM.
+// Device voxel map of both feature types (one build): table = planar slots
+// [0, cap[0]), point slots [cap[0], cap[0] + cap[1]), then one slot holding the
+// range-error word; records (build order and voxel-sorted) planar [0, n[0]) then
+// point [n[0], n[0] + n[1]); normals for planar records only.
 struct VoxMap {
-  DBuf<uint4> table;      // fmx::Slot[cap]
-  uint64_t cap = 0;       // power of two
+  DBuf<uint4> table;            // fmx::Slot
+  uint64_t cap[2] = {0, 0};     // powers of two
+  uint32_t n[2] = {0, 0};
   DBuf<double4> tpos, tnrm;     // transformed records, build order
   DBuf<uint32_t> rslot, rseg;   // per build-order record
   DBuf<double4> pos, nrm;       // voxel-sorted
   DBuf<uint32_t> seg, rid;      // voxel-sorted segment (pair) and build-order id
-  uint32_t n = 0;
-  uint32_t voxels = 0;
 };
 
 struct Seg {
@@ -198,7 +201,7 @@ struct fmx_ctx {
 
   // ---- window keypoint store + maps
   fmx::Pool pool[2];
-  fmx::VoxMap map[2];
+  fmx::VoxMap map;  // both feature types
   std::vector<uint64_t> map_scans;  // pair k -> scan id
   fmx::DBuf<fmx::Seg> segs[2];
   fmx::HBuf<fmx::Seg> h_segs[2];
@@ -210,7 +213,7 @@ struct fmx_ctx {
   double cell_w = 0;    // internal cell width of the built map
   int cell_m = 1;       // subdivision: rings searched
   bool have_map = false;
-  fmx::DBuf<uint32_t> map_err;
+  uint32_t* map_err_p = nullptr;  // range-error word (in map.table)
 
   // ---- match results (query-indexed; planar then point)
   fmx::DBuf<int32_t> m_pair;

@@ -42,37 +42,56 @@ __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
   return lo;
 }
 
-__global__ __launch_bounds__(256) void k_map_insert(const float4* __restrict__ pool_pos,
-                                                    const float4* __restrict__ pool_nrm, int planar,
-                                                    const Seg* __restrict__ segs, int K,
-                                                    const double* __restrict__ poses, uint32_t nrec,
-                                                    double w, Slot* __restrict__ table, uint64_t mask,
-                                                    double4* __restrict__ tpos, double4* __restrict__ tnrm,
-                                                    uint32_t* __restrict__ rslot, uint32_t* __restrict__ rseg,
-                                                    uint32_t* __restrict__ err) {
+// Both feature types in one launch (the fused VoxMap layout, fmx_internal.hpp):
+// record rec < n0 is planar record rec, else point record rec - n0; each type has its
+// own table section (point slots at off1) and segment list.
+struct BuildArgs {
+  const float4* pool_pos[2];
+  const float4* pool_nrm;  // planar only
+  const Seg* segs[2];
+  int K;
+  const double* poses;
+  uint32_t n0, n;  // planar records, all records
+  double w;
+  Slot* table;
+  uint64_t mask[2];
+  uint64_t off1;  // first point slot
+  double4* tpos;
+  double4* tnrm;  // [n0]
+  uint32_t* rslot;
+  uint32_t* rseg;
+  uint32_t* err;
+};
+
+__global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
-  if (rec >= nrec) return;
-  const int s = find_seg(segs, K, rec);
+  if (rec >= a.n) return;
+  const int t = rec < a.n0 ? 0 : 1;
+  const uint32_t r = t == 0 ? rec : rec - a.n0;
+  const Seg* segs = a.segs[t];
+  const int s = find_seg(segs, a.K, r);
   const Seg sg = segs[s];
-  const double* T = poses + 12 * s;
-  const float4 lp = pool_pos[sg.pool_off + (rec - sg.off)];
+  const double* T = a.poses + 12 * s;
+  const float4 lp = a.pool_pos[t][sg.pool_off + (r - sg.off)];
   double wp[3];
   d_xform(T, (double)lp.x, (double)lp.y, (double)lp.z, wp);  // PlanarFeat::transform (features.hpp:137-140)
-  tpos[rec] = make_double4(wp[0], wp[1], wp[2], 0.0);
-  if (planar) {
-    const float4 ln = pool_nrm[sg.pool_off + (rec - sg.off)];
+  a.tpos[rec] = make_double4(wp[0], wp[1], wp[2], 0.0);
+  if (t == 0) {
+    const float4 ln = a.pool_nrm[sg.pool_off + (r - sg.off)];
     double wn[3];
     d_rot(T, (double)ln.x, (double)ln.y, (double)ln.z, wn);
-    tnrm[rec] = make_double4(wn[0], wn[1], wn[2], 0.0);
+    a.tnrm[rec] = make_double4(wn[0], wn[1], wn[2], 0.0);
   }
-  rseg[rec] = (uint32_t)s;
-  const int cx = (int)floor(wp[0] / w), cy = (int)floor(wp[1] / w), cz = (int)floor(wp[2] / w);
+  a.rseg[rec] = (uint32_t)s;
+  const int cx = (int)floor(wp[0] / a.w), cy = (int)floor(wp[1] / a.w), cz = (int)floor(wp[2] / a.w);
   if (!key_in_range(cx, cy, cz)) {
-    atomicOr(err, 1u);
-    rslot[rec] = 0xFFFFFFFFu;
+    atomicOr(a.err, 1u);
+    a.rslot[rec] = 0xFFFFFFFFu;
     return;
   }
   const unsigned long long key = pack_key(cx, cy, cz);
+  Slot* table = a.table + (t == 0 ? 0 : a.off1);
+  const uint64_t mask = a.mask[t];
   uint64_t h = mix64(key) & mask;
   for (;;) {
     const unsigned long long prev = atomicCAS(&table[h].key, 0ull, key);
@@ -80,7 +99,7 @@ __global__ __launch_bounds__(256) void k_map_insert(const float4* __restrict__ p
     h = (h + 1) & mask;
   }
   atomicAdd(&table[h].count, 1u);
-  rslot[rec] = (uint32_t)h;
+  a.rslot[rec] = (uint32_t)((t == 0 ? 0 : a.off1) + h);
 }
 
 struct CountIn {
@@ -93,12 +112,12 @@ struct FirstOut {
 };
 
 // After the scatter each slot's `first` has advanced by `count`: records of a voxel
-// are [first - count, first).
-__global__ __launch_bounds__(256) void k_map_scatter(uint32_t nrec, const uint32_t* __restrict__ rslot,
+// are [first - count, first).  Planar slots precede point slots in the scan, so
+// planar records land in [0, n0) and nrm is written for them only.
+__global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec, const uint32_t* __restrict__ rslot,
                                                      const uint32_t* __restrict__ rseg,
                                                      const double4* __restrict__ tpos,
-                                                     const double4* __restrict__ tnrm, int planar,
-                                                     Slot* __restrict__ table,
+                                                     const double4* __restrict__ tnrm, Slot* __restrict__ table,
                                                      double4* __restrict__ pos, double4* __restrict__ nrm,
                                                      uint32_t* __restrict__ seg, uint32_t* __restrict__ rid) {
   const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
@@ -107,7 +126,7 @@ __global__ __launch_bounds__(256) void k_map_scatter(uint32_t nrec, const uint32
   if (s == 0xFFFFFFFFu) return;
   const uint32_t o = atomicAdd(&table[s].first, 1u);
   pos[o] = tpos[rec];
-  if (planar) nrm[o] = tnrm[rec];
+  if (rec < n0) nrm[o] = tnrm[rec];
   seg[o] = rseg[rec];
   rid[o] = rec;
 }
@@ -643,44 +662,59 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   c->map_poses_p = c->map_blob.p;
   c->map_inv_p = c->map_blob.p + 12 * (size_t)Kc;
   const Seg* dseg = reinterpret_cast<const Seg*>(c->map_blob.p + 24 * (size_t)Kc);
-  c->map_err.ensure(1);
+  // fused build of both types: one table allocation (planar slots, point slots, then
+  // the range-error word in one extra slot), one record numbering, one launch each
+  // for zeroing, insert, count scan and scatter
+  VoxMap& M = c->map;
+  const uint32_t n = nrec[0] + nrec[1];
   for (int t = 0; t < 2; ++t) {
-    Pool& pool = c->pool[t];
-    VoxMap& M = c->map[t];
-    const uint32_t n = nrec[t];
-    M.n = n;
-    const uint64_t use = next_pow2(std::max<uint64_t>(2ull * n, 1024));  // load factor <= 0.5
-    M.table.ensure(use);
-    M.cap = use;
-    // zero the table (and, for t == 0, the range-error flag that follows the fill)
-    FMX_HIP(hipMemsetAsync(M.table.p, 0, use * sizeof(Slot), st));
-    if (t == 0) FMX_HIP(hipMemsetAsync(c->map_err.p, 0, 4, st));
-    M.tpos.ensure(n + 1);
-    M.rslot.ensure(n + 1);
-    M.rseg.ensure(n + 1);
-    M.pos.ensure(n + 1);
-    M.seg.ensure(n + 1);
-    M.rid.ensure(n + 1);
-    if (t == 0) {
-      M.tnrm.ensure(n + 1);
-      M.nrm.ensure(n + 1);
-    }
-    const double bytes = (t == 0 ? 2.0 * 32.0 : 2.0 * 16.0) * n + 16.0 * (double)use;
-    ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
-    if (n > 0) {
-      hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, pool.pos.p, pool.nrm.p, t == 0 ? 1 : 0,
-                         dseg + t * Kc, K, c->map_poses_p, n, c->cell_w, reinterpret_cast<Slot*>(M.table.p), use - 1,
-                         M.tpos.p, M.tnrm.p, M.rslot.p, M.rseg.p, c->map_err.p);
-      FMX_HIP(hipGetLastError());
-      c->scan_scratch.ensure(scan_scratch_size(use) + 4);
-      c->dev_u32.ensure(8);
-      exclusive_scan(CountIn{reinterpret_cast<const Slot*>(M.table.p)}, FirstOut{reinterpret_cast<Slot*>(M.table.p)},
-                     use, c->scan_scratch.p, c->dev_u32.p + 4, st);
-      hipLaunchKernelGGL(k_map_scatter, dim3((n + 255) / 256), dim3(256), 0, st, n, M.rslot.p, M.rseg.p, M.tpos.p,
-                         M.tnrm.p, t == 0 ? 1 : 0, reinterpret_cast<Slot*>(M.table.p), M.pos.p, M.nrm.p, M.seg.p,
-                         M.rid.p);
-      FMX_HIP(hipGetLastError());
-    }
+    M.n[t] = nrec[t];
+    M.cap[t] = next_pow2(std::max<uint64_t>(2ull * nrec[t], 1024));  // load factor <= 0.5
+  }
+  const uint64_t slots = M.cap[0] + M.cap[1];
+  M.table.ensure(slots + 1);
+  c->map_err_p = reinterpret_cast<uint32_t*>(M.table.p + slots);
+  FMX_HIP(hipMemsetAsync(M.table.p, 0, (slots + 1) * sizeof(Slot), st));
+  M.tpos.ensure(n + 1);
+  M.tnrm.ensure(nrec[0] + 1);
+  M.rslot.ensure(n + 1);
+  M.rseg.ensure(n + 1);
+  M.pos.ensure(n + 1);
+  M.nrm.ensure(nrec[0] + 1);
+  M.seg.ensure(n + 1);
+  M.rid.ensure(n + 1);
+  const double bytes = 2.0 * 32.0 * nrec[0] + 2.0 * 16.0 * nrec[1] + 16.0 * (double)slots;
+  ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
+  if (n > 0) {
+    BuildArgs ba;
+    ba.pool_pos[0] = c->pool[0].pos.p;
+    ba.pool_pos[1] = c->pool[1].pos.p;
+    ba.pool_nrm = c->pool[0].nrm.p;
+    ba.segs[0] = dseg;
+    ba.segs[1] = dseg + Kc;
+    ba.K = K;
+    ba.poses = c->map_poses_p;
+    ba.n0 = nrec[0];
+    ba.n = n;
+    ba.w = c->cell_w;
+    ba.table = reinterpret_cast<Slot*>(M.table.p);
+    ba.mask[0] = M.cap[0] - 1;
+    ba.mask[1] = M.cap[1] - 1;
+    ba.off1 = M.cap[0];
+    ba.tpos = M.tpos.p;
+    ba.tnrm = M.tnrm.p;
+    ba.rslot = M.rslot.p;
+    ba.rseg = M.rseg.p;
+    ba.err = c->map_err_p;
+    hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, ba);
+    FMX_HIP(hipGetLastError());
+    c->scan_scratch.ensure(scan_scratch_size(slots) + 4);
+    c->dev_u32.ensure(8);
+    exclusive_scan(CountIn{reinterpret_cast<const Slot*>(M.table.p)}, FirstOut{reinterpret_cast<Slot*>(M.table.p)},
+                   slots, c->scan_scratch.p, c->dev_u32.p + 4, st);
+    hipLaunchKernelGGL(k_map_scatter, dim3((n + 255) / 256), dim3(256), 0, st, nrec[0], n, M.rslot.p, M.rseg.p,
+                       M.tpos.p, M.tnrm.p, reinterpret_cast<Slot*>(M.table.p), M.pos.p, M.nrm.p, M.seg.p, M.rid.p);
+    FMX_HIP(hipGetLastError());
   }
   c->have_map = true;
   c->have_match = false;
@@ -738,9 +772,10 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->ins_blk.ensure(nb + 1);
   c->ins_off.ensure(nb + 1);
   c->h_counts.ensure(2 * (size_t)K + 4);
-  auto view = [&](int t) {
-    VoxMap& M = c->map[t];
-    return MapView{reinterpret_cast<const Slot*>(M.table.p), M.cap ? M.cap - 1 : 0, M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
+  auto view = [&](int t) {  // type t's table section over the shared record arrays
+    VoxMap& M = c->map;
+    return MapView{reinterpret_cast<const Slot*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
+                   M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
   };
   // Algorithmic bytes of a match launch: query read (16 B) +
   // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + 16 B per hash probe +
