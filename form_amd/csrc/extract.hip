@@ -26,6 +26,7 @@
 #include "fmx_internal.hpp"
 
 #include <cfloat>
+#include <cstdlib>
 
 namespace fmx {
 namespace {
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(256) void k_closest(const float4* __restrict__ scan
 
 // Cyclic Jacobi on the symmetric 3x3 covariance in double; returns the unit
 // eigenvector of the smallest eigenvalue (Eigen::SelfAdjointEigenSolver col(0)).
-__device__ void smallest_eigvec(const float cov[3][3], double n[3]) {
+__device__ __forceinline__ void smallest_eigvec(const float cov[3][3], double n[3]) {
   double A[3][3], V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) A[i][j] = (double)cov[i][j];
@@ -530,9 +531,13 @@ __device__ void smallest_eigvec(const float cov[3][3], double n[3]) {
       }
     }
   }
-  int mi = 0;
-  if (A[1][1] < A[mi][mi]) mi = 1;
-  if (A[2][2] < A[mi][mi]) mi = 2;
+  int mi = 0;  // first smallest diagonal entry (no dynamic indexing: no scratch)
+  double dm = A[0][0];
+  if (A[1][1] < dm) {
+    mi = 1;
+    dm = A[1][1];
+  }
+  if (A[2][2] < dm) mi = 2;
   double v0 = mi == 0 ? V[0][0] : (mi == 1 ? V[0][1] : V[0][2]);
   double v1 = mi == 0 ? V[1][0] : (mi == 1 ? V[1][1] : V[1][2]);
   double v2 = mi == 0 ? V[2][0] : (mi == 1 ? V[2][1] : V[2][2]);
@@ -560,7 +565,7 @@ __global__ __launch_bounds__(256) void k_fit(const float4* __restrict__ scan,
   const bool active = (uint32_t)slot < row_counts[2 * r];
   const int found = active ? fit_one(scan, sel_slots, closest, a, nrm_slots, r, slot) : 0;
   const int nfound = __syncthreads_count(found);
-  if (threadIdx.x == 0 && nfound) atomicAdd(&row_ok[r], (uint32_t)nfound);
+  if (threadIdx.x == 0 && nfound) atomicAdd(&row_ok[2 * r], (uint32_t)nfound);  // pair [2r, 2r+1], see k_row_scan
 }
 
 __device__ int fit_one(const float4* __restrict__ scan, const uint32_t* __restrict__ sel_slots,
@@ -624,6 +629,293 @@ __device__ int fit_one(const float4* __restrict__ scan, const uint32_t* __restri
   return out.w != 0.f ? 1 : 0;
 }
 
+// find_closest + compute_normal for one scan line in one workgroup (C <= 2048):
+// rows r-1, r, r+1 (float4) and the planar masks of r+-1 are staged in LDS, so the
+// argmin scans and the neighbour walks read LDS instead of chains of dependent
+// global loads.  Same semantics as k_closest + k_fit (which serve wider rows):
+//   closest: one wave per selected point, own 64-column block first, then every
+//            block whose AABB lower bound (shrunk 1e-5) does not exceed the best;
+//   fit:     one lane per selected point, the reference's neighbour push order.
+// The row's found-normal count is stored directly (one block per row).
+constexpr int kNrmThreads = 1024;
+constexpr int kNrmMaxC = 2048;
+
+template <int KC>
+__global__ __launch_bounds__(kNrmThreads) void k_normals(const float4* __restrict__ scan,
+                                                         const uint8_t* __restrict__ mask,
+                                                         const uint32_t* __restrict__ sel_slots,
+                                                         const uint32_t* __restrict__ row_counts, ExArgs a,
+                                                         float4* __restrict__ nrm_slots,
+                                                         uint32_t* __restrict__ row_ok) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int C = a.C, R = a.R, r = blockIdx.x, k = KC > 0 ? KC : a.k;
+  const int half = blockIdx.y;  // two workgroups per line split its selected points
+  const int nblk = (C + kWave - 1) / kWave;
+  // rows r-1, r, r+1; in rows r+-1 the pad component .w holds the planar mask (1/0).
+  // One float4 of padding per 64 columns (px): column jj of different 64-column
+  // blocks then falls in different LDS banks (blocks would otherwise be 1 KB apart).
+  const int CP = C + (C >> 6) + 1;
+  auto px = [](int j) { return j + (j >> 6); };
+  float4* s_row = reinterpret_cast<float4*>(smem);          // [3][CP]
+  float4* s_lo = s_row + 3 * CP;                            // [2][nblk]
+  float4* s_hi = s_lo + 2 * nblk;                           // [2][nblk]
+  int2* s_cl = reinterpret_cast<int2*>(s_hi + 2 * nblk);    // [cap_pl] closest columns in r-1 / r+1
+  unsigned long long* s_best = reinterpret_cast<unsigned long long*>(s_cl + a.cap_pl);  // [cap_pl]
+  uint32_t* s_items = reinterpret_cast<uint32_t*>(s_best + a.cap_pl);                   // [cap_pl * nblk]
+  int* s_col = reinterpret_cast<int*>(s_items + (size_t)a.cap_pl * nblk);              // [cap_pl] selected columns
+  const int tid = threadIdx.x;
+  __shared__ int s_found;
+  __shared__ int s_nitems;
+  if (tid == 0) s_found = 0;
+#ifdef FMX_NRM_TIMING
+  uint64_t ts[5], tp[12];
+  int ntp = 0;
+  ts[0] = wall_clock64();
+#endif
+  for (int s = 0; s < 3; ++s) {
+    const int rr = r - 1 + s;
+    if (rr < 0 || rr >= R) continue;
+    const float4* src = scan + (size_t)rr * C;
+    const uint8_t* msk = mask + (size_t)rr * C;
+    for (int c = tid; c < C; c += kNrmThreads) {
+      float4 q = src[c];
+      if (s != 1) q.w = msk[c] ? 1.f : 0.f;
+      s_row[s * CP + px(c)] = q;
+    }
+  }
+  __syncthreads();
+#ifdef FMX_NRM_TIMING
+  ts[1] = wall_clock64();
+#endif
+  // AABBs of the planar-valid points per 64-column block of rows r-1 / r+1: 16
+  // threads per block, 4 columns each, then a 16-lane min/max (empty: lo = +inf,
+  // hi = -inf); the selected columns of row r go to LDS meanwhile
+  const int nsel_all = (int)row_counts[2 * r];
+  const int hs = (nsel_all + 1) / 2;
+  const int s_beg = half * hs, nsel = min(nsel_all, s_beg + hs);  // this block: slots [s_beg, nsel)
+  for (int s = s_beg + tid; s < nsel; s += kNrmThreads) s_col[s] = (int)sel_slots[(size_t)r * a.cap_pl + s];
+  for (int t0 = 0; t0 < 2 * nblk * 16; t0 += kNrmThreads) {
+    const int t = t0 + tid;
+    const int wb = t / 16, part = t % 16;
+    float lx = INFINITY, ly = INFINITY, lz = INFINITY, hx = -INFINITY, hy = -INFINITY, hz = -INFINITY;
+    if (wb < 2 * nblk) {
+      const int d = wb / nblk, bk = wb % nblk;
+      const int rr = d == 0 ? r - 1 : r + 1;
+      if (rr >= 0 && rr < R) {
+        const float4* row = s_row + (d == 0 ? 0 : 2) * CP;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int jcol = bk * kWave + part * 4 + u;
+          if (jcol < C) {
+            const float4 q = row[px(jcol)];
+            if (q.w != 0.f) {
+              lx = fminf(lx, q.x);
+              ly = fminf(ly, q.y);
+              lz = fminf(lz, q.z);
+              hx = fmaxf(hx, q.x);
+              hy = fmaxf(hy, q.y);
+              hz = fmaxf(hz, q.z);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      lx = fminf(lx, __shfl_xor(lx, o, 16));
+      ly = fminf(ly, __shfl_xor(ly, o, 16));
+      lz = fminf(lz, __shfl_xor(lz, o, 16));
+      hx = fmaxf(hx, __shfl_xor(hx, o, 16));
+      hy = fmaxf(hy, __shfl_xor(hy, o, 16));
+      hz = fmaxf(hz, __shfl_xor(hz, o, 16));
+    }
+    if (wb < 2 * nblk && part == 0) {
+      s_lo[wb] = make_float4(lx, ly, lz, 0.f);
+      s_hi[wb] = make_float4(hx, hy, hz, 0.f);
+    }
+  }
+  __syncthreads();
+#ifdef FMX_NRM_TIMING
+  ts[2] = wall_clock64();
+#endif
+  // find_closest (:402-420) over rows r-1 / r+1, the whole workgroup per row: the
+  // argmin over a candidate's points is an LDS atomicMin of the key (fp32 distance
+  // bits << 32 | column) — distances are >= 0, so the key orders like the reference
+  // (smaller distance, then first index).  Phase 1: the candidate's own 64-column
+  // block; phase 2: list every other block whose AABB lower bound (shrunk 1e-5) does
+  // not exceed that best (conservative: the final best can only be smaller); phase
+  // 3: the listed blocks.  Exact, with three barriers per row instead of a serial
+  // chain per candidate.
+#pragma unroll 1
+  for (int d = 0; d < 2; ++d) {
+    const int rr = d == 0 ? r - 1 : r + 1;
+    const bool have = rr >= 0 && rr < R;
+    const float4* row = s_row + (d == 0 ? 0 : 2) * CP;
+    for (int s = s_beg + tid; s < nsel; s += kNrmThreads) s_best[s] = ~0ull;
+    if (tid == 0) s_nitems = 0;
+    __syncthreads();
+#ifdef FMX_NRM_TIMING
+    tp[ntp < 12 ? ntp++ : 11] = wall_clock64();
+#endif
+    // key of column j for query p (~0 when not a candidate); one thread folds its
+    // columns in a register and issues a single atomicMin per candidate
+    auto key = [&](const float4& p, int j) -> unsigned long long {
+      const float4 q = row[px(j)];
+      const float dd = dist2f(q, p);
+      if (q.w == 0.f || !(dd <= FLT_MAX)) return ~0ull;  // reference: double(d) < DBL_MAX
+      return ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)j;
+    };
+    // work items are laid out candidate-fastest so the lanes of a wave update
+    // different candidates' keys (no same-address LDS atomics within a wave)
+    // threads = 256 candidate lanes x 4 column groups (no runtime divisions)
+    const int tl = tid & 255, tg = tid >> 8;
+    if (have) {
+      for (int s = s_beg + tl; s < nsel; s += 256) {
+        const int c = s_col[s];
+        const float4 p = s_row[CP + px(c)];
+        const int j0 = (c / kWave) * kWave;
+        unsigned long long kb = ~0ull;
+#pragma unroll 4
+        for (int jj = tg; jj < kWave; jj += 4)
+          if (j0 + jj < C) kb = min(kb, key(p, j0 + jj));
+        if (kb != ~0ull) atomicMin(&s_best[s], kb);
+      }
+    }
+    __syncthreads();
+#ifdef FMX_NRM_TIMING
+    tp[ntp < 12 ? ntp++ : 11] = wall_clock64();
+#endif
+    if (have) {
+      const int nsr = (nsel - s_beg + 255) & ~255;  // whole 256-lane rounds: ballots see full waves
+      for (int sb = 0; sb < nsr * ((nblk + 3) / 4); sb += 256) {
+        const int s = s_beg + (sb % nsr) + tl, bk = (sb / nsr) * 4 + tg;
+        bool keep = false;
+        if (s < nsel && bk < nblk) {
+          const int c = s_col[s];
+          const float4 lo = s_lo[d * nblk + bk], hi = s_hi[d * nblk + bk];
+          if (bk != c / kWave && lo.x <= hi.x) {  // not the own block, not empty
+            // fp32 bound: pruning only has to be conservative, and the 1e-5 shrink
+            // dwarfs the few-ulp fp32 error of the bound and of the distances
+            const float4 p = s_row[CP + px(c)];
+            const float ex = fmaxf(fmaxf(lo.x - p.x, p.x - hi.x), 0.f);
+            const float ey = fmaxf(fmaxf(lo.y - p.y, p.y - hi.y), 0.f);
+            const float ez = fmaxf(fmaxf(lo.z - p.z, p.z - hi.z), 0.f);
+            const float lb = (ex * ex + ey * ey + ez * ez) * (1.f - 1e-5f);
+            const unsigned long long b = s_best[s];
+            keep = b == ~0ull || lb <= __uint_as_float((uint32_t)(b >> 32));
+          }
+        }
+        const uint64_t m = __ballot(keep);  // one counter add per wave
+        int base = 0;
+        if (lane_id() == 0 && m) base = atomicAdd(&s_nitems, __popcll(m));
+        base = __shfl(base, 0, 64);
+        if (keep) s_items[base + __popcll(m & lanemask_lt())] = (uint32_t)(s * 64 + bk);  // nblk <= 32
+      }
+    }
+    __syncthreads();
+#ifdef FMX_NRM_TIMING
+    tp[ntp < 12 ? ntp++ : 11] = wall_clock64();
+#endif
+    const int nitems = s_nitems;
+
+    for (int q = tl; q < nitems; q += 256) {
+      const uint32_t it = s_items[q];
+      const int s = (int)(it >> 6), bk = (int)(it & 63);
+      const float4 p = s_row[CP + px(s_col[s])];
+      unsigned long long kb = ~0ull;
+#pragma unroll 4
+      for (int jj = tg; jj < kWave; jj += 4)
+        if (bk * kWave + jj < C) kb = min(kb, key(p, bk * kWave + jj));
+      if (kb != ~0ull) atomicMin(&s_best[s], kb);
+    }
+    __syncthreads();
+#ifdef FMX_NRM_TIMING
+    tp[ntp < 12 ? ntp++ : 11] = wall_clock64();
+#endif
+    for (int s = s_beg + tid; s < nsel; s += kNrmThreads) {
+      const unsigned long long b = s_best[s];
+      const int col = b == ~0ull ? -1 : (int)(uint32_t)b;
+      if (d == 0) s_cl[s].x = col;
+      else s_cl[s].y = col;
+    }
+  }
+  __syncthreads();
+#ifdef FMX_NRM_TIMING
+  ts[3] = wall_clock64();
+#endif
+  // compute_normal (:263-329), one lane per selected point; points addressed as
+  // (LDS row 0/1/2, column): every walk stays inside its row (valid columns lie in
+  // [k, C-k) and the walk is at most k long)
+  int found = 0;
+  for (int slot = s_beg + tid; slot < nsel; slot += kNrmThreads) {
+    const int c = s_col[slot];
+    const float4 p = s_row[CP + px(c)];
+    const int2 cl = s_cl[slot];
+    const double r2 = a.radius2;
+    auto walk = [&](auto&& visit) {
+      auto nbrs = [&](const float4* row, int j) {  // find_neighbors (:422-448)
+        const float4 pj = row[px(j)];
+        for (int i = 1; i <= k; ++i) {
+          const float4 q = row[px(j + i)];
+          if ((double)dist2f(q, pj) < r2) visit(q);
+          else break;
+        }
+        for (int i = 1; i <= k; ++i) {
+          const float4 q = row[px(j - i)];
+          if ((double)dist2f(q, pj) < r2) visit(q);
+          else break;
+        }
+      };
+      nbrs(s_row + CP, c);
+      if (cl.x >= 0) {
+        visit(s_row[px(cl.x)]);
+        nbrs(s_row, cl.x);
+      }
+      if (cl.y >= 0) {
+        visit(s_row[2 * CP + px(cl.y)]);
+        nbrs(s_row + 2 * CP, cl.y);
+      }
+    };
+    int cnt = 0;
+    walk([&](float4) { ++cnt; });
+    float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((cl.x >= 0 || cl.y >= 0) && cnt >= a.min_points) {
+      const float nf = (float)cnt;
+      float cov[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+      walk([&](float4 q) {
+        const float ax = (q.x - p.x) / nf, ay = (q.y - p.y) / nf, az = (q.z - p.z) / nf;
+        const float av[3] = {ax, ay, az};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) cov[i][jj] = cov[i][jj] + av[i] * av[jj];
+      });
+      double n[3];
+      smallest_eigvec(cov, n);
+      const double dp = (n[0] * (double)p.x + n[1] * (double)p.y) + n[2] * (double)p.z;
+      if (dp > 0) {
+        n[0] = -n[0];
+        n[1] = -n[1];
+        n[2] = -n[2];
+      }
+      out = make_float4((float)n[0], (float)n[1], (float)n[2], 1.0f);  // w = 1: normal found
+      ++found;
+    }
+    nrm_slots[(size_t)r * a.cap_pl + slot] = out;
+  }
+  if (found) atomicAdd(&s_found, found);
+  __syncthreads();
+  if (tid == 0) row_ok[2 * r + half] = (uint32_t)s_found;  // k_row_scan adds the pair
+#ifdef FMX_NRM_TIMING
+  ts[4] = wall_clock64();
+  if (tid == 0 && half == 0 && (r == 5 || r == 64 || r == 100))
+    printf("nrm row %d nsel %d: load %d aabb %d closest %d fit %d | %d %d %d %d %d %d %d %d\n", r, nsel,
+           (int)(ts[1] - ts[0]), (int)(ts[2] - ts[1]), (int)(ts[3] - ts[2]), (int)(ts[4] - ts[3]), (int)(tp[0] - ts[2]),
+           (int)(tp[1] - tp[0]), (int)(tp[2] - tp[1]), (int)(tp[3] - tp[2]), (int)(tp[4] - tp[3]), (int)(tp[5] - tp[4]),
+           (int)(tp[6] - tp[5]), (int)(tp[7] - tp[6]));
+#endif
+}
+
 // per-row offsets of {planar with normal, points, planar selected}: one block
 __global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, const uint32_t* row_ok, int R,
                                                    uint32_t* row_off /* [3][R+1] */, uint32_t* host_totals,
@@ -636,7 +928,7 @@ __global__ __launch_bounds__(1024) void k_row_scan(const uint32_t* row_counts, c
     const int r = r0 + threadIdx.x;
     for (int t = 0; t < 3; ++t) {
       uint32_t v = 0;
-      if (r < R) v = t == 0 ? row_ok[r] : (t == 1 ? row_counts[2 * r + 1] : row_counts[2 * r]);
+      if (r < R) v = t == 0 ? row_ok[2 * r] + row_ok[2 * r + 1] : (t == 1 ? row_counts[2 * r + 1] : row_counts[2 * r]);
       const uint32_t incl = wave_incl_scan(v);
       const int w = threadIdx.x / kWave;
       if (lane_id() == 63) ws[w] = incl;
@@ -730,7 +1022,7 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   c->sel_slots.ensure((size_t)R * a.cap_pl);
   c->pt_slots.ensure((size_t)R * a.cap_pt);
   c->row_counts.ensure(2 * (size_t)R);
-  c->row_ok.ensure(R);
+  c->row_ok.ensure(2 * (size_t)R);  // found normals per line: [2r] + [2r+1]
   c->row_off.ensure(3 * ((size_t)R + 1));
   c->closest.ensure((size_t)R * a.cap_pl);
   c->nrm_slots.ensure((size_t)R * a.cap_pl);
@@ -755,22 +1047,46 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
                          c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
   }
   FMX_HIP(hipGetLastError());
-  FMX_HIP(hipMemsetAsync(c->row_ok.p, 0, R * sizeof(uint32_t), st));
   const int nslots = R * a.cap_pl;
   const int nblk = (C + 63) / 64;
-  c->blk_lo.ensure((size_t)R * nblk);
-  c->blk_hi.ensure((size_t)R * nblk);
-  {
-    ProfScope ps(c->prof, PROF_CLOSEST, 16.0 * N + N + 8.0 * nslots, st);
-    hipLaunchKernelGGL(k_row_blocks, dim3((R * nblk + 3) / 4), dim3(256), 0, st, d_scan, c->planar_mask.p, R, C,
-                       c->blk_lo.p, c->blk_hi.p);
-    hipLaunchKernelGGL(k_closest, dim3((nslots + 3) / 4), dim3(256), 0, st, d_scan, c->planar_mask.p,
-                       c->sel_slots.p, c->row_counts.p, R, C, a.cap_pl, c->blk_lo.p, c->blk_hi.p, c->closest.p);
-  }
-  {
-    ProfScope ps(c->prof, PROF_FIT, 0.0, st);
-    hipLaunchKernelGGL(k_fit, dim3((a.cap_pl + 255) / 256, R), dim3(256), 0, st, d_scan, c->sel_slots.p,
-                       c->row_counts.p, c->closest.p, a, c->nrm_slots.p, c->row_ok.p);
+  static const bool split_normals = std::getenv("FMX_SPLIT_NORMALS") != nullptr;  // A/B / test switch
+  // k_normals: one workgroup per line, rows r-1..r+1 in LDS (160 KB per CU, minus
+  // the kernel's few static bytes)
+  const size_t lds_n = (size_t)3 * (C + (C >> 6) + 1) * 16 + (size_t)4 * nblk * 16 + (size_t)a.cap_pl * 20 +
+                       (size_t)a.cap_pl * nblk * 4;
+  constexpr size_t kNrmLdsMax = 160 * 1024 - 256;
+  if (C <= kNrmMaxC && lds_n <= kNrmLdsMax && !split_normals) {
+    if (!c->nrm_attr_set) {
+      FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_normals<5>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNrmLdsMax));
+      FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_normals<0>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNrmLdsMax));
+      c->nrm_attr_set = true;
+    }
+    ProfScope ps(c->prof, PROF_FIT, 48.0 * N + 2.0 * N + 16.0 * nslots, st);
+    if (a.k == 5)
+      hipLaunchKernelGGL(k_normals<5>, dim3(R, 2), dim3(kNrmThreads), lds_n, st, d_scan, c->planar_mask.p, c->sel_slots.p,
+                         c->row_counts.p, a, c->nrm_slots.p, c->row_ok.p);
+    else
+      hipLaunchKernelGGL(k_normals<0>, dim3(R, 2), dim3(kNrmThreads), lds_n, st, d_scan, c->planar_mask.p, c->sel_slots.p,
+                         c->row_counts.p, a, c->nrm_slots.p, c->row_ok.p);
+    FMX_HIP(hipGetLastError());
+  } else {
+    FMX_HIP(hipMemsetAsync(c->row_ok.p, 0, 2 * R * sizeof(uint32_t), st));
+    c->blk_lo.ensure((size_t)R * nblk);
+    c->blk_hi.ensure((size_t)R * nblk);
+    {
+      ProfScope ps(c->prof, PROF_CLOSEST, 16.0 * N + N + 8.0 * nslots, st);
+      hipLaunchKernelGGL(k_row_blocks, dim3((R * nblk + 3) / 4), dim3(256), 0, st, d_scan, c->planar_mask.p, R, C,
+                         c->blk_lo.p, c->blk_hi.p);
+      hipLaunchKernelGGL(k_closest, dim3((nslots + 3) / 4), dim3(256), 0, st, d_scan, c->planar_mask.p,
+                         c->sel_slots.p, c->row_counts.p, R, C, a.cap_pl, c->blk_lo.p, c->blk_hi.p, c->closest.p);
+    }
+    {
+      ProfScope ps(c->prof, PROF_FIT, 0.0, st);
+      hipLaunchKernelGGL(k_fit, dim3((a.cap_pl + 255) / 256, R), dim3(256), 0, st, d_scan, c->sel_slots.p,
+                         c->row_counts.p, c->closest.p, a, c->nrm_slots.p, c->row_ok.p);
+    }
   }
   uint32_t seq = 0;
   {

@@ -243,6 +243,7 @@ struct fmx_ctx {
   uint32_t work_blocks = 0;
   double last_probes = 0, last_cands = 0;
   bool counts_pending = false;
+  bool nrm_attr_set = false;
   bool lds_attr_set = false;
 
   // ---- linearize

@@ -37,6 +37,7 @@ GEOMETRIES = {
     "c4": ScanGeometry(128, 2048, 22.5, 0.01, 0.02),   # OS2-128
     "tiny": ScanGeometry(16, 256, 15.0, 0.01, 0.02),
     "small": ScanGeometry(32, 512, 16.6, 0.01, 0.02),
+    "wide": ScanGeometry(8, 4096, 15.0, 0.01, 0.02),  # > 2048 columns: the split normals path
 }
 
 

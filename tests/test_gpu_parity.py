@@ -17,11 +17,16 @@ def _ctx(fmx, p):
     return fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**p)))
 
 
-@pytest.mark.parametrize("config,k", [("tiny", 0), ("tiny", 5), ("small", 2), ("c2", 0), ("c3", 1), ("c4", 0)])
-def test_extract_matches_oracle(fmx_mod, oracle, config, k):
+@pytest.mark.parametrize("config,k,nbr", [("tiny", 0, 5), ("tiny", 5, 5), ("small", 2, 5), ("c2", 0, 5), ("c3", 1, 5),
+                                          ("c4", 0, 5), ("small", 3, 4), ("c2", 1, 3), ("wide", 0, 5),
+                                          ("wide", 2, 4)])
+def test_extract_matches_oracle(fmx_mod, oracle, config, k, nbr):
+    """nbr != 5 runs the runtime-neighbour-count kernels; "wide" (4096 columns) the
+    split find_closest / fit kernels instead of the LDS-staged k_normals."""
     import torch
     scan, T, geo = synth.make_scan(config, k)
     p = synth.default_params(geo)
+    p["neighbor_points"] = nbr
     ref = oracle.extract(scan.numpy(), p)
     ctx = _ctx(fmx_mod, p)
     ctx.extract(scan.to("cuda:0"), k)
