@@ -21,14 +21,17 @@ from collections import defaultdict
 
 # fmx kernel symbol fragment -> bench.py profile id
 KMAP = {
-    "k_match(": "match",
-    "k_extract_rows(": "extract_rows",
-    "k_closest(": "closest",
-    "k_fit(": "fit",
-    "k_linearize<1>": "linearize",
+    "k_match": "match",
+    "k_extract_rows": "extract_rows",
+    "k_normals": "fit",  # find_closest + compute_normal, fused (C <= 2048)
+    "k_closest": "closest",
+    "k_fit": "fit",
+    "k_linearize_total": "linearize",  # register_scan's fused linearization
+    "k_linearize<1>": "linearize_pairs",
     "k_linearize<0>": "linearize_full",
-    "k_map_insert(": "map_build_insert",
-    "k_map_scatter(": "map_build_scatter",
+    "k_map_insert": "map_build_insert",
+    "k_map_scatter": "map_build_scatter",
+    "k_insert": "insert",
 }
 
 

@@ -1,11 +1,17 @@
 """Summarise a rocprofv3 kernel_trace.csv: busy vs idle time over the last steps and
 the per-kernel launch sequence of one register_scan (bench.py C4 run)."""
 import csv
+import re
 import sys
 from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+def short(n):
+    m = re.search(r"(k_\w+|__amd_rocclr_\w+)(<[^>(]*>)?", n)
+    return (m.group(1) + (m.group(2) or "")) if m else n[:40]
+
+
+ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
 print("kernels:", len(ev))
 # steps start at the extraction kernel
 starts = [i for i, e in enumerate(ev) if "k_extract_rows" in e[2]]
@@ -23,12 +29,11 @@ if len(starts) >= 3:
     print(f"one step: span {span/1e3:.1f} us, kernel-busy {busy/1e3:.1f} us, launches {len(seg)}")
     prev_end = t0
     for s, e, n in seg:
-        short = n.split("(")[0].replace("void ", "")[:60]
-        print(f"  +{(s - t0)/1e3:8.1f}  gap {(s - prev_end)/1e3:7.1f}  dur {(e - s)/1e3:7.1f}  {short}")
+        print(f"  +{(s - t0)/1e3:8.1f}  gap {(s - prev_end)/1e3:7.1f}  dur {(e - s)/1e3:7.1f}  {n}")
         prev_end = max(prev_end, e)
     tot = defaultdict(float)
     for s, e, n in ev[starts[1]:starts[-1]]:
-        tot[n.split("(")[0][:60]] += (e - s) / 1e3
+        tot[n] += (e - s) / 1e3
     nsteps = len(starts) - 2
     print("per-step kernel time (us):")
     for k, v in sorted(tot.items(), key=lambda x: -x[1]):
