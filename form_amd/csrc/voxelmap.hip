@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -125,7 +127,8 @@ __global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec,
   const uint32_t s = rslot[rec];
   if (s == 0xFFFFFFFFu) return;
   const uint32_t o = atomicAdd(&table[s].first, 1u);
-  pos[o] = tpos[rec];
+  const double4 tp = tpos[rec];
+  pos[o] = make_double4(tp.x, tp.y, tp.z, (double)rec);  // .w: build order (k_match tie-break)
   if (rec < n0) nrm[o] = tnrm[rec];
   seg[o] = rseg[rec];
   rid[o] = rec;
@@ -236,18 +239,31 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         h = (h + 1) & M.mask;
       }
     };
-    auto test = [&](uint32_t i) {
-      const double4 p = M.pos[i];
+    // a record is one double4: world position + its build order in .w (exact in a
+    // double), so a candidate test is one 32-B load
+    auto fold = [&](const double4& p, uint32_t i) {
       const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
       const double d2 = (dx * dx + dz * dz) + dy * dy;
-      if (d2 <= best) {
-        const uint32_t rid = M.rid[i];
-        if (d2 < best || rid < best_rid) {
-          best = d2;
-          best_rid = rid;
-          best_i = i;
-        }
+      const uint32_t rid = (uint32_t)p.w;
+      if (d2 <= best && (d2 < best || rid < best_rid)) {
+        best = d2;
+        best_rid = rid;
+        best_i = i;
       }
+    };
+    // this lane's share (first + g, step kGroup) of records [first, first + count):
+    // four loads in flight per round, folded in record order (the same argmin)
+    auto scan_range = [&](uint32_t first, uint32_t count) {
+      const uint32_t end = first + count;
+      uint32_t i = first + g;
+      for (; i + 3 * kGroup < end; i += 4 * kGroup) {
+        const double4 p0 = M.pos[i], p1 = M.pos[i + kGroup], p2 = M.pos[i + 2 * kGroup], p3 = M.pos[i + 3 * kGroup];
+        fold(p0, i);
+        fold(p1, i + kGroup);
+        fold(p2, i + 2 * kGroup);
+        fold(p3, i + 3 * kGroup);
+      }
+      for (; i < end; i += kGroup) fold(M.pos[i], i);
     };
     auto group_min = [&]() {  // argmin over (d^2, build order) across the kGroup lanes
 #pragma unroll
@@ -271,7 +287,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       first = __shfl(first, 0, kGroup);
       count = __shfl(count, 0, kGroup);
       n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
-      for (uint32_t i = first + g; i < first + count; i += kGroup) test(i);
+      scan_range(first, count);
     }
     group_min();  // every lane now holds the own-voxel best: the bound for phase 2
     // phase 2: the neighbour cells in passes of increasing lower bound — ring-1 faces
@@ -309,7 +325,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
           const uint32_t cnt = __shfl(vc, l, kGroup);
           const uint32_t first = __shfl(vf, l, kGroup);
           n_cand += cnt / kGroup + (g < (int)(cnt % kGroup) ? 1 : 0);
-          for (uint32_t i = first + g; i < first + cnt; i += kGroup) test(i);
+          scan_range(first, cnt);
           group_min();
         }
       }
@@ -349,7 +365,16 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   // work counters (probes, candidate records) for the algorithmic-byte model: one
   // plain store per block (no same-address atomics), summed on the host
   __shared__ uint32_t s_work[2][kMatchThreads / kWave];
+#ifdef FMX_MATCH_MAXLANE  // debug: per-block maximum per lane instead of sums
+  uint32_t wp = n_probe, wc = n_cand;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    wp = max(wp, (uint32_t)__shfl_xor((int)wp, o, 64));
+    wc = max(wc, (uint32_t)__shfl_xor((int)wc, o, 64));
+  }
+#else
   const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
+#endif
   if (lane_id() == 0) {
     s_work[0][threadIdx.x / kWave] = wp;
     s_work[1][threadIdx.x / kWave] = wc;
@@ -358,8 +383,13 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   if (threadIdx.x == 0) {
     uint32_t tp = 0, tc = 0;
     for (int i = 0; i < kMatchThreads / kWave; ++i) {
+#ifdef FMX_MATCH_MAXLANE
+      tp = max(tp, s_work[0][i]);
+      tc = max(tc, s_work[1][i]);
+#else
       tp += s_work[0][i];
       tc += s_work[1][i];
+#endif
     }
     work[2 * blockIdx.x] = tp;
     work[2 * blockIdx.x + 1] = tc;
@@ -848,6 +878,16 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
     }
     c->last_probes = tp;
     c->last_cands = tc;
+    static const bool dbg = std::getenv("FMX_MATCH_DEBUG") != nullptr;  // per-block work spread
+    if (dbg && c->work_blocks) {
+      uint32_t mp = 0, mc = 0;
+      for (uint32_t b = 0; b < c->work_blocks; ++b) {
+        mp = std::max(mp, c->h_work.p[2 * b]);
+        mc = std::max(mc, c->h_work.p[2 * b + 1]);
+      }
+      fprintf(stderr, "match blocks %u: probes mean %.1f max %u, candidate-lane-tests mean %.1f max %u\n",
+              c->work_blocks, tp / c->work_blocks, mp, tc / c->work_blocks, mc);
+    }
   }
   c->counts_pending = false;
 }
