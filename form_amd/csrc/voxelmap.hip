@@ -185,8 +185,8 @@ struct MatchArgs {
 // sizes (~4e4 queries) the chip would otherwise hold ~2 waves per CU and every
 // probe's latency would be exposed.
 constexpr int kGroup = 8;
-constexpr int kQPB = 64;                     // queries per block
-constexpr int kMatchThreads = kQPB * kGroup;  // 512
+constexpr int kQPB = 32;  // queries per block: 256 threads, so every block of a scan is resident at once
+constexpr int kMatchThreads = kQPB * kGroup;  // 256
 
 __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
@@ -200,6 +200,10 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
                                                          uint32_t* __restrict__ host_counts,
                                                          uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off) {
   extern __shared__ uint32_t s_hist[];  // [K]
+#ifdef FMX_MATCH_TIMING
+  uint64_t mtime[6];
+  mtime[0] = wall_clock64();
+#endif
   if (icp && icp->icp_done) return;  // device ICP loop already converged
   const double* Tj = icp ? icp->Tbefore : a.Tj;
   const bool planar = blockIdx.x < a.nb_pl;
@@ -290,6 +294,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       scan_range(first, count);
     }
     group_min();  // every lane now holds the own-voxel best: the bound for phase 2
+#ifdef FMX_MATCH_TIMING
+    mtime[1] = wall_clock64();
+#endif
     // phase 2: the neighbour cells in passes of increasing lower bound — ring-1 faces
     // (shifts 1..6), ring-1 edges + corners (7..26), then ring 2 (27..124) when the
     // map uses half-width cells — each pass pruned against the best found so far.  In
@@ -331,8 +338,14 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       }
     };
     pass(1, 7);
+#ifdef FMX_MATCH_TIMING
+    mtime[2] = wall_clock64();
+#endif
     pass(7, 27);
     if (a.rings >= 2) pass(27, 125);
+#ifdef FMX_MATCH_TIMING
+    mtime[3] = wall_clock64();
+#endif
     if (g == 0) {
       const bool found = best_i != 0xFFFFFFFFu;
       int32_t pair = -1;
@@ -362,6 +375,13 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
     }
   }
+#ifdef FMX_MATCH_TIMING
+  __syncthreads();
+  mtime[4] = wall_clock64();
+  if (threadIdx.x == 0 && (blockIdx.x % 50) == 0)
+    printf("MB %d %llu %llu %d %d %d\n", (int)blockIdx.x, (unsigned long long)mtime[0], (unsigned long long)mtime[4],
+           (int)(mtime[1] - mtime[0]), (int)(mtime[2] - mtime[1]), (int)(mtime[3] - mtime[2]));
+#endif
   // work counters (probes, candidate records) for the algorithmic-byte model: one
   // plain store per block (no same-address atomics), summed on the host
   __shared__ uint32_t s_work[2][kMatchThreads / kWave];
@@ -450,6 +470,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, carry);
   }
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef FMX_MATCH_TIMING
+  if (threadIdx.x == 0) printf("MLAST %d %llu\n", (int)blockIdx.x, (unsigned long long)wall_clock64());
+#endif
 }
 
 struct HistIn {
@@ -543,8 +566,8 @@ __global__ __launch_bounds__(1024) void k_pair_base(int K, uint32_t nb_pl, uint3
 }
 
 // Stable scatter of accepted matches into pair-major SoA correspondences:
-// one wave per match block (kQPB = 64 queries), rank by ballot within the wave.
-__global__ __launch_bounds__(64) void k_pair_scatter(uint32_t nq_pl, uint32_t nq_pt, uint32_t nb_pl, int K,
+// one (partial) wave per match block (kQPB queries), rank by ballot within the wave.
+__global__ __launch_bounds__(kQPB) void k_pair_scatter(uint32_t nq_pl, uint32_t nq_pt, uint32_t nb_pl, int K,
                                                      const int32_t* __restrict__ m_pair,
                                                      const double4* __restrict__ m_pi,
                                                      const double4* __restrict__ m_ni,
@@ -838,7 +861,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
                        c->h_counts.d);
     FMX_HIP(hipGetLastError());
     if (nb > 0 && c->K > 0) {
-      hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(64), 0, st, c->n_qpl, c->n_qpt, a.nb_pl, a.K, c->m_pair.p,
+      hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(kQPB), 0, st, c->n_qpl, c->n_qpt, a.nb_pl, a.K, c->m_pair.p,
                          c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, nb_pt, c->pair_base.p,
                          c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt, icp);
       FMX_HIP(hipGetLastError());

@@ -6,7 +6,7 @@ p = synth.default_params(geo)
 ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**p)))
 w = synth.World()
 ctx.profile(True)
-for k in range(30):
+for k in range(12):
     s = synth.raycast(w, synth.trajectory_pose(k), geo, synth.SEED + 7919 * (k + 1), "cuda:0")
     ctx.register_scan(s)
     torch.cuda.synchronize()
