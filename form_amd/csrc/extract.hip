@@ -65,7 +65,7 @@ __device__ int block_compact(int b, int e, F flag, int* list, int* ws) {
 
 // KC > 0: neighbor_points fixed at compile time (the default 5), so every +-k loop
 // unrolls and its LDS reads issue together; KC = 0 reads it from the arguments.
-template <int KC>
+template <int KC, bool PAR>
 __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __restrict__ scan, ExArgs a,
                                                               uint8_t* __restrict__ planar_mask,
                                                               uint32_t* __restrict__ sel_slots,
@@ -148,6 +148,319 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
   __syncthreads();
   TSTAMP();
 
+  if constexpr (PAR) {
+    // ================= sector-parallel selection (pps <= 512, S <= 16) ==============
+    // Sectors interact only through suppression spilling k-1 columns over a sector
+    // boundary (parity hazard 5).  Every sector is run speculatively at once (wave s
+    // = sector s) as if nothing spilled in; then, in sector order, sector s is re-run
+    // only if the FINAL selection of sector s-1 suppresses a column that the
+    // speculative run of s depended on: for the planar greedy a column it ACCEPTED
+    // (removing a candidate the greedy rejected changes nothing), for the point pass
+    // a column that was ELIGIBLE (the stride of extract_point depends on |U|).
+    const int S = a.S, pps = C / S, P1 = a.P + 1;
+    const int w = tid / kWave, lane = lane_id();
+    auto sec_b = [&](int s) { return s * pps; };
+    auto sec_e = [&](int s) { return s == S - 1 ? C : (s + 1) * pps; };
+    int* srt = reinterpret_cast<int*>(pts);                         // sorted candidate columns, per sector at b
+    uint32_t* pos = reinterpret_cast<uint32_t*>(srt + C);            // chunk-lane stamps per column
+    const int nwd = (C + 63) / 64 + 1;
+    uint64_t* accb = reinterpret_cast<uint64_t*>(pts) + C;           // accepted (speculative) bitmap
+    int* klist = reinterpret_cast<int*>(accb + nwd);                 // [S][P+1] kept columns in key order
+    int* sel_pt = reinterpret_cast<int*>(curv);                      // point selections, per sector at b (after planar)
+    __shared__ int s_cntS[16], s_keepS[16], s_nuS[16], s_nptS[16];
+    if (tid < 16) s_cntS[tid] = s_keepS[tid] = s_nuS[tid] = s_nptS[tid] = 0;
+    for (int c = tid; c < C; c += kRowThreads) pos[c] = 0xFFFFFFFFu;
+    for (int i = tid; i < nwd; i += kRowThreads) accb[i] = 0;
+    __syncthreads();
+    // P1: candidates (used && curvature < threshold, :340-342) as keys (curvature
+    // bits, column), per sector
+    for (int c = tid; c < C; c += kRowThreads)
+      if (used[c] && (double)curv[c] < a.thr) {
+        const int s = min(c / pps, S - 1);
+        keys[sec_b(s) + atomicAdd(&s_cntS[s], 1)] = ((uint64_t)__float_as_uint(curv[c]) << 32) | (uint32_t)c;
+      }
+    __syncthreads();
+    TSTAMP();
+    // P2: wave s bitonic-sorts sector s's keys in registers (8 per lane, blocked:
+    // element e = lane * 8 + u), pads with ~0
+    if (w < S) {
+      const int b = sec_b(w), n = s_cntS[w];
+      uint64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = lane * 8 + u < n ? keys[b + lane * 8 + u] : ~0ull;
+#pragma unroll
+      for (int kk = 2; kk <= 512; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+          if (j >= 8) {
+            const int lj = j >> 3;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int e = lane * 8 + u;
+              const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)v[u], lj, 64);
+              const bool up = (e & kk) == 0, lower = (e & j) == 0;
+              v[u] = (up == lower) ? (v[u] < o ? v[u] : o) : (v[u] < o ? o : v[u]);
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int pu = u ^ j;
+              if (pu > u) {
+                const int e = lane * 8 + u;
+                const bool up = (e & kk) == 0;
+                const uint64_t x = v[u], y = v[pu];
+                const bool sw = up ? (x > y) : (x < y);
+                v[u] = sw ? y : x;
+                v[pu] = sw ? x : y;
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (lane * 8 + u < n) srt[b + lane * 8 + u] = (int)(uint32_t)v[u];
+    }
+    __syncthreads();
+    TSTAMP();
+    // planar greedy of sector s by one wave (:343-355), as k_extract_rows; columns
+    // [b, blk_hi] are suppressed by the previous sector (blk_hi < b: none)
+    auto planar_greedy = [&](int s, int blk_hi) {
+      const int b = sec_b(s), e = sec_e(s), n = s_cntS[s];
+      int kept = 0;
+      uint32_t chunk = 0;
+      for (int base = 0; base < n && kept < P1; base += kWave, ++chunk) {
+        const uint32_t stamp = ((uint32_t)s << 14) | chunk;
+        const int idx = base + lane;
+        const bool in = idx < n;
+        const int c = in ? srt[b + idx] : b;
+        const int lo = c - (k - 1) < b ? b : c - (k - 1), hi = c + (k - 1) >= e ? e - 1 : c + (k - 1);
+        bool und = in && c > blk_hi;
+        if (in) {
+          pos[c] = (stamp << 6) | (uint32_t)lane;
+          const int w0 = lo >> 6, w1 = hi >> 6;
+          for (int ww = w0; ww <= w1; ++ww) {
+            uint64_t m = accb[ww];
+            if (ww == w0) m &= ~0ull << (lo & 63);
+            if (ww == w1) m &= ~0ull >> (63 - (hi & 63));
+            if (m) und = false;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint64_t conf = 0;
+        if (und) {
+#pragma unroll
+          for (int j = lo; j <= hi; ++j) {
+            const uint32_t q = pos[j];
+            if ((q >> 6) == stamp && (int)(q & 63) < lane) conf |= 1ull << (q & 63);
+          }
+        }
+        uint64_t A = 0;
+        for (;;) {
+          const uint64_t U = __ballot(und);
+          if (U == 0) break;
+          const bool acc = und && (conf & U) == 0;
+          A |= __ballot(acc);
+          if (acc || (conf & A) != 0) und = false;
+        }
+        if ((A >> lane) & 1) {
+          const int rank = kept + __popcll(A & lanemask_lt());
+          if (rank < P1) klist[s * P1 + rank] = c;
+          atomicOr(reinterpret_cast<unsigned long long*>(&accb[c >> 6]), 1ull << (c & 63));
+        }
+        kept += __popcll(A);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane == 0) s_keepS[s] = kept < P1 ? kept : P1;
+    };
+    if (w < S) planar_greedy(w, -1);
+    __syncthreads();
+    TSTAMP();
+    // P4: fix-up in sector order (wave 0)
+    if (w == 0) {
+      for (int s = 1; s < S; ++s) {
+        const int b = sec_b(s), e = sec_e(s);
+        const int np = s_keepS[s - 1];
+        int mx = -1;
+        for (int i = lane; i < np; i += kWave) mx = max(mx, klist[(s - 1) * P1 + i]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+        const int hi = min(mx + (k - 1), e - 1);
+        if (mx < 0 || hi < b) continue;
+        // did the speculative run accept a column in [b, hi]?
+        bool hit = false;
+        for (int c = b + lane; c <= hi; c += kWave)
+          if ((accb[c >> 6] >> (c & 63)) & 1) hit = true;
+        if (!__ballot(hit)) continue;
+        for (int c = b + lane; c < e; c += kWave)  // clear the sector's accepted bits
+          atomicAnd(reinterpret_cast<unsigned long long*>(&accb[c >> 6]), ~(1ull << (c & 63)));
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        planar_greedy(s, hi);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __syncthreads();
+    TSTAMP();
+    // P5: suppression used[c +- n], n in [0, k) of every kept point (:347-350)
+    for (int t = tid; t < S * P1; t += kRowThreads) {
+      const int s = t / P1, i = t % P1;
+      if (i < s_keepS[s]) {
+        const int c = klist[t];
+        for (int n = 0; n < k; ++n) {
+          used[c + n] = 0;
+          used[c - n] = 0;
+        }
+      }
+    }
+    __syncthreads();
+    int pl_count = 0;
+    for (int s = 0; s < S; ++s) {
+      const int nk = s_keepS[s];
+      for (int i = tid; i < nk; i += kRowThreads)
+        if (pl_count + i < a.cap_pl) sel_slots[(size_t)r * a.cap_pl + pl_count + i] = (uint32_t)klist[s * P1 + i];
+      pl_count += nk;
+    }
+    TSTAMP();
+    // ---------------- point features (extraction.tpp:70-96)
+    // eligible = (used == planar_valid) && point_valid (:77-79); state[] keeps the
+    // eligibility for the fix-up
+    for (int c = tid; c < C; c += kRowThreads) {
+      const uint8_t f = flg[c];
+      const uint8_t el = ((f & 1) && (used[c] == ((f >> 2) & 1))) ? 1 : 0;
+      win[c] = el;
+      state[c] = el;
+    }
+    __syncthreads();
+    TSTAMP();
+    // one sector's extract_point by one wave: U = eligible columns of [b, e) in
+    // order (suppressed columns [b, blk_hi] excluded), phase A literal by lane 0,
+    // phase B as a register scan; suppression stays inside the sector (what it spills
+    // into the next sector is the fix-up's business)
+    auto point_pass = [&](int s, int blk_hi) {
+      const int b = sec_b(s), e = sec_e(s);
+      int nu = 0;
+      for (int c0 = b; c0 < e; c0 += kWave) {
+        const int c = c0 + lane;
+        const bool f = c < e && c > blk_hi && win[c] != 0;
+        const uint64_t m = __ballot(f);
+        if (f) list[b + nu + __popcll(m & lanemask_lt())] = c;
+        nu += __popcll(m);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      auto suppress = [&](int c) {
+        for (int n = 0; n < k; ++n) {
+          if (c + n < e) win[c + n] = 0;
+          if (c - n >= b) win[c - n] = 0;
+        }
+      };
+      int nf = 0, offA = 0;
+      bool stopA = false;
+      const int factor = a.Ppt > 0 ? 1 + nu / a.Ppt : 0;
+      if (lane == 0 && a.Ppt > 0) {
+        for (int off = 0; off < factor && !stopA; ++off) {
+          for (int ui = off; ui < nu; ui += factor) {
+            const int c = list[b + ui];
+            if (win[c]) {
+              sel_pt[b + nf] = c;
+              suppress(c);
+              nf++;
+            }
+            if (nf > a.Ppt) {
+              stopA = true;
+              offA = off;
+              break;
+            }
+          }
+        }
+      }
+      nf = __shfl(nf, 0, 64);
+      stopA = __shfl((int)stopA, 0, 64) != 0;
+      offA = __shfl(offA, 0, 64);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (stopA) {
+        const int nA = nf;
+        int last = -0x40000000;
+        const int ohi = min(factor, nu);  // heads U[o] exist for o < nu only
+        for (int o0 = offA + 1; o0 < ohi; o0 += kWave) {
+          const int o = o0 + lane;
+          const int c = o < ohi ? list[b + o] : 0x7FFFFFFF;
+          const int el = o < ohi ? (int)win[c] : 0;
+          const int nl = min(kWave, ohi - o0);
+          for (int l = 0; l < nl; ++l) {
+            const int cl = __builtin_amdgcn_readlane(c, l);
+            const int ell = __builtin_amdgcn_readlane(el, l);
+            if (ell && cl > last + (k - 1)) {
+              if (lane == 0) sel_pt[b + nf] = cl;
+              last = cl;
+              nf++;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int i = nA + lane; i < nf; i += kWave) suppress(sel_pt[b + i]);  // phase-B heads (:388-391)
+      }
+      if (lane == 0) {
+        s_nptS[s] = nf;
+        s_nuS[s] = nu;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    };
+    if (w < S) point_pass(w, -1);
+    __syncthreads();
+    TSTAMP();
+    // Q3: fix-up in sector order (wave 0): the previous sector's final selections
+    // suppress [b, mx + k - 1]; if an eligible column lies there, re-run the sector
+    if (w == 0) {
+      for (int s = 1; s < S; ++s) {
+        const int b = sec_b(s), e = sec_e(s);
+        const int np = s_nptS[s - 1], bp = sec_b(s - 1);
+        int mx = -1;
+        for (int i = lane; i < np; i += kWave) mx = max(mx, sel_pt[bp + i]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+        const int hi = min(mx + (k - 1), e - 1);
+        if (mx < 0 || hi < b) continue;
+        bool hit = false;
+        for (int c = b + lane; c <= hi; c += kWave)
+          if (state[c]) hit = true;
+        if (!__ballot(hit)) continue;
+        for (int c = b + lane; c < e; c += kWave) win[c] = state[c];  // eligibility before the speculative run
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        point_pass(s, hi);
+      }
+    }
+    __syncthreads();
+    TSTAMP();
+    int pt_count = 0;
+    for (int s = 0; s < S; ++s) {
+      const int np = s_nptS[s], b = sec_b(s);
+      for (int i = tid; i < np; i += kRowThreads)  // (bounded: selections are >= k apart)
+        if (pt_count + i < a.cap_pt) pt_slots[(size_t)r * a.cap_pt + pt_count + i] = (uint32_t)sel_pt[b + i];
+      pt_count += np;
+    }
+    if (tid == 0) {
+      row_counts[2 * r] = (uint32_t)min(pl_count, a.cap_pl);
+      row_counts[2 * r + 1] = (uint32_t)min(pt_count, a.cap_pt);
+    }
+#ifdef FMX_EXTRACT_TIMING
+    if (tid == 0 && (r == 5 || r == 64 || r == 120)) {
+      int d[16] = {0};
+      for (int i = 1; i < nts && i < 17; ++i) d[i - 1] = (int)(tstamp[i] - tstamp[i - 1]);
+      printf("PAR row %d: pre %d %d %d %d | cand %d sort %d greedy %d fix %d supp+out %d | elig %d pass %d fix %d\n", r, d[0], d[1],
+             d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11]);
+    }
+#endif
+    return;
+  } else {
   // ---------------- planar features: sectors in order (extraction.tpp:44-68)
   // pts[] is dead from here on; its 16C bytes hold the key-sorted candidates srt[C],
   // the chunk-lane map pos[C] ((stamp << 6) | lane) and the accepted bitmap accb.
@@ -324,11 +637,12 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
         // than k-1 columns past the last taken head: a 1-D greedy scanned from
         // registers, 64 heads per chunk, state kept wave-uniform.
         int last = -0x40000000;
-        for (int o0 = offA + 1; o0 < factor; o0 += kWave) {
+        const int ohi = min(factor, nu);  // heads U[o] exist for o < nu only
+        for (int o0 = offA + 1; o0 < ohi; o0 += kWave) {
           const int o = o0 + tid;
-          const int c = o < factor ? list[o] : 0x7FFFFFFF;
-          const int el = o < factor ? (int)win[c] : 0;
-          const int nl = min(kWave, factor - o0);
+          const int c = o < ohi ? list[o] : 0x7FFFFFFF;
+          const int el = o < ohi ? (int)win[c] : 0;
+          const int nl = min(kWave, ohi - o0);
           for (int l = 0; l < nl; ++l) {
             const int cl = __builtin_amdgcn_readlane(c, l);
             const int ell = __builtin_amdgcn_readlane(el, l);
@@ -376,6 +690,7 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
            d[18], d[19], d[20], d[21], d[22], d[23]);
   }
 #endif
+  }  // !PAR
 }
 
 // Per-row 64-column block AABBs of the planar-valid points (one wave per block),
@@ -1031,20 +1346,39 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   c->cols = C;
   const size_t lds = (size_t)C * (16 + 4 + 4 + 4 + 4);
   if (!c->lds_attr_set) {
-    FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extract_rows<5>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * (16 + 4 + 4 + 4 + 4)));
-    FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extract_rows<0>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * (16 + 4 + 4 + 4 + 4)));
+    const int lmax = 4096 * (16 + 4 + 4 + 4 + 4);
+    const void* kern[4] = {reinterpret_cast<const void*>(k_extract_rows<5, false>),
+                           reinterpret_cast<const void*>(k_extract_rows<0, false>),
+                           reinterpret_cast<const void*>(k_extract_rows<5, true>),
+                           reinterpret_cast<const void*>(k_extract_rows<0, true>)};
+    for (const void* kf : kern) FMX_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, lmax));
     c->lds_attr_set = true;
   }
+  // sector-parallel selection when every sector sorts in one wave's registers (<= 512
+  // columns), there is a wave per sector, sectors are longer than the suppression
+  // reach, and the kept lists fit the dead point area of LDS
+  const int pps = C / a.S;
+  const size_t nwd = (size_t)(C + 63) / 64 + 1;
+  static const bool seq_sel = std::getenv("FMX_SEQ_SECTORS") != nullptr;  // A/B / test switch
+  const bool par = !seq_sel && pps <= 512 && a.S <= 16 && pps >= 2 * a.k &&
+                   8 * (size_t)C + 8 * nwd + 4 * (size_t)a.S * (a.P + 1) <= 16 * (size_t)C;
   {
     ProfScope ps(c->prof, PROF_EXTRACT_ROWS, 16.0 * N + N, st);
-    if (a.k == 5)
-      hipLaunchKernelGGL(k_extract_rows<5>, dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
-                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
-    else
-      hipLaunchKernelGGL(k_extract_rows<0>, dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
-                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+    if (par) {
+      if (a.k == 5)
+        hipLaunchKernelGGL((k_extract_rows<5, true>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                           c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+      else
+        hipLaunchKernelGGL((k_extract_rows<0, true>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                           c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+    } else {
+      if (a.k == 5)
+        hipLaunchKernelGGL((k_extract_rows<5, false>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a,
+                           c->planar_mask.p, c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+      else
+        hipLaunchKernelGGL((k_extract_rows<0, false>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a,
+                           c->planar_mask.p, c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+    }
   }
   FMX_HIP(hipGetLastError());
   const int nslots = R * a.cap_pl;

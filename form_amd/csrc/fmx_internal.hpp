@@ -30,6 +30,10 @@ struct StatusError : std::runtime_error {
       throw ::fmx::HipError(std::string(#call) + ": " + hipGetErrorString(e_));              \
   } while (0)
 
+inline uint64_t& dbuf_reallocs() {  // diagnostic (FMX_HOST_TIMING prints it)
+  static uint64_t n = 0;
+  return n;
+}
 // Growable device buffer (grows only; contents are not preserved across growth).
 template <class T>
 struct DBuf {
@@ -37,9 +41,10 @@ struct DBuf {
   size_t cap = 0;
   void ensure(size_t n) {
     if (n <= cap) return;
-    if (p) (void)hipFree(p);
+    ++dbuf_reallocs();
+    if (p) (void)hipFree(p);  // synchronizes the device: grow geometrically so it stays rare
     p = nullptr;
-    size_t c = n + n / 4 + 64;
+    size_t c = 2 * n + 64;
     FMX_HIP(hipMalloc(&p, c * sizeof(T)));
     cap = c;
   }
@@ -282,10 +287,11 @@ struct HostTiming {
   ~HostTiming() {
     if (!on) return;
     static const char* names[8] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop", "insert+tail",
-                                   "lm_host_math", "launch"};
+                                   "map_host_prep", "map_launches"};
     for (int i = 0; i < 8; ++i)
       if (n[i]) fprintf(stderr, "host %-14s %10.1f us total %8llu calls %8.2f us/call\n", names[i], t[i] * 1e6,
                         (unsigned long long)n[i], t[i] * 1e6 / n[i]);
+    fprintf(stderr, "host device-buffer reallocations %llu\n", (unsigned long long)dbuf_reallocs());
   }
 };
 inline HostTiming& host_timing() {

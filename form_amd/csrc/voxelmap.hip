@@ -664,6 +664,7 @@ uint64_t next_pow2(uint64_t v) {
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w,
                    hipStream_t stream) {
   hipStream_t st = stream ? stream : c->stream;
+  HostScope* hs_prep = new HostScope(6);
   const int K = (int)scans.size();
   const int Kc = std::max(K, 1);
   c->map_scans = scans;
@@ -711,6 +712,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     nrec[t] = n;
   }
   c->map_blob.ensure(n_d);
+  delete hs_prep;
   FMX_HIP(hipMemcpyAsync(c->map_blob.p, hp, n_d * sizeof(double), hipMemcpyHostToDevice, st));
   c->map_poses_p = c->map_blob.p;
   c->map_inv_p = c->map_blob.p + 12 * (size_t)Kc;
@@ -738,6 +740,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   M.rid.ensure(n + 1);
   const double bytes = 2.0 * 32.0 * nrec[0] + 2.0 * 16.0 * nrec[1] + 16.0 * (double)slots;
   ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
+  HostScope* hs_l = new HostScope(7);
   if (n > 0) {
     BuildArgs ba;
     ba.pool_pos[0] = c->pool[0].pos.p;
@@ -769,6 +772,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
                        M.tpos.p, M.tnrm.p, reinterpret_cast<Slot*>(M.table.p), M.pos.p, M.nrm.p, M.seg.p, M.rid.p);
     FMX_HIP(hipGetLastError());
   }
+  delete hs_l;
   c->have_map = true;
   c->have_match = false;
   c->have_qo = false;
