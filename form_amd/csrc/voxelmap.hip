@@ -184,7 +184,7 @@ struct MatchArgs {
 // (d^2, build order).  ~8x the threads of a lane-per-query kernel: at per-scan
 // sizes (~4e4 queries) the chip would otherwise hold ~2 waves per CU and every
 // probe's latency would be exposed.
-constexpr int kGroup = 8;
+constexpr int kGroup = 8;  // lanes per query (16 made the kernel 15% faster but register_scan slower)
 constexpr int kQPB = 32;  // queries per block: 256 threads, so every block of a scan is resident at once
 constexpr int kMatchThreads = kQPB * kGroup;  // 256
 
@@ -269,18 +269,29 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       }
       for (; i < end; i += kGroup) fold(M.pos[i], i);
     };
-    auto group_min = [&]() {  // argmin over (d^2, build order) across the kGroup lanes
-#pragma unroll
-      for (int o = kGroup / 2; o > 0; o >>= 1) {
-        const double ob = __shfl_xor(best, o, kGroup);
-        const uint32_t orid = __shfl_xor(best_rid, o, kGroup);
-        const uint32_t oi = __shfl_xor(best_i, o, kGroup);
+    // argmin over (d^2, build order) across the group's lanes with DPP moves (VALU
+    // latency, no LDS crossbar): [row_mirror l <-> 15-l,] row_half_mirror l <-> 7-l,
+    // quad xor 2, quad xor 1 leave every lane with the group minimum
+    auto group_min = [&]() {
+      auto step = [&](auto ctrl_tag) {
+        constexpr int CTRL = decltype(ctrl_tag)::value;
+        const long long bb = __double_as_longlong(best);
+        const int blo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)bb, CTRL, 0xF, 0xF, false);
+        const int bhi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(bb >> 32), CTRL, 0xF, 0xF, false);
+        const double ob = __longlong_as_double((long long)(((unsigned long long)(uint32_t)bhi << 32) | (uint32_t)blo));
+        const uint32_t orid = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_rid, CTRL, 0xF, 0xF, false);
+        const uint32_t oi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_i, CTRL, 0xF, 0xF, false);
         if (oi != 0xFFFFFFFFu && (best_i == 0xFFFFFFFFu || ob < best || (ob == best && orid < best_rid))) {
           best = ob;
           best_rid = orid;
           best_i = oi;
         }
-      }
+      };
+      static_assert(kGroup == 8 || kGroup == 16, "DPP reduction assumes 8- or 16-lane groups");
+      if constexpr (kGroup == 16) step(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
+      step(std::integral_constant<int, 0x141>{});  // row_half_mirror
+      step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+      step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
     };
     const bool inr = key_in_range(bx, by, bz);
     // phase 1: the query's own voxel (shift 0, visited first by the reference too),
