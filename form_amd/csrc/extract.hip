@@ -26,6 +26,7 @@
 #include "fmx_internal.hpp"
 
 #include <cfloat>
+#include <functional>
 #include <cstdlib>
 
 namespace fmx {
@@ -1315,7 +1316,8 @@ __global__ __launch_bounds__(256) void k_write_features(const float4* __restrict
 
 }  // namespace
 
-void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out) {
+void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
+                 const std::function<void()>& while_waiting) {
   const auto& E = c->P.extraction;
   ExArgs a;
   a.R = R;
@@ -1430,7 +1432,10 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
                        c->h_u32.d, c->h_flag.d, seq);
   }
   FMX_HIP(hipGetLastError());
-  // totals (planar-with-normal, points, selected) were written to mapped host memory
+  // totals (planar-with-normal, points, selected) were written to mapped host memory;
+  // the caller may queue independent work (register_scan: the map build on the side
+  // stream) before the host blocks on them
+  if (while_waiting) while_waiting();
   wait_flag(c, c->h_flag.p, seq);
   const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
   // sized for the worst case, not the totals just read: a wrong total can then never

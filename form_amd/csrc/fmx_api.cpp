@@ -403,7 +403,8 @@ void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const
   c->have_qo = false;
 }
 
-void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out) {
+void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out,
+                const std::function<void()>& while_waiting = nullptr) {
   const auto& E = c->P.extraction;
   const size_t R = (size_t)E.num_rows, C = (size_t)E.num_columns;
   if (!xyzw && n) throw StatusError(FMX_E_INVAL, "null scan");
@@ -420,7 +421,7 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
     FMX_HIP(hipMemcpyAsync(c->scan.p, xyzw, n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     d = c->scan.p;
   }
-  run_extract(c, d, (int)R, (int)C, out);
+  run_extract(c, d, (int)R, (int)C, out, while_waiting);
   c->q_scan = scan;
   c->have_queries = true;
   c->have_match = false;
@@ -617,32 +618,38 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     if (i != j) cj[i] = {0, 0};
   // to_voxel_map x2, voxel width = max_dist_matching (form.cpp:61-65).  The map holds
   // only earlier scans at their current estimates, so it does not depend on this
-  // scan's features: FMX_MAP_SIDE builds it on the side stream next to extraction
-  // (measured neutral: host launch cost already serializes the two).
+  // scan's features.
   std::set<uint64_t> sset;
   for (int t = 0; t < 2; ++t)
     for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
   std::vector<uint64_t> scans(sset.begin(), sset.end());
   std::vector<double> poses(12 * scans.size());
   for (size_t k = 0; k < scans.size(); ++k) std::memcpy(&poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double));
-  static const bool side = std::getenv("FMX_MAP_SIDE") != nullptr;  // A/B switch, default off
-  if (side) {
-    FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
-    FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
-    FMX_HIP(hipEventRecord(c->ev_join, c->side));
-  } else {
-    HostScope hs_map(3);
-    run_map_build(c, scans, poses.data(), P.max_dist_matching);
-  }
-  // extract (form.cpp:51)
+  // The map build goes to the side stream and is queued while the extraction kernels
+  // run (extraction occupies one CU per scan line, so the build's kernels take the
+  // idle CUs, and its host launch cost hides behind the extraction wait).
+  // FMX_MAP_INLINE: build on the main stream first (A/B).
+  static const bool inline_map = std::getenv("FMX_MAP_INLINE") != nullptr;
   fmx_feature_counts fc{};
-  {
+  if (inline_map) {
+    {
+      HostScope hs_map(3);
+      run_map_build(c, scans, poses.data(), P.max_dist_matching);
+    }
     HostScope hs_ex(2);
     do_extract(c, xyzw, n, j, on_dev, &fc);
+  } else {
+    FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
+    HostScope hs_ex(2);
+    do_extract(c, xyzw, n, j, on_dev, &fc, [&] {
+      HostScope hs_map(3);
+      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
+      FMX_HIP(hipEventRecord(c->ev_join, c->side));
+    });
+    FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   }
   HostScope* hs_icp = new HostScope(4);
-  if (side) FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   uint64_t icp = 0, lm_it = 0, lins = 0;
   static const bool host_lm = std::getenv("FMX_DEVICE_LM") == nullptr;  // default: host LM
   if (host_lm) {

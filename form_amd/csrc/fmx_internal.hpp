@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -362,7 +363,8 @@ inline uint32_t next_flag(fmx_ctx* c) {
   return ++c->flag_seq;
 }
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
-void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out);
+void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
+                 const std::function<void()>& while_waiting = nullptr);
 // st: stream to build on (default the context stream; register_scan uses the side
 // stream so the build overlaps extraction)
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w,
