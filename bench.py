@@ -47,6 +47,10 @@ def parse():
                     help="extra steps, after the timed ones, with per-kernel HIP-event timing (roofline); "
                          "default = --steps.  The timed region itself runs without event overhead.")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="smooth", choices=["smooth", "single"],
+                    help="ConstraintManager mode: smooth = the reference default (window smoother), "
+                         "single = the disable_smoothing ablation (single-pose LM)")
+    ap.add_argument("--no-ablation", action="store_true", help="skip the other mode's secondary measurement")
     ap.add_argument("--subdiv", type=int, default=None, help="override voxel_subdivision (device map cells per voxel edge)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
@@ -88,12 +92,14 @@ def sum_over_ranks(x, world, local):
     return float(t.item())
 
 
-def cpu_baseline(scans_host, params, budget_s):
+def cpu_baseline(scans_host, params, budget_s, single):
     """Oracle register_scan on the host cores over the first scans of the same stream."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O  # CPU baseline only (test infrastructure)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    est = O.Estimator(O.default_params(params), threads)
+    prm = O.default_params(params)
+    prm.disable_smoothing = int(single)
+    est = O.Estimator(prm, threads)
     times = []
     t_all = time.perf_counter()
     poses = []
@@ -108,18 +114,20 @@ def cpu_baseline(scans_host, params, budget_s):
     steady = times[1:] if len(times) > 2 else times
     per = float(np.median(steady))
     return dict(value=1.0 / per, unit="scans/s", cores=threads, kind="port",
-                sample=f"oracle register_scan (C++ restatement, std::thread at the reference's two TBB sites) "
+                sample=f"oracle register_scan ({'single-pose' if single else 'smoothing'} mode; C++ restatement, "
+                       f"std::thread at the reference's TBB sites: normals, match queries, factor linearization) "
                        f"over the first {len(times)} scans of the same synthetic stream; median of "
                        f"{len(steady)} steady-state scans = {per * 1e3:.1f} ms/scan",
                 ms_per_scan=per * 1e3), poses
 
 
-def ate_block(scans_host, oracle_poses, params, k0, device):
+def ate_block(scans_host, oracle_poses, params, k0, device, single):
     """ATE of the GPU path and of the CPU oracle path over the same scans against the
     synthetic ground truth (the newer_college ATE is unavailable
     offline).  Untimed; a fresh context replays the sample."""
     n = len(oracle_poses)
-    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params)), device=device)
+    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params),
+                                          disable_smoothing=single), device=device)
     gpu = []
     for s in scans_host[:n]:
         ctx.register_scan(s)
@@ -235,8 +243,29 @@ def main():
     scans = [synth.raycast(world_obj, synth.trajectory_pose(k0 + k), geo, synth.SEED + 7919 * (k0 + k + 1), dev)
              for k in range(total)]
     torch.cuda.synchronize()
-    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params),
-                                          voxel_subdivision=a.subdiv or 0), device=local)
+    single = a.mode == "single"
+
+    def new_ctx(single_pose):
+        return fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params),
+                                               voxel_subdivision=a.subdiv or 0, disable_smoothing=single_pose),
+                           device=local)
+
+    ablation = None
+    if not a.no_ablation:  # the other mode over the same scans (secondary, untimed by the driver)
+        actx = new_ctx(not single)
+        for k in range(a.warmup):
+            actx.register_scan(scans[k])
+        actx.sync()
+        ta = time.perf_counter()
+        for k in range(a.warmup, a.warmup + a.steps):
+            actx.register_scan(scans[k])
+        actx.sync()
+        ta = time.perf_counter() - ta
+        ablation = {"mode": "single-pose (disable_smoothing)" if not single else "smoothing (default)",
+                    "scans_per_s": round(a.steps / ta, 3), "ms_per_step": round(ta / a.steps * 1e3, 3)}
+        actx.close()
+        del actx
+    ctx = new_ctx(single)
     for k in range(a.warmup):
         ctx.register_scan(scans[k])
     ctx.sync()
@@ -301,7 +330,7 @@ def main():
         "dtype": "fp32 points / fp64 map, residuals and normal equations",
         "data": "synthetic (ray-cast organized scans, seed 0x464F524D; no datasets offline)",
         "config": {"workload": f"{a.workload}: {geo.rows}x{geo.cols} organized scan stream ({n_pts} pts/scan), "
-                               "register_scan single-pose mode",
+                               f"register_scan, {'single-pose ablation (disable_smoothing)' if single else 'smoothing mode (ConstraintManager default)'}",
                    "points_per_scan": n_pts, "parallelism": f"replicas x{world}"},
         "mpts_per_s": round(value * n_pts / 1e6, 3),
         "roofline": roof,
@@ -310,10 +339,12 @@ def main():
         "counters": st_mean,
         "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
     }
+    if ablation is not None:
+        out["ablation"] = ablation
     if not a.no_cpu_baseline and world == 1:
         host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
-        out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s)
-        out["ate"] = ate_block(host, opos, params, k0, local)
+        out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s, single)
+        out["ate"] = ate_block(host, opos, params, k0, local, single)
     print(json.dumps(out))
     if world > 1:
         import torch.distributed as dist

@@ -21,7 +21,7 @@ using namespace fmx;
 // ============================================================================ profiling
 namespace fmx {
 static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest", "fit",      "compact",   "map_build",
-                                             "match",        "pair_sort", "linearize", "lin_final", "error_eval", "insert"};
+                                             "match",        "pair_sort", "linearize", "lin_final", "error_eval", "insert", "window"};
 
 ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), bytes(by), st(s) {
   if (!pr.on) return;
@@ -64,160 +64,11 @@ static void prof_collect(fmx_ctx* c) {
 }
 }  // namespace fmx
 
-// ============================================================================ pose algebra
+#include "pose.hpp"
+#include "smoother.hpp"
+using namespace fmxh;
+
 namespace {
-struct Pose {
-  double m[12];  // row-major [R | t]
-};
-Pose identity() {
-  Pose p{};
-  p.m[0] = p.m[5] = p.m[10] = 1.0;
-  return p;
-}
-Pose compose(const Pose& a, const Pose& b) {  // gtsam Pose3::operator*
-  Pose c;
-  for (int i = 0; i < 3; ++i) {
-    for (int j = 0; j < 3; ++j)
-      c.m[4 * i + j] = (a.m[4 * i] * b.m[j] + a.m[4 * i + 1] * b.m[4 + j]) + a.m[4 * i + 2] * b.m[8 + j];
-    c.m[4 * i + 3] = ((a.m[4 * i] * b.m[3] + a.m[4 * i + 1] * b.m[7]) + a.m[4 * i + 2] * b.m[11]) + a.m[4 * i + 3];
-  }
-  return c;
-}
-Pose inverse(const Pose& a) {  // (R^T, R^T(-t))
-  Pose c;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) c.m[4 * i + j] = a.m[4 * j + i];
-  const double nt[3] = {-a.m[3], -a.m[7], -a.m[11]};
-  for (int i = 0; i < 3; ++i) c.m[4 * i + 3] = (c.m[4 * i] * nt[0] + c.m[4 * i + 1] * nt[1]) + c.m[4 * i + 2] * nt[2];
-  return c;
-}
-void cross(const double a[3], const double b[3], double o[3]) {
-  o[0] = a[1] * b[2] - a[2] * b[1];
-  o[1] = a[2] * b[0] - a[0] * b[2];
-  o[2] = a[0] * b[1] - a[1] * b[0];
-}
-Pose expmap(const double xi[6]) {  // gtsam Pose3::Expmap, tangent [w; v]
-  const double* w = xi;
-  const double* v = xi + 3;
-  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-  double A, B, a, b;
-  if (th2 <= DBL_EPSILON) {
-    A = 1.0;
-    B = 0.5;
-    a = 0.5;
-    b = 1.0 / 6.0;
-  } else {
-    const double th = std::sqrt(th2);
-    A = std::sin(th) / th;
-    B = (1.0 - std::cos(th)) / th2;
-    a = B;
-    b = (th - std::sin(th)) / (th2 * th);
-  }
-  const double W[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
-  Pose T;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      const double w2 = W[i][0] * W[0][j] + W[i][1] * W[1][j] + W[i][2] * W[2][j];
-      T.m[4 * i + j] = (i == j ? 1.0 : 0.0) + A * W[i][j] + B * w2;
-    }
-  double wxv[3], wxwxv[3];
-  cross(w, v, wxv);
-  cross(w, wxv, wxwxv);
-  for (int i = 0; i < 3; ++i) T.m[4 * i + 3] = v[i] + a * wxv[i] + b * wxwxv[i];
-  return T;
-}
-void logmap(const Pose& T, double xi[6]) {  // gtsam Pose3::Logmap
-  const double* m = T.m;
-  const double tr = m[0] + m[5] + m[10];
-  double w[3];
-  if (tr + 1.0 < 1e-10) {
-    if (std::abs(m[10] + 1.0) > 1e-10) {
-      const double s = M_PI / std::sqrt(2.0 + 2.0 * m[10]);
-      w[0] = s * m[2]; w[1] = s * m[6]; w[2] = s * (1.0 + m[10]);
-    } else if (std::abs(m[5] + 1.0) > 1e-10) {
-      const double s = M_PI / std::sqrt(2.0 + 2.0 * m[5]);
-      w[0] = s * m[1]; w[1] = s * (1.0 + m[5]); w[2] = s * m[9];
-    } else {
-      const double s = M_PI / std::sqrt(2.0 + 2.0 * m[0]);
-      w[0] = s * (1.0 + m[0]); w[1] = s * m[4]; w[2] = s * m[8];
-    }
-  } else {
-    const double tr_3 = tr - 3.0;
-    double mag;
-    if (tr_3 < -1e-7) {
-      const double th = std::acos((tr - 1.0) / 2.0);
-      mag = th / (2.0 * std::sin(th));
-    } else {
-      mag = 0.5 - tr_3 * tr_3 / 12.0;
-    }
-    w[0] = mag * (m[9] - m[6]);
-    w[1] = mag * (m[2] - m[8]);
-    w[2] = mag * (m[4] - m[1]);
-  }
-  const double t = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-  xi[0] = w[0]; xi[1] = w[1]; xi[2] = w[2];
-  const double tt[3] = {m[3], m[7], m[11]};
-  if (t < 1e-10) {
-    xi[3] = tt[0]; xi[4] = tt[1]; xi[5] = tt[2];
-    return;
-  }
-  const double wn[3] = {w[0] / t, w[1] / t, w[2] / t};
-  double WT[3], WWT[3];
-  cross(wn, tt, WT);
-  cross(wn, WT, WWT);
-  const double Tan = std::tan(0.5 * t);
-  for (int i = 0; i < 3; ++i) xi[3 + i] = tt[i] - (0.5 * t) * WT[i] + (1 - t / (2. * Tan)) * WWT[i];
-}
-void normalize_rot(Pose& P) {  // gtsam Rot3::normalized (constraints.cpp:93-95)
-  double* R = P.m;
-  const double det = R[0] * (R[5] * R[10] - R[6] * R[9]) - R[1] * (R[4] * R[10] - R[6] * R[8]) +
-                     R[2] * (R[4] * R[9] - R[5] * R[8]);
-  if (std::fabs(det - 1) < 1e-12) return;
-  const double x[3] = {R[0], R[1], R[2]}, y[3] = {R[4], R[5], R[6]};
-  const double err = x[0] * y[0] + x[1] * y[1] + x[2] * y[2];
-  double xo[3], yo[3], zo[3];
-  for (int i = 0; i < 3; ++i) {
-    xo[i] = x[i] - (err / 2) * y[i];
-    yo[i] = y[i] - (err / 2) * x[i];
-  }
-  cross(xo, yo, zo);
-  const double sx = 0.5 * (3 - (xo[0] * xo[0] + xo[1] * xo[1] + xo[2] * xo[2]));
-  const double sy = 0.5 * (3 - (yo[0] * yo[0] + yo[1] * yo[1] + yo[2] * yo[2]));
-  const double sz = 0.5 * (3 - (zo[0] * zo[0] + zo[1] * zo[1] + zo[2] * zo[2]));
-  for (int i = 0; i < 3; ++i) {
-    R[i] = sx * xo[i];
-    R[4 + i] = sy * yo[i];
-    R[8 + i] = sz * zo[i];
-  }
-}
-
-bool chol_solve6(const double H[6][6], const double g[6], double x[6]) {
-  double L[6][6] = {};
-  for (int i = 0; i < 6; ++i)
-    for (int j = 0; j <= i; ++j) {
-      double s = H[i][j];
-      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
-      if (i == j) {
-        if (s <= 0) return false;
-        L[i][i] = std::sqrt(s);
-      } else {
-        L[i][j] = s / L[j][j];
-      }
-    }
-  double y[6];
-  for (int i = 0; i < 6; ++i) {
-    double s = g[i];
-    for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
-    y[i] = s / L[i][i];
-  }
-  for (int i = 5; i >= 0; --i) {
-    double s = y[i];
-    for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
-    x[i] = s / L[i][i];
-  }
-  return true;
-}
-
 // KeyScanner::step (form/mapping/keyscanner.cpp:29-91)
 struct KScan {
   uint64_t idx;
@@ -438,6 +289,12 @@ struct fmx_ctx::Est {
   std::map<uint64_t, std::map<uint64_t, std::pair<uint32_t, uint32_t>>> cons;
   KeyScanner ks;
   std::vector<double> poses_i, poses_j, G, err;
+  // smoothing mode (ConstraintManager members, constraints.hpp:74-101)
+  std::vector<PriorF> priors;  // m_other_factors: the prior on X(0)
+  std::vector<LinF> margs;     // m_other_factors: marginal LinearContainerFactors
+  // every stored pair's linearization at `values` (the last full LM's final state),
+  // keyed (j, i): m_fast_linear and marginalize reuse it
+  std::map<std::pair<uint64_t, uint64_t>, std::vector<double>> gcache;
 };
 
 namespace {
@@ -581,6 +438,174 @@ struct DeviceLM {
   }
 };
 
+// ------------------------------------------------------------------ smoothing mode
+// Window keys (Values order) and their current poses.
+std::vector<uint64_t> window_keys(const fmx_ctx::Est& e) {
+  std::vector<uint64_t> k;
+  for (auto& [s, T] : e.values) k.push_back(s);
+  return k;
+}
+std::vector<Pose> window_poses(const fmx_ctx::Est& e) {
+  std::vector<Pose> x;
+  for (auto& [s, T] : e.values) x.push_back(T);
+  return x;
+}
+
+// m_fast_linear (constraints.cpp:268-288): ONE HessianFactor of every previous pair
+// linearized at m_values.  m_values of those keys are the last full LM's final state,
+// whose per-pair linearizations are cached (minus the pairs marginalization dropped).
+LinF fast_linear(const fmx_ctx::Est& e) {
+  LinF L;
+  std::set<uint64_t> ks;
+  for (auto& [ji, G] : e.gcache) {
+    ks.insert(ji.first);
+    ks.insert(ji.second);
+  }
+  if (ks.empty()) return L;
+  L.keys.assign(ks.begin(), ks.end());
+  DenseSys S;
+  S.init(L.keys);
+  for (auto& [ji, G] : e.gcache) S.add_pair(S.slot.at(ji.second), S.slot.at(ji.first), G.data());
+  for (uint64_t k : L.keys) L.lin.push_back(e.values.at(k));
+  L.info.swap(S.A);
+  return L;
+}
+
+// ICP loop (form.cpp:67-89) + optimize(false) (form.cpp:92-93) in smoothing mode:
+// every LM runs over all window poses; the current scan's FeatureFactors linearize
+// from the sorted match, the stored pairs from the window store (window.hip).
+void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uint64_t& lm_it, uint64_t& lins) {
+  const fmx_params& P = c->P;
+  const double sigma = P.planar_constraint_sigma;
+  const LinF fast = fast_linear(e);
+  const std::vector<uint64_t> keys = window_keys(e);
+  std::map<uint64_t, int> slot;
+  for (size_t k = 0; k < keys.size(); ++k) slot[keys[k]] = (int)k;
+  WinGraph g;
+  g.keys = keys;
+  for (auto& p : e.priors) g.priors.push_back(&p);
+  for (auto& m : e.margs) g.lins.push_back(&m);
+  if (!fast.keys.empty()) g.lins.push_back(&fast);
+  std::vector<double> table;
+  for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
+    ++icp;
+    const Pose before = e.values.at(j);
+    run_match(c, before.m, P.max_dist_matching, P.min_dist_map, nullptr, true);  // pair-major
+    // get_graph(true): the current scan's K pairs (empty ones linearize to zero)
+    g.pairs.clear();
+    for (uint32_t k = 0; k < c->K; ++k) g.pairs.push_back({slot.at(c->map_scans[k]), slot.at(j)});
+    const int K = (int)c->K;
+    g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
+      table.resize(12 * ((size_t)K + 1));
+      for (int k = 0; k < K; ++k) std::memcpy(&table[12 * k], x[slot.at(c->map_scans[k])].m, 12 * sizeof(double));
+      std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
+      win_linearize_current(c, table.data(), sigma, G);
+      match_counts_fetch(c, false);  // the match finished before the linearization
+      for (int k = 0; k < K; ++k)
+        if (c->cnt_pl[k] + c->cnt_pt[k] == 0) std::fill(G + (size_t)k * kPairG, G + (size_t)(k + 1) * kPairG, 0.0);
+    };
+    const WinLMResult R = window_lm(g, window_poses(e));
+    lm_it += R.iters;
+    lins += R.lins;
+    const Pose after = R.x[slot.at(j)];
+    double xi[6];
+    logmap(compose(inverse(before), after), xi);
+    double dn = 0;
+    for (double v : xi) dn += v * v;
+    if (std::sqrt(dn) < P.new_pose_threshold) break;
+    e.values[j] = after;  // update_current_pose
+  }
+  // the last match is the scan's constraint set: into the window store
+  match_counts_fetch(c);
+  win_persist(c, j);
+  // optimize(false): every stored pair's FeatureFactor (constraints.cpp:294-305)
+  const std::vector<WinPair> prs = win_pairs(c);
+  g.lins.clear();
+  for (auto& m : e.margs) g.lins.push_back(&m);
+  g.pairs.clear();
+  for (auto& p : prs) g.pairs.push_back({slot.at(p.i), slot.at(p.j)});
+  if (!prs.empty()) win_set_pairs(c, prs, keys);
+  g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
+    table.resize(12 * keys.size());
+    for (size_t k = 0; k < keys.size(); ++k) std::memcpy(&table[12 * k], x[k].m, 12 * sizeof(double));
+    win_linearize_stored(c, table.data(), (int)keys.size(), sigma, G);
+  };
+  const WinLMResult R = window_lm(g, window_poses(e));
+  lm_it += R.iters;
+  lins += R.lins;
+  for (size_t k = 0; k < keys.size(); ++k) e.values[keys[k]] = R.x[k];  // update_values
+  e.gcache.clear();
+  for (size_t p = 0; p < prs.size(); ++p)
+    e.gcache[{prs[p].j, prs[p].i}].assign(R.G.begin() + p * kPairG, R.G.begin() + (p + 1) * kPairG);
+}
+
+// ConstraintManager::marginalize (constraints.cpp:120-203): the factors touching the
+// marginalized keys (priors, marginal factors, FeatureFactors), linearized at
+// m_values, are eliminated onto the remaining keys as a LinearContainerFactor.
+void smooth_marginalize(fmx_ctx::Est& e, const std::vector<uint64_t>& marg) {
+  std::set<uint64_t> M;
+  for (uint64_t m : marg)
+    if (e.values.count(m)) M.insert(m);
+  if (M.empty()) return;
+  std::set<uint64_t> keys(M.begin(), M.end());
+  std::vector<PriorF> dp;
+  std::vector<LinF> dl;
+  for (auto it = e.priors.begin(); it != e.priors.end();)
+    if (M.count(it->key)) {
+      dp.push_back(*it);
+      it = e.priors.erase(it);
+    } else ++it;
+  for (auto it = e.margs.begin(); it != e.margs.end();) {
+    bool hit = false;
+    for (uint64_t k : it->keys) hit |= M.count(k) > 0;
+    if (hit) {
+      for (uint64_t k : it->keys) keys.insert(k);
+      dl.push_back(std::move(*it));
+      it = e.margs.erase(it);
+    } else ++it;
+  }
+  std::vector<std::pair<std::pair<uint64_t, uint64_t>, const std::vector<double>*>> dpairs;
+  for (auto& [ji, G] : e.gcache)
+    if (M.count(ji.first) || M.count(ji.second)) {
+      dpairs.push_back({ji, &G});
+      keys.insert(ji.first);
+      keys.insert(ji.second);
+    }
+  std::vector<uint64_t> order(M.begin(), M.end()), rest;
+  for (uint64_t k : keys)
+    if (!M.count(k)) rest.push_back(k);
+  order.insert(order.end(), rest.begin(), rest.end());
+  // same factor order as a sorted-Values linearization (priors, linear, pairs), then
+  // permuted so the eliminated keys come first
+  std::vector<uint64_t> sorted(keys.begin(), keys.end());
+  DenseSys S;
+  S.init(sorted);
+  for (auto& p : dp) S.add_prior(p, e.values.at(p.key));
+  for (auto& l : dl) {
+    std::vector<Pose> xk;
+    for (uint64_t k : l.keys) xk.push_back(e.values.at(k));
+    S.add_linf(l, xk);
+  }
+  for (auto& [ji, G] : dpairs) S.add_pair(S.slot.at(ji.second), S.slot.at(ji.first), G->data());
+  DenseSys T;
+  T.init(order);
+  std::vector<int> map(S.D + 1);
+  for (size_t k = 0; k < sorted.size(); ++k)
+    for (int d = 0; d < 6; ++d) map[6 * k + d] = 6 * T.slot.at(sorted[k]) + d;
+  map[S.D] = T.D;
+  for (int r = 0; r <= S.D; ++r)
+    for (int cc = 0; cc <= S.D; ++cc) T.at(map[r], map[cc]) = S.at(r, cc);
+  LinF L;
+  if (!rest.empty() && schur_marginal(T.A, T.D, 6 * (int)M.size(), L.info)) {
+    L.keys = rest;
+    for (uint64_t k : rest) L.lin.push_back(e.values.at(k));
+    e.margs.push_back(std::move(L));
+  }
+  for (auto it = e.gcache.begin(); it != e.gcache.end();)
+    if (M.count(it->first.first) || M.count(it->first.second)) it = e.gcache.erase(it);
+    else ++it;
+}
+
 size_t num_recent_connections(const fmx_ctx::Est& e, uint64_t s, uint64_t oldest) {  // constraints.cpp:319-336
   size_t cnt = 0;
   for (auto& [j, m] : e.cons) {
@@ -613,6 +638,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   e.init = true;
   const uint64_t j = e.scan;
   e.values[j] = pred;
+  if (j == 0) e.priors.push_back(PriorF{0, pred, 1e-3});  // addPrior (constraints.cpp:217-220)
   auto& cj = e.cons[j];
   for (auto& [i, T] : e.values)
     if (i != j) cj[i] = {0, 0};
@@ -652,7 +678,9 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   HostScope* hs_icp = new HostScope(4);
   uint64_t icp = 0, lm_it = 0, lins = 0;
   static const bool host_lm = std::getenv("FMX_DEVICE_LM") == nullptr;  // default: host LM
-  if (host_lm) {
+  if (!P.disable_smoothing) {
+    smooth_register(c, e, j, icp, lm_it, lins);
+  } else if (host_lm) {
     // ICP loop (form.cpp:67-89) with the LM on the host (one sync per linearization)
     DeviceLM lm{c, e, P.planar_constraint_sigma};
     bool converged = false;
@@ -751,7 +779,9 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   auto marg = e.ks.step(j, fc.planar + fc.point, [&](uint64_t i) {
     return num_recent_connections(e, i, e.ks.oldest_rf());
   });
+  if (!P.disable_smoothing) smooth_marginalize(e, marg);
   for (uint64_t m : marg) {
+    if (!P.disable_smoothing) win_remove(c, m);
     e.values.erase(m);
     e.cons.erase(m);
     for (auto& [jj, mm] : e.cons) mm.erase(m);
@@ -794,7 +824,7 @@ void fmx_default_params(fmx_params* p) {
   p->new_pose_threshold = 1e-4;
   p->max_num_rematches = 30;
   p->planar_constraint_sigma = 0.1;  // constraints.hpp:60
-  p->disable_smoothing = 1;
+  p->disable_smoothing = 0;  // ConstraintManager default (constraints.hpp:56): smoothing
   p->max_num_keyscans = 50;  // keyscanner.hpp:55-64
   p->max_steps_unused_keyscan = 10;
   p->max_num_recent_scans = 10;
@@ -869,6 +899,12 @@ void fmx_destroy(fmx_ctx* c) {
   c->partials.release(); c->G.release(); c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
+  {
+    auto& W = c->win;
+    for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }
+    W.chunks.release(); W.chunk_range.release(); W.partials.release(); W.dposes.release();
+    W.pticket.release(); W.dticket.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);

@@ -98,6 +98,7 @@ enum ProfId {
   PROF_LIN_FINAL,
   PROF_ERROR,
   PROF_INSERT,
+  PROF_WINDOW,
   PROF_COUNT
 };
 
@@ -170,10 +171,50 @@ struct IcpDev {
 };
 
 struct Chunk {
-  uint32_t type;  // 0 plane rows, 1 point pairs
+  uint32_t type;  // bits 0-7: 0 plane rows, 1 point pairs; window chunks: pose slot i
+                  // in bits 8-19, pose slot j in bits 20-31
   uint32_t pair;
   uint32_t begin;
   uint32_t end;
+};
+// Linearize chunk sizes: rows strided over the 64 lanes of one wave.
+constexpr int kPlaneChunk = 256;   // plane rows per chunk of the sorted match
+constexpr int kPointChunk = 128;   // point pairs per chunk (three rows each)
+constexpr int kWinPlaneRows = 256;  // window store chunks
+constexpr int kWinPointPairs = 128;
+
+// ---- smoothing-mode window store (window.hip)
+constexpr int kWinMaxArgPoses = 36;  // pose table by value up to this many poses
+struct WinPoses {
+  double m[kWinMaxArgPoses][12];
+};
+struct WinPair {  // one FeatureFactor(X(i), X(j))'s rows in the arena
+  uint64_t i, j;
+  uint64_t pl_off, pt_off;
+  uint32_t pl_n, pt_n;
+};
+struct WinSeg {  // scan j's correspondences (the last match of its ICP loop)
+  uint64_t pl_off = 0, pt_off = 0;
+  uint32_t pl_n = 0, pt_n = 0;
+  std::vector<WinPair> pairs;  // i ascending
+};
+struct WinStore {
+  DBuf<double> pl[2], pt[2];  // ping-pong arenas: plane [9][cap_pl], point [6][cap_pt]
+  int cur = 0;
+  uint64_t cap_pl = 0, cap_pt = 0, tail_pl = 0, tail_pt = 0;
+  std::map<uint64_t, WinSeg> segs;
+  // uploaded pair set (win_set_pairs)
+  DBuf<Chunk> chunks;
+  DBuf<uint32_t> chunk_range;
+  uint32_t nch = 0;
+  int npairs = 0;
+  uint64_t rows_pl = 0, rows_pt = 0;
+  bool chunks_valid = false;
+  // launch scratch
+  DBuf<double> partials, dposes;
+  DBuf<uint32_t> pticket, dticket;
+  HBuf<double> hG, hposes;
+  HBuf<uint32_t> hmeta;
 };
 
 }  // namespace fmx
@@ -269,6 +310,9 @@ struct fmx_ctx {
   // ---- device ICP/LM state
   fmx::DBuf<fmx::IcpDev> icp;
   fmx::HBuf<fmx::IcpDev> h_icp;
+
+  // ---- smoothing-mode window store
+  fmx::WinStore win;
 
   // ---- host estimator state (register_scan)
   struct Est;
@@ -390,6 +434,12 @@ void run_linearize_mapj(fmx_ctx* c, const double* pose_j34, double sigma, int mo
 void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, double* out);
 void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
                  const double* ppj, const uint32_t* nt, const double* tpi, const double* tpj);
-constexpr int kPlaneChunk = 64;  // plane rows per linearize chunk (one wave, one row per lane)
-constexpr int kPointChunk = 64;  // point pairs per linearize chunk (three rows per lane)
+// window.hip (smoothing mode): correspondence store maintenance + batched linearization
+void win_reserve(fmx_ctx* c, uint64_t npl, uint64_t npt);
+void win_persist(fmx_ctx* c, uint64_t j);
+void win_remove(fmx_ctx* c, uint64_t s);
+std::vector<WinPair> win_pairs(fmx_ctx* c);
+void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vector<uint64_t>& keys);
+void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out);
+void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
 }  // namespace fmx

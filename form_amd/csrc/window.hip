@@ -1,0 +1,479 @@
+// window.hip — smoothing mode (ConstraintManager's default, disable_smoothing = false,
+// form/optimization/constraints.hpp:54-56): the window's correspondence store and the
+// batched linearization of MANY FeatureFactors per launch.
+//
+// The reference keeps every scan's matches as PlanePoint/PointPoint buffers per pair
+// (m_constraints[j][i], constraints.hpp:95-101) until scan i or j is marginalized, and
+// GTSAM linearizes them factor by factor:
+//   * fast mode  — the current scan's FeatureFactors every LM iteration of the ICP
+//                  loop (get_graph(true), constraints.cpp:257-266);
+//   * full mode  — every pair every LM iteration of optimize(false)
+//                  (constraints.cpp:294-305, form.cpp:92);
+//   * m_fast_linear / marginalize — every previous (resp. dropped) pair once per scan
+//                  (constraints.cpp:268-288, 164-167).
+// Here: a device arena of pair-major SoA rows (plane p_i, n_i, p_j = 9 doubles; point
+// p_i, p_j = 6 doubles, the same layout the sorted match writes), one segment per
+// scan j, and k_win_linearize: DenseFactor::linearize (gtsam.hpp:67-86) of a list of
+// pairs in ONE launch, 13 x 13 augmented information (91 doubles) + error per pair.
+//
+// k_win_linearize: one wave per chunk (<= kWinPlaneRows plane rows or kWinPointPairs
+// point pairs of one pair, strided over the lanes), fp64 register accumulation of the
+// 91 sums, wave reduce-scatter (entries 0..63 -> lane, 64..90 -> lane pairs), agent-
+// scope partial stores (visible across XCD L2s), a per-pair ticket whose last chunk
+// sums the pair's partials in chunk order (deterministic) and stores that pair's G to
+// pinned host memory (write-through) and drains; a ticket over pairs lets the last
+// finisher publish the completion word.  HBM-bound: 72 B per plane row, 48 B per
+// point pair, ~300 / ~900 flop.
+#include "fmx_device.hpp"
+#include "fmx_internal.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace fmx {
+namespace {
+
+#include "factor_rows.hpp"
+
+constexpr int kWinWaves = 4;  // waves per block, one chunk each
+constexpr int kWinLd = 96;    // doubles per chunk partial (91 used)
+constexpr int kWinG = 92;     // per pair: 91 G entries + error
+
+// v[0..63] summed over the wave; afterwards lane l holds entry l in v[0].
+__device__ __forceinline__ double wave_reduce_scatter64(double (&v)[64]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int half = 32 >> k;
+    const bool hi = (lane >> (5 - k)) & 1;
+#pragma unroll
+    for (int j = 0; j < half; ++j) {
+      const double a = v[j], b = v[j + half];
+      const double send = hi ? a : b;
+      const double keep = hi ? b : a;
+      v[j] = keep + __shfl_xor(send, half, 64);
+    }
+  }
+  return v[0];
+}
+// v[0..31] summed over the wave; afterwards lanes 2i and 2i+1 hold entry i.
+__device__ __forceinline__ double wave_reduce_scatter32w(double (&v)[32]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int half = 16 >> k;
+    const bool hi = (lane >> (5 - k)) & 1;
+#pragma unroll
+    for (int j = 0; j < half; ++j) {
+      const double a = v[j], b = v[j + half];
+      const double send = hi ? a : b;
+      const double keep = hi ? b : a;
+      v[j] = keep + __shfl_xor(send, 32 >> k, 64);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
+__device__ __forceinline__ void agent_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double agent_load(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+struct WinArgs {
+  const Chunk* chunks;
+  const uint32_t* n_chunks;     // device count (chunks of the sorted match) ...
+  uint32_t n_chunks_host;       // ... or this when n_chunks is null
+  const uint32_t* chunk_range;  // [npairs + 1]
+  int npairs;
+  const double* c_pl;
+  size_t ld_pl;
+  const double* c_pt;
+  size_t ld_pt;
+  const double* dposes;  // pose table in device memory, or null: by value (WinPoses)
+  int implicit_j;        // >= 0: chunk.pair indexes pose i, pose j = implicit_j
+  double inv;            // 1 / sigma (FastIsotropic invsigma_, gtsam.hpp:96)
+  double* partials;      // [chunk][kWinLd]
+  uint32_t* pair_ticket; // [pair], self-resetting
+  uint32_t* done_ticket; // self-resetting
+  double* hostG;         // pinned mapped [pair][kWinG]
+  uint32_t* flag;
+  uint32_t seq;
+};
+
+__global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, WinPoses wp) {
+  const int w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t ch = blockIdx.x * kWinWaves + w;
+  const uint32_t nch = a.n_chunks ? *a.n_chunks : a.n_chunks_host;
+  if (nch == 0) {  // nothing to linearize: publish at once
+    if (blockIdx.x == 0 && threadIdx.x == 0) publish_flag(a.flag, a.seq);
+    return;
+  }
+  if (ch >= nch) return;
+  const Chunk d = a.chunks[ch];
+  const uint32_t type = d.type & 0xFFu;
+  const int slot = (int)d.pair;
+  int pi, pj;
+  if (a.implicit_j >= 0) {
+    pi = slot;
+    pj = a.implicit_j;
+  } else {
+    pi = (int)((d.type >> 8) & 0xFFFu);
+    pj = (int)(d.type >> 20);
+  }
+  const double* Ti = a.dposes ? a.dposes + 12 * pi : wp.m[pi];
+  const double* Tj = a.dposes ? a.dposes + 12 * pj : wp.m[pj];
+  double acc[91];
+#pragma unroll
+  for (int i = 0; i < 91; ++i) acc[i] = 0.0;
+  double H[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) H[i] = 0.0;
+  if (type == 0) {
+    for (uint32_t row = d.begin + lane; row < d.end; row += kWave) {
+      const double* c = a.c_pl + row;
+      const size_t ld = a.ld_pl;
+      const double pi3[3] = {c[0], c[ld], c[2 * ld]};
+      const double ni3[3] = {c[3 * ld], c[4 * ld], c[5 * ld]};
+      const double pj3[3] = {c[6 * ld], c[7 * ld], c[8 * ld]};
+      double r;
+      plane_row<0>(Ti, Tj, pi3, ni3, pj3, r, H);
+      accum_row<0>(H, r, a.inv, acc);
+    }
+  } else {
+    for (uint32_t row = d.begin + lane; row < d.end; row += kWave) {
+      const double* c = a.c_pt + row;
+      const size_t ld = a.ld_pt;
+      const double pi3[3] = {c[0], c[ld], c[2 * ld]};
+      const double pj3[3] = {c[3 * ld], c[4 * ld], c[5 * ld]};
+      double wpi[3], wpj[3];
+      d_xform(Ti, pi3[0], pi3[1], pi3[2], wpi);
+      d_xform(Tj, pj3[0], pj3[1], pj3[2], wpj);
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        double r;
+        point_row<0>(Ti, Tj, pi3, pj3, wpi, wpj, ax, r, H);
+        accum_row<0>(H, r, a.inv, acc);
+      }
+    }
+  }
+  // wave sums: entries 0..63 -> lane, 64..90 -> lanes 2i, 2i+1
+  double v64[64], v32[32];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v64[i] = acc[i];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) v32[i] = i < 27 ? acc[64 + i] : 0.0;
+  const double e0 = wave_reduce_scatter64(v64);
+  const double e1 = wave_reduce_scatter32w(v32);
+  double* P = a.partials + (size_t)ch * kWinLd;
+  agent_store(P + lane, e0);
+  if ((lane & 1) == 0 && (lane >> 1) < 27) agent_store(P + 64 + (lane >> 1), e1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the pair's last chunk sums its chunk partials in chunk order
+  const uint32_t cb = a.chunk_range[slot], ce = a.chunk_range[slot + 1];
+  uint32_t t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(a.pair_ticket + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, 0, 64);
+  if (t != ce - cb - 1) return;
+  // chunk partials in chunk order, loads batched 8 deep (adding 0.0 past the end is exact)
+  double s0 = 0.0, s1 = 0.0;
+  for (uint32_t c0 = cb; c0 < ce; c0 += 8) {
+    double x0[8], x1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t c = c0 + u;
+      const double* Pc = a.partials + (size_t)c * kWinLd;
+      x0[u] = c < ce ? agent_load(Pc + lane) : 0.0;
+      x1[u] = (c < ce && lane < 27) ? agent_load(Pc + 64 + lane) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s0 += x0[u];
+      s1 += x1[u];
+    }
+  }
+  // G of this pair straight to pinned host memory (write-through), error = 0.5 G[12][12]
+  double* G = a.hostG + (size_t)slot * kWinG;
+  host_store(G + lane, s0);
+  if (lane < 27) host_store(G + 64 + lane, s1);
+  if (lane == 26) host_store(G + 91, 0.5 * s1);
+  if (lane == 0) __hip_atomic_store(a.pair_ticket + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pair's host stores are performed
+  // pairs with rows (the others have no chunk and never finish; the host zeroes them)
+  uint32_t n_ne = 0;
+  for (int k0 = 0; k0 < a.npairs; k0 += kWave) {
+    const int k = k0 + lane;
+    const bool ne = k < a.npairs && a.chunk_range[k + 1] > a.chunk_range[k];
+    n_ne += (uint32_t)__popcll(__ballot(ne));
+  }
+  if (lane == 0) t = __hip_atomic_fetch_add(a.done_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, 0, 64);
+  if (t != n_ne - 1) return;
+  // every pair finisher drained its host stores before taking its ticket: publish
+  if (lane == 0) {
+    __hip_atomic_store(a.done_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    publish_flag(a.flag, a.seq);
+  }
+}
+
+// Copy n_pl plane rows (9 comps) and n_pt point pairs (6 comps) between SoA buffers.
+__global__ void k_rows_copy(const double* __restrict__ spl, size_t lds_pl, uint64_t so_pl, double* __restrict__ dpl,
+                            size_t ldd_pl, uint64_t do_pl, uint32_t n_pl, const double* __restrict__ spt, size_t lds_pt,
+                            uint64_t so_pt, double* __restrict__ dpt, size_t ldd_pt, uint64_t do_pt, uint32_t n_pt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t npl = (uint64_t)n_pl * 9, npt = (uint64_t)n_pt * 6;
+  if (i < npl) {
+    const uint32_t comp = (uint32_t)(i / n_pl), r = (uint32_t)(i % n_pl);
+    dpl[comp * ldd_pl + do_pl + r] = spl[comp * lds_pl + so_pl + r];
+  } else if (i < npl + npt) {
+    const uint64_t k = i - npl;
+    const uint32_t comp = (uint32_t)(k / n_pt), r = (uint32_t)(k % n_pt);
+    dpt[comp * ldd_pt + do_pt + r] = spt[comp * lds_pt + so_pt + r];
+  }
+}
+
+void rows_copy(hipStream_t st, const double* spl, size_t lds_pl, uint64_t so_pl, double* dpl, size_t ldd_pl,
+               uint64_t do_pl, uint32_t n_pl, const double* spt, size_t lds_pt, uint64_t so_pt, double* dpt,
+               size_t ldd_pt, uint64_t do_pt, uint32_t n_pt) {
+  const uint64_t n = (uint64_t)n_pl * 9 + (uint64_t)n_pt * 6;
+  if (n == 0) return;
+  const uint32_t nb = (uint32_t)((n + 255) / 256);
+  hipLaunchKernelGGL(k_rows_copy, dim3(nb), dim3(256), 0, st, spl, lds_pl, so_pl, dpl, ldd_pl, do_pl, n_pl, spt,
+                     lds_pt, so_pt, dpt, ldd_pt, do_pt, n_pt);
+  FMX_HIP(hipGetLastError());
+}
+
+// Launch k_win_linearize, wait for its word, copy npairs x 92 doubles out.
+void win_launch(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double* G_out,
+                double bytes) {
+  WinStore& W = c->win;
+  hipStream_t st = c->stream;
+  WinPoses wp;
+  if (nposes <= kWinMaxArgPoses) {
+    std::memcpy(wp.m, poses, (size_t)nposes * 12 * sizeof(double));
+    a.dposes = nullptr;
+  } else {
+    W.hposes.ensure(12 * (size_t)nposes);
+    std::memcpy(W.hposes.p, poses, (size_t)nposes * 12 * sizeof(double));
+    W.dposes.ensure(12 * (size_t)nposes);
+    FMX_HIP(hipMemcpyAsync(W.dposes.p, W.hposes.p, (size_t)nposes * 12 * sizeof(double), hipMemcpyHostToDevice, st));
+    a.dposes = W.dposes.p;
+  }
+  const int np = std::max(a.npairs, 1);
+  W.partials.ensure((size_t)std::max<uint32_t>(grid_chunks, 1) * kWinLd);
+  ensure_zeroed(W.pticket, (size_t)np, st);
+  ensure_zeroed(W.dticket, 1, st);
+  W.hG.ensure((size_t)np * kWinG);
+  a.partials = W.partials.p;
+  a.pair_ticket = W.pticket.p;
+  a.done_ticket = W.dticket.p;
+  a.hostG = W.hG.d;
+  a.seq = next_flag(c);
+  a.flag = c->h_flag.d;
+  const uint32_t blocks = std::max<uint32_t>((grid_chunks + kWinWaves - 1) / kWinWaves, 1);
+  {
+    ProfScope ps(c->prof, PROF_WINDOW, bytes, st);
+    hipLaunchKernelGGL(k_win_linearize, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
+    FMX_HIP(hipGetLastError());
+  }
+  wait_flag(c, c->h_flag.p, a.seq);
+  if (G_out) std::memcpy(G_out, W.hG.p, (size_t)a.npairs * kWinG * sizeof(double));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- store maintenance
+// Append the current scan's sorted correspondences (the last fmx match, sorted mode,
+// counts fetched) as segment j: pairs (map_scans[k], j) with rows, i ascending.
+void win_persist(fmx_ctx* c, uint64_t j) {
+  WinStore& W = c->win;
+  hipStream_t st = c->stream;
+  if (!c->have_corr) throw StatusError(FMX_E_STATE, "win_persist: no sorted match");
+  uint64_t npl = 0, npt = 0;
+  for (uint32_t k = 0; k < c->K; ++k) {
+    npl += c->cnt_pl[k];
+    npt += c->cnt_pt[k];
+  }
+  win_reserve(c, npl, npt);
+  WinSeg s;
+  s.pl_off = W.tail_pl;
+  s.pt_off = W.tail_pt;
+  s.pl_n = (uint32_t)npl;
+  s.pt_n = (uint32_t)npt;
+  uint64_t op = 0, ot = 0;
+  for (uint32_t k = 0; k < c->K; ++k) {
+    if (c->cnt_pl[k] + c->cnt_pt[k] > 0)
+      s.pairs.push_back(WinPair{c->map_scans[k], j, s.pl_off + op, s.pt_off + ot, c->cnt_pl[k], c->cnt_pt[k]});
+    op += c->cnt_pl[k];
+    ot += c->cnt_pt[k];
+  }
+  rows_copy(st, c->c_pl.p, c->ld_pl, 0, W.pl[W.cur].p, W.cap_pl, s.pl_off, (uint32_t)npl, c->c_pt.p, c->ld_pt, 0,
+            W.pt[W.cur].p, W.cap_pt, s.pt_off, (uint32_t)npt);
+  W.tail_pl += npl;
+  W.tail_pt += npt;
+  W.segs[j] = std::move(s);
+}
+
+// Room for (npl, npt) more rows at the tail: compact the live segments into the other
+// arena (growing both when the live rows fill more than half of it).
+void win_reserve(fmx_ctx* c, uint64_t npl, uint64_t npt) {
+  WinStore& W = c->win;
+  hipStream_t st = c->stream;
+  if (W.cap_pl == 0) {
+    W.cap_pl = std::max<uint64_t>(c->P.keypoint_pool_capacity, 1u << 20);
+    W.cap_pt = std::max<uint64_t>(W.cap_pl / 4, 1u << 18);
+    for (int b = 0; b < 2; ++b) {
+      W.pl[b].ensure(9 * W.cap_pl);
+      W.pt[b].ensure(6 * W.cap_pt);
+    }
+    W.cap_pl = W.pl[0].cap / 9;  // DBuf over-allocates: use it
+    W.cap_pt = W.pt[0].cap / 6;
+  }
+  if (W.tail_pl + npl <= W.cap_pl && W.tail_pt + npt <= W.cap_pt) return;
+  uint64_t live_pl = npl, live_pt = npt;
+  for (auto& [j, s] : W.segs) {
+    live_pl += s.pl_n;
+    live_pt += s.pt_n;
+  }
+  const int nxt = 1 - W.cur;
+  uint64_t cap_pl = W.cap_pl, cap_pt = W.cap_pt;
+  while (2 * live_pl > cap_pl) cap_pl *= 2;
+  while (2 * live_pt > cap_pt) cap_pt *= 2;
+  if (cap_pl != W.cap_pl || cap_pt != W.cap_pt) {  // grow: both arenas (contents move below)
+    W.pl[nxt].ensure(9 * cap_pl);
+    W.pt[nxt].ensure(6 * cap_pt);
+  }
+  const uint64_t ncap_pl = cap_pl != W.cap_pl ? W.pl[nxt].cap / 9 : W.cap_pl;
+  const uint64_t ncap_pt = cap_pt != W.cap_pt ? W.pt[nxt].cap / 6 : W.cap_pt;
+  uint64_t tpl = 0, tpt = 0;
+  for (auto& [j, s] : W.segs) {
+    rows_copy(st, W.pl[W.cur].p, W.cap_pl, s.pl_off, W.pl[nxt].p, ncap_pl, tpl, s.pl_n, W.pt[W.cur].p, W.cap_pt,
+              s.pt_off, W.pt[nxt].p, ncap_pt, tpt, s.pt_n);
+    for (auto& p : s.pairs) {
+      p.pl_off = p.pl_off - s.pl_off + tpl;
+      p.pt_off = p.pt_off - s.pt_off + tpt;
+    }
+    s.pl_off = tpl;
+    s.pt_off = tpt;
+    tpl += s.pl_n;
+    tpt += s.pt_n;
+  }
+  W.cur = nxt;
+  W.tail_pl = tpl;
+  W.tail_pt = tpt;
+  if (ncap_pl != W.cap_pl || ncap_pt != W.cap_pt) {  // the old arena grows too (free space only)
+    W.pl[1 - nxt].ensure(9 * ncap_pl);
+    W.pt[1 - nxt].ensure(6 * ncap_pt);
+  }
+  W.cap_pl = ncap_pl;
+  W.cap_pt = ncap_pt;
+  W.chunks_valid = false;
+}
+
+// KeypointMap / ConstraintManager erase of scan s (constraints.cpp:195-203): its
+// segment and every pair (s, j) of the other segments.  Rows stay until compaction.
+void win_remove(fmx_ctx* c, uint64_t s) {
+  WinStore& W = c->win;
+  W.segs.erase(s);
+  for (auto& [j, seg] : W.segs)
+    seg.pairs.erase(std::remove_if(seg.pairs.begin(), seg.pairs.end(), [&](const WinPair& p) { return p.i == s; }),
+                    seg.pairs.end());
+  W.chunks_valid = false;
+}
+
+// Every stored pair (j ascending, i ascending): the full-mode factor list.
+std::vector<WinPair> win_pairs(fmx_ctx* c) {
+  std::vector<WinPair> out;
+  for (auto& [j, s] : c->win.segs)
+    for (auto& p : s.pairs) out.push_back(p);
+  return out;
+}
+
+// Chunk table for the stored pairs `prs` (slots = list order) with pose slots into
+// `keys`; uploaded once per pair set (the LM's linearizations reuse it).
+void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vector<uint64_t>& keys) {
+  WinStore& W = c->win;
+  hipStream_t st = c->stream;
+  std::map<uint64_t, uint32_t> slot;
+  for (size_t k = 0; k < keys.size(); ++k) slot[keys[k]] = (uint32_t)k;
+  if (keys.size() > 0xFFF) throw StatusError(FMX_E_INVAL, "window larger than 4095 poses");
+  std::vector<Chunk> ch;
+  std::vector<uint32_t> cr(prs.size() + 1);
+  uint64_t rows_pl = 0, rows_pt = 0;
+  for (size_t k = 0; k < prs.size(); ++k) {
+    const WinPair& p = prs[k];
+    cr[k] = (uint32_t)ch.size();
+    const uint32_t tag = (slot.at(p.i) << 8) | (slot.at(p.j) << 20);
+    for (uint32_t r = 0; r < p.pl_n; r += kWinPlaneRows)
+      ch.push_back(Chunk{0u | tag, (uint32_t)k, (uint32_t)(p.pl_off + r),
+                         (uint32_t)(p.pl_off + std::min<uint32_t>(p.pl_n, r + kWinPlaneRows))});
+    for (uint32_t r = 0; r < p.pt_n; r += kWinPointPairs)
+      ch.push_back(Chunk{1u | tag, (uint32_t)k, (uint32_t)(p.pt_off + r),
+                         (uint32_t)(p.pt_off + std::min<uint32_t>(p.pt_n, r + kWinPointPairs))});
+    rows_pl += p.pl_n;
+    rows_pt += p.pt_n;
+  }
+  cr[prs.size()] = (uint32_t)ch.size();
+  if (W.tail_pl > 0xFFFFFFFFull || W.tail_pt > 0xFFFFFFFFull)
+    throw StatusError(FMX_E_OOM, "window store exceeds 2^32 rows");
+  const size_t nch = ch.size();
+  W.chunks.ensure(nch + 1);
+  W.chunk_range.ensure(prs.size() + 2);
+  W.hmeta.ensure(4 * nch + prs.size() + 2);
+  std::memcpy(W.hmeta.p, ch.data(), nch * sizeof(Chunk));
+  std::memcpy(W.hmeta.p + 4 * nch, cr.data(), cr.size() * sizeof(uint32_t));
+  if (nch) FMX_HIP(hipMemcpyAsync(W.chunks.p, W.hmeta.p, nch * sizeof(Chunk), hipMemcpyHostToDevice, st));
+  FMX_HIP(hipMemcpyAsync(W.chunk_range.p, W.hmeta.p + 4 * nch, cr.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                         st));
+  FMX_HIP(hipStreamSynchronize(st));  // the staging buffer is reused by the next upload
+  W.nch = (uint32_t)nch;
+  W.npairs = (int)prs.size();
+  W.rows_pl = rows_pl;
+  W.rows_pt = rows_pt;
+  W.chunks_valid = true;
+}
+
+// DenseFactor::linearize of every pair of the last win_set_pairs at poses[key slot]:
+// G_out[npairs][92] = 91 packed-upper 13 x 13 entries + error.
+void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out) {
+  WinStore& W = c->win;
+  if (!W.chunks_valid) throw StatusError(FMX_E_STATE, "win_linearize_stored: pair set not uploaded");
+  WinArgs a{};
+  a.chunks = W.chunks.p;
+  a.n_chunks = nullptr;
+  a.n_chunks_host = W.nch;
+  a.chunk_range = W.chunk_range.p;
+  a.npairs = W.npairs;
+  a.c_pl = W.pl[W.cur].p;
+  a.ld_pl = W.cap_pl;
+  a.c_pt = W.pt[W.cur].p;
+  a.ld_pt = W.cap_pt;
+  a.implicit_j = -1;
+  a.inv = 1.0 / sigma;
+  win_launch(c, a, W.nch, poses, nposes, G_out, 72.0 * W.rows_pl + 48.0 * W.rows_pt + 8.0 * kWinG * W.npairs);
+}
+
+// Same for the current scan's K pairs straight from the sorted match (device-built
+// chunk table): poses[k] = pose of map_scans[k], poses[K] = the current pose.
+void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out) {
+  if (!c->have_corr) throw StatusError(FMX_E_STATE, "win_linearize_current: no sorted match");
+  WinArgs a{};
+  a.chunks = c->chunks.p;
+  a.n_chunks = c->n_chunks.p;
+  a.chunk_range = c->chunk_range.p;
+  a.npairs = (int)c->K;
+  a.c_pl = c->c_pl.p;
+  a.ld_pl = c->ld_pl;
+  a.c_pt = c->c_pt.p;
+  a.ld_pt = c->ld_pt;
+  a.implicit_j = (int)c->K;
+  a.inv = 1.0 / sigma;
+  // exact row counts arrive with the match counts; the byte model uses the last known
+  win_launch(c, a, c->max_chunks, poses, (int)c->K + 1, G_out,
+             72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K);
+}
+
+}  // namespace fmx

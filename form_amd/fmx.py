@@ -117,7 +117,7 @@ class EstimatorParams:
     new_pose_threshold: float = 1e-4
     max_num_rematches: int = 30
     planar_constraint_sigma: float = 0.1
-    disable_smoothing: bool = True
+    disable_smoothing: bool = False  # constraints.hpp:56 (True: single-pose ablation)
     max_num_keyscans: int = 50
     max_steps_unused_keyscan: int = 10
     max_num_recent_scans: int = 10

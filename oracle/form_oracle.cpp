@@ -22,6 +22,7 @@
 #include <functional>
 #include <limits>
 #include <map>
+#include <optional>
 #include <set>
 #include <thread>
 #include <unordered_map>
@@ -784,6 +785,341 @@ struct LM {
   }
 };
 
+// ----------------------------------------------------------------------------
+// Smoothing mode — ConstraintManager's default (disable_smoothing = false,
+// constraints.hpp:54-56): Levenberg-Marquardt over EVERY window pose with a dense
+// solve (DenseLMOptimizer, gtsam.hpp:39-56: gfg.optimizeDensely()) on the graph of
+// get_graph(fast) (constraints.cpp:252-308):
+//   * m_other_factors: the prior on X(0) (step, constraints.cpp:217-220) and the
+//     marginal LinearContainerFactors left by marginalize (:120-203);
+//   * fast: the current scan's FeatureFactors + m_fast_linear, ONE HessianFactor of
+//     every previous pair linearized at m_values when first needed (:268-288);
+//   * full: every pair's FeatureFactor (:294-305).
+// External GTSAM algorithms restated from their published behaviour (parity
+// unpinned): PriorFactor<Pose3> (H = I, e = -Local(x, prior)), LinearContainerFactor
+// (error / linearize of a HessianFactor at delta = Local(lin, x)), HessianFactor
+// augmented information [G g; g^T f], partial Cholesky elimination, Values::retract
+// (x * Expmap(delta)), LM damping H + lambda*I (diagonalDamping = false).
+// ----------------------------------------------------------------------------
+using Values = std::map<uint64_t, Pose>;
+
+struct PriorF {  // PriorFactor<Pose3>, isotropic sigma (pose_noise = 1e-3, constraints.hpp:63)
+  uint64_t key;
+  Pose mean;
+  double sigma;
+};
+struct LinF {  // LinearContainerFactor around a HessianFactor over `keys`
+  std::vector<uint64_t> keys;
+  std::vector<Pose> lin;     // linearization point per key
+  std::vector<double> info;  // (6k+1)^2 augmented information [G g; g^T f], row-major
+};
+struct PairRef {  // one FeatureFactor(X(i), X(j)) (factor.cpp:131-186)
+  uint64_t i, j;
+  const PairData* d;
+};
+
+// Dense augmented system [H g; g^T c] over the window keys (Values order).
+struct Sys {
+  std::vector<uint64_t> keys;
+  std::map<uint64_t, int> slot;
+  int D = 0;
+  std::vector<double> A;
+  void init(const std::vector<uint64_t>& ks) {
+    keys = ks;
+    slot.clear();
+    for (size_t k = 0; k < ks.size(); ++k) slot[ks[k]] = (int)k;
+    D = 6 * (int)ks.size();
+    A.assign((size_t)(D + 1) * (D + 1), 0.0);
+  }
+  double& at(int r, int c) { return A[(size_t)r * (D + 1) + c]; }
+  // column of augmented index a of a factor whose key slots are ks (last = rhs)
+  void add_block(const std::vector<int>& cols, const double* info) {  // info full (m x m)
+    const int m = (int)cols.size();
+    for (int a = 0; a < m; ++a)
+      for (int b = 0; b < m; ++b) at(cols[a], cols[b]) += info[a * m + b];
+  }
+};
+
+// LinearContainerFactor::linearize: G' = G, g' = g - G d, f' = f + d^T G d - 2 d^T g.
+void linf_at(const LinF& L, const Values& x, std::vector<double>& out, double* err) {
+  const int n = 6 * (int)L.keys.size(), m = n + 1;
+  std::vector<double> d(n);
+  for (size_t k = 0; k < L.keys.size(); ++k)
+    pose_logmap(compose(inverse(L.lin[k]), x.at(L.keys[k])), &d[6 * k]);
+  out = L.info;
+  std::vector<double> Gd(n, 0.0);
+  for (int r = 0; r < n; ++r) {
+    double s = 0;
+    for (int c = 0; c < n; ++c) s += L.info[r * m + c] * d[c];
+    Gd[r] = s;
+  }
+  double dGd = 0, dg = 0;
+  for (int r = 0; r < n; ++r) {
+    dGd += d[r] * Gd[r];
+    dg += d[r] * L.info[r * m + n];
+  }
+  for (int r = 0; r < n; ++r) {
+    out[r * m + n] -= Gd[r];
+    out[n * m + r] -= Gd[r];
+  }
+  out[n * m + n] += dGd - 2.0 * dg;
+  if (err) *err = 0.5 * out[n * m + n];  // HessianFactor::error(delta) = 0.5 (f - 2 d^T g + d^T G d)
+}
+
+// PriorFactor<Pose3>::evaluateError: H = I, e = -Logmap(x^-1 * prior); whitened 1/sigma.
+void prior_at(const PriorF& P, const Pose& x, double info[49], double* err) {
+  double l[6];
+  pose_logmap(compose(inverse(x), P.mean), l);
+  const double inv = 1.0 / P.sigma;
+  double a[7][7] = {};
+  for (int k = 0; k < 6; ++k) a[k][k] = inv;  // A = I / sigma
+  double b[6];
+  for (int k = 0; k < 6; ++k) b[k] = l[k] * inv;  // b = -e / sigma
+  std::fill(info, info + 49, 0.0);
+  for (int r = 0; r < 6; ++r) {
+    info[r * 7 + r] = inv * inv;
+    info[r * 7 + 6] = info[6 * 7 + r] = inv * b[r];
+  }
+  double f = 0;
+  for (int k = 0; k < 6; ++k) f += b[k] * b[k];
+  info[48] = f;
+  if (err) *err = 0.5 * f;
+  (void)a;
+}
+
+// Cholesky solve of an n x n SPD system (row-major); false when not positive definite.
+bool chol_solve(std::vector<double> H, const std::vector<double>& g, std::vector<double>& x, int n) {
+  for (int j = 0; j < n; ++j) {
+    double s = H[(size_t)j * n + j];
+    for (int k = 0; k < j; ++k) s -= H[(size_t)j * n + k] * H[(size_t)j * n + k];
+    if (!(s > 0)) return false;
+    const double ljj = std::sqrt(s);
+    H[(size_t)j * n + j] = ljj;
+    for (int i = j + 1; i < n; ++i) {
+      double t = H[(size_t)i * n + j];
+      for (int k = 0; k < j; ++k) t -= H[(size_t)i * n + k] * H[(size_t)j * n + k];
+      H[(size_t)i * n + j] = t / ljj;
+    }
+  }
+  std::vector<double> y(n);
+  for (int i = 0; i < n; ++i) {
+    double s = g[i];
+    for (int k = 0; k < i; ++k) s -= H[(size_t)i * n + k] * y[k];
+    y[i] = s / H[(size_t)i * n + i];
+  }
+  x.assign(n, 0.0);
+  for (int i = n - 1; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < n; ++k) s -= H[(size_t)k * n + i] * x[k];
+    x[i] = s / H[(size_t)i * n + i];
+  }
+  return true;
+}
+
+// Columns of a pair's 13 x 13 augmented block in the window system.
+std::vector<int> pair_cols(const Sys& S, uint64_t i, uint64_t j) {
+  std::vector<int> c(13);
+  const int si = S.slot.at(i), sj = S.slot.at(j);
+  for (int k = 0; k < 6; ++k) {
+    c[k] = 6 * si + k;
+    c[6 + k] = 6 * sj + k;
+  }
+  c[12] = S.D;
+  return c;
+}
+void unpack91(const double* G, double full[169]) {
+  int o = 0;
+  for (int a = 0; a < 13; ++a)
+    for (int b = a; b < 13; ++b) full[a * 13 + b] = full[b * 13 + a] = G[o++];
+}
+
+struct WindowGraph {
+  std::vector<const PriorF*> priors;
+  std::vector<const LinF*> lins;
+  std::vector<PairRef> pairs;
+  double sigma;
+  int nthreads;
+
+  // NonlinearFactorGraph::linearize at x into the dense window system; returns the error.
+  // Pair factors are linearized in parallel (GTSAM's TBB linearize), summed in order.
+  double linearize(const Values& x, Sys& S) const {
+    std::vector<uint64_t> ks;
+    for (auto& [k, T] : x) ks.push_back(k);
+    S.init(ks);
+    std::vector<double> G(91 * pairs.size()), e(pairs.size());
+    parallel_for(pairs.size(), nthreads, [&](size_t b, size_t en) {
+      for (size_t p = b; p < en; ++p)
+        linearize_pair(*pairs[p].d, x.at(pairs[p].i), x.at(pairs[p].j), sigma, 0, &G[91 * p], &e[p]);
+    });
+    double err = 0;
+    for (auto* P : priors) {
+      double info[49], pe;
+      prior_at(*P, x.at(P->key), info, &pe);
+      std::vector<int> cols(7);
+      for (int k = 0; k < 6; ++k) cols[k] = 6 * S.slot.at(P->key) + k;
+      cols[6] = S.D;
+      S.add_block(cols, info);
+      err += pe;
+    }
+    for (auto* L : lins) {
+      std::vector<double> info;
+      double le;
+      linf_at(*L, x, info, &le);
+      std::vector<int> cols;
+      for (uint64_t k : L->keys)
+        for (int d = 0; d < 6; ++d) cols.push_back(6 * S.slot.at(k) + d);
+      cols.push_back(S.D);
+      S.add_block(cols, info.data());
+      err += le;
+    }
+    double full[169];
+    for (size_t p = 0; p < pairs.size(); ++p) {
+      unpack91(&G[91 * p], full);
+      S.add_block(pair_cols(S, pairs[p].i, pairs[p].j), full);
+      err += e[p];
+    }
+    return err;
+  }
+  double error(const Values& x) const {
+    std::vector<double> e(pairs.size());
+    parallel_for(pairs.size(), nthreads, [&](size_t b, size_t en) {
+      for (size_t p = b; p < en; ++p) e[p] = error_pair(*pairs[p].d, x.at(pairs[p].i), x.at(pairs[p].j), sigma);
+    });
+    double err = 0;
+    for (auto* P : priors) {
+      double info[49], pe;
+      prior_at(*P, x.at(P->key), info, &pe);
+      err += pe;
+    }
+    for (auto* L : lins) {
+      std::vector<double> info;
+      double le;
+      linf_at(*L, x, info, &le);
+      err += le;
+    }
+    for (double v : e) err += v;
+    return err;
+  }
+};
+
+Values retract(const Values& x, const std::vector<double>& dx) {  // Values::retract
+  Values o;
+  size_t k = 0;
+  for (auto& [key, T] : x) o[key] = compose(T, pose_expmap(&dx[6 * k++]));
+  return o;
+}
+
+// LevenbergMarquardtOptimizer (GTSAM defaults, as LM above) over every window pose.
+Values window_lm(const WindowGraph& g, const Values& x0, int* iters_out) {
+  double lambda = 1e-5;
+  Values x = x0;
+  double err = g.error(x);
+  int iters = 0;
+  if (err <= 0.0) {
+    *iters_out = 0;
+    return x;
+  }
+  auto iterate = [&]() {
+    Sys S;
+    g.linearize(x, S);
+    const int D = S.D;
+    std::vector<double> H((size_t)D * D), gg(D);
+    for (int r = 0; r < D; ++r) {
+      for (int c = 0; c < D; ++c) H[(size_t)r * D + c] = S.at(r, c);
+      gg[r] = S.at(r, D);
+    }
+    const double cc = S.at(D, D), oldLin = 0.5 * cc;
+    while (true) {
+      std::vector<double> Hd = H, dx;
+      for (int r = 0; r < D; ++r) Hd[(size_t)r * D + r] += lambda;
+      const bool ok = chol_solve(Hd, gg, dx, D);
+      bool success = false, stop = false;
+      Values xn;
+      double nerr = err;
+      if (ok) {
+        double dHd = 0, dg = 0;
+        for (int r = 0; r < D; ++r) {
+          double h = 0;
+          for (int c = 0; c < D; ++c) h += H[(size_t)r * D + c] * dx[c];
+          dHd += dx[r] * h;
+          dg += dx[r] * gg[r];
+        }
+        const double newLin = 0.5 * (dHd - 2 * dg + cc), linChange = oldLin - newLin;
+        if (linChange >= 0) {
+          xn = retract(x, dx);
+          nerr = g.error(xn);
+          const double costChange = err - nerr;
+          if (linChange > DBL_EPSILON * oldLin) success = (costChange / linChange) > 1e-3;
+          else success = true;
+          if (std::abs(costChange) < 1e-5 * err) stop = true;
+        }
+      }
+      if (success) {
+        lambda = std::max(0.0, lambda / 10.0);
+        x = xn;
+        err = nerr;
+        return;
+      } else if (!stop) {
+        lambda *= 10.0;
+        if (lambda >= 1e5) return;
+      } else {
+        return;
+      }
+    }
+  };
+  double cur, newErr = err;
+  bool conv;
+  do {
+    cur = newErr;
+    iterate();
+    ++iters;
+    newErr = err;
+    if (newErr <= 0.0) conv = true;
+    else {
+      const double absDec = cur - newErr, relDec = absDec / cur;
+      conv = (relDec <= 1e-5) || (absDec <= 1e-5);
+    }
+  } while (iters < 100 && !conv && std::isfinite(cur));
+  *iters_out = iters;
+  return x;
+}
+
+// Schur complement of the augmented system eliminating the first nm columns (partial
+// Cholesky elimination, GaussianFactorGraph::eliminatePartialMultifrontal): returns
+// the (n - nm + 1)^2 augmented information on the rest; false if the eliminated block
+// is not positive definite.
+bool schur(const std::vector<double>& A, int n, int nm, std::vector<double>& out) {
+  const int m = n + 1, r = m - nm;
+  std::vector<double> L((size_t)nm * nm, 0.0);
+  for (int j = 0; j < nm; ++j) {
+    double s = A[(size_t)j * m + j];
+    for (int k = 0; k < j; ++k) s -= L[(size_t)j * nm + k] * L[(size_t)j * nm + k];
+    if (!(s > 0)) return false;
+    L[(size_t)j * nm + j] = std::sqrt(s);
+    for (int i = j + 1; i < nm; ++i) {
+      double t = A[(size_t)i * m + j];
+      for (int k = 0; k < j; ++k) t -= L[(size_t)i * nm + k] * L[(size_t)j * nm + k];
+      L[(size_t)i * nm + j] = t / L[(size_t)j * nm + j];
+    }
+  }
+  // Y = L^-1 A_MR  (nm x r)
+  std::vector<double> Y((size_t)nm * r);
+  for (int c = 0; c < r; ++c)
+    for (int i = 0; i < nm; ++i) {
+      double s = A[(size_t)i * m + nm + c];
+      for (int k = 0; k < i; ++k) s -= L[(size_t)i * nm + k] * Y[(size_t)k * r + c];
+      Y[(size_t)i * r + c] = s / L[(size_t)i * nm + i];
+    }
+  out.assign((size_t)r * r, 0.0);
+  for (int a = 0; a < r; ++a)
+    for (int b = 0; b < r; ++b) {
+      double s = 0;
+      for (int k = 0; k < nm; ++k) s += Y[(size_t)k * r + a] * Y[(size_t)k * r + b];
+      out[(size_t)a * r + b] = A[(size_t)(nm + a) * m + nm + b] - s;
+    }
+  return true;
+}
+
 // KeyScanner::step (keyscanner.cpp:29-91), restated for the oracle pipeline.
 struct KScan {
   uint64_t idx;
@@ -835,7 +1171,123 @@ struct Estimator {
   std::map<uint64_t, std::vector<float>> kp_planar, kp_point;
   // m_constraints[j][i] -> (planar count, point count)
   std::map<uint64_t, std::map<uint64_t, std::pair<size_t, size_t>>> cons;
+  // smoothing-mode state (ConstraintManager members, constraints.hpp:74-101)
+  std::map<uint64_t, std::map<uint64_t, PairData>> pdata;  // m_constraints[j][i] rows
+  std::vector<PriorF> priors;                              // m_other_factors: priors
+  std::vector<LinF> margs;                                 // m_other_factors: marginals
+  bool have_fast = false;                                  // m_fast_linear
+  LinF fast;
   explicit Estimator(const orc_params& p, int nt) : P(p), nthreads(nt), ks(P) {}
+
+  // Linearize `prs` (+ priors / linear factors) at `values` into a Sys over `order`.
+  void linearize_into(Sys& S, const std::vector<uint64_t>& order, const std::vector<PairRef>& prs,
+                      const std::vector<const PriorF*>& pri, const std::vector<const LinF*>& lfs) const {
+    WindowGraph g{pri, lfs, prs, P.planar_constraint_sigma, nthreads};
+    Values sub;
+    for (uint64_t k : order) sub[k] = values.at(k);
+    g.linearize(sub, S);  // Values order (sorted)
+    if (order != S.keys) {  // permute into `order`
+      Sys T;
+      T.init(order);
+      std::vector<int> map(S.D + 1);
+      for (size_t k = 0; k < S.keys.size(); ++k)
+        for (int d = 0; d < 6; ++d) map[6 * k + d] = 6 * T.slot.at(S.keys[k]) + d;
+      map[S.D] = T.D;
+      for (int r = 0; r <= S.D; ++r)
+        for (int c = 0; c <= S.D; ++c) T.at(map[r], map[c]) = S.at(r, c);
+      S = T;
+    }
+  }
+  // ConstraintManager::optimize (constraints.cpp:103-118) in smoothing mode
+  Values optimize_window(bool fast_mode, int* iters) {
+    std::vector<const PriorF*> pri;
+    std::vector<const LinF*> lfs;
+    for (auto& p : priors) pri.push_back(&p);
+    for (auto& m : margs) lfs.push_back(&m);
+    std::vector<PairRef> prs;
+    for (auto& [j, m] : pdata)
+      for (auto& [i, d] : m) {
+        if (d.np() + d.nt() == 0) continue;  // is_empty (constraints.cpp:34-37)
+        if (fast_mode && j != scan) continue;
+        prs.push_back({i, j, &d});
+      }
+    if (fast_mode) {
+      if (!have_fast) {  // m_fast_linear: every previous pair at m_values (:268-288)
+        std::vector<PairRef> prev;
+        std::set<uint64_t> ks;
+        for (auto& [j, m] : pdata)
+          for (auto& [i, d] : m)
+            if (j != scan && d.np() + d.nt() > 0) {
+              prev.push_back({i, j, &d});
+              ks.insert(i);
+              ks.insert(j);
+            }
+        fast = LinF{};
+        if (!prev.empty()) {
+          std::vector<uint64_t> order(ks.begin(), ks.end());
+          Sys S;
+          linearize_into(S, order, prev, {}, {});
+          fast.keys = order;
+          for (uint64_t k : order) fast.lin.push_back(values.at(k));
+          fast.info = S.A;
+        }
+        have_fast = true;
+      }
+      if (!fast.keys.empty()) lfs.push_back(&fast);
+    }
+    WindowGraph g{pri, lfs, prs, P.planar_constraint_sigma, nthreads};
+    return window_lm(g, values, iters);
+  }
+  // ConstraintManager::marginalize (constraints.cpp:120-203): every factor touching a
+  // marginalized key is linearized at m_values and the keys are eliminated; the
+  // marginal on the remaining keys becomes a LinearContainerFactor.
+  void marginalize(const std::vector<uint64_t>& marg) {
+    std::set<uint64_t> M;
+    for (uint64_t m : marg)
+      if (values.count(m)) M.insert(m);
+    if (M.empty()) return;
+    std::set<uint64_t> keys(M.begin(), M.end());
+    std::vector<PriorF> dp;
+    std::vector<LinF> dl;
+    for (auto it = priors.begin(); it != priors.end();)
+      if (M.count(it->key)) {
+        dp.push_back(*it);
+        it = priors.erase(it);
+      } else ++it;
+    for (auto it = margs.begin(); it != margs.end();) {
+      bool hit = false;
+      for (uint64_t k : it->keys) hit |= M.count(k) > 0;
+      if (hit) {
+        for (uint64_t k : it->keys) keys.insert(k);
+        dl.push_back(std::move(*it));
+        it = margs.erase(it);
+      } else ++it;
+    }
+    std::vector<PairRef> prs;
+    for (auto& [j, m] : pdata)
+      for (auto& [i, d] : m)
+        if (d.np() + d.nt() > 0 && (M.count(i) || M.count(j))) {
+          prs.push_back({i, j, &d});
+          keys.insert(i);
+          keys.insert(j);
+        }
+    std::vector<uint64_t> order(M.begin(), M.end()), rest;
+    for (uint64_t k : keys)
+      if (!M.count(k)) rest.push_back(k);
+    order.insert(order.end(), rest.begin(), rest.end());
+    std::vector<const PriorF*> pri;
+    std::vector<const LinF*> lfs;
+    for (auto& p : dp) pri.push_back(&p);
+    for (auto& l : dl) lfs.push_back(&l);
+    Sys S;
+    linearize_into(S, order, prs, pri, lfs);
+    LinF L;
+    if (!rest.empty() && schur(S.A, S.D, 6 * (int)M.size(), L.info)) {
+      L.keys = rest;
+      for (uint64_t k : rest) L.lin.push_back(values.at(k));
+      margs.push_back(std::move(L));
+    }
+  }
 
   // ConstraintManager::predict_next, constraints.cpp:71-101
   Pose predict_next() const {
@@ -872,6 +1324,8 @@ struct Estimator {
     if (init) ++scan;
     init = true;
     values[scan] = pred;
+    have_fast = false;  // step() resets m_fast_linear (constraints.cpp:214)
+    if (scan == 0) priors.push_back({0, pred, 1e-3});  // addPrior (:217-220)
     cons[scan];  // get_constraints creates buckets for every other scan in values
     for (auto& [i, T] : values)
       if (i != scan) cons[scan][i] = {0, 0};
@@ -901,7 +1355,8 @@ struct Estimator {
     for (auto& [s, v] : kp_point) maps[1].add_scan(s, values.at(s), v.data(), (uint32_t)(v.size() / 3));
     auto t2 = clk::now();
     // ICP loop, form.cpp:67-89
-    std::map<uint64_t, PairData> pairs;
+    std::map<uint64_t, PairData> local_pairs;
+    std::map<uint64_t, PairData>& pairs = P.disable_smoothing ? local_pairs : pdata[scan];
     std::vector<uint8_t> found[2];
     std::vector<double> d2s[2];
     int icp = 0, lm_total = 0;
@@ -936,12 +1391,17 @@ struct Estimator {
           }
         }
       }
-      std::vector<std::pair<Pose, const PairData*>> lp;
-      for (auto& [i, pd] : pairs)
-        if (pd.np() + pd.nt() > 0) lp.push_back({values.at(i), &pd});
-      LM lm{lp, P.planar_constraint_sigma};
       int li = 0;
-      Pose after = lm.optimize(before, &li);
+      Pose after;
+      if (P.disable_smoothing) {
+        std::vector<std::pair<Pose, const PairData*>> lp;
+        for (auto& [i, pd] : pairs)
+          if (pd.np() + pd.nt() > 0) lp.push_back({values.at(i), &pd});
+        LM lm{lp, P.planar_constraint_sigma};
+        after = lm.optimize(before, &li);
+      } else {
+        after = optimize_window(true, &li).at(scan);
+      }
       lm_total += li;
       double xi[6];
       pose_logmap(compose(inverse(before), after), xi);
@@ -951,7 +1411,11 @@ struct Estimator {
       values[scan] = after;
     }
     // optimize(false) (form.cpp:92-93)
-    {
+    if (!P.disable_smoothing) {
+      int li = 0;
+      values = optimize_window(false, &li);  // update_values (same size: replace)
+      lm_total += li;
+    } else {
       std::vector<std::pair<Pose, const PairData*>> lp;
       for (auto& [i, pd] : pairs)
         if (pd.np() + pd.nt() > 0) lp.push_back({values.at(i), &pd});
@@ -981,10 +1445,13 @@ struct Estimator {
     // KeyScanner::step + marginalize (form.cpp:98-111)
     auto marg = ks.step(scan, nq[0] + nq[1],
                         [&](uint64_t i) { return num_recent_connections(i, ks.oldest_rf()); });
+    if (!P.disable_smoothing) marginalize(marg);
     for (uint64_t m : marg) {
       values.erase(m);
       cons.erase(m);
       for (auto& [j, mm] : cons) mm.erase(m);
+      pdata.erase(m);
+      for (auto& [j, mm] : pdata) mm.erase(m);
       kp_planar.erase(m);
       kp_point.erase(m);
     }
@@ -1032,7 +1499,7 @@ void orc_default_params(orc_params* p) {
   p->new_pose_threshold = 1e-4;
   p->max_num_rematches = 30;
   p->planar_constraint_sigma = 0.1;  // constraints.hpp:60
-  p->disable_smoothing = 1;          // the oracle pipeline runs the single-pose mode
+  p->disable_smoothing = 0;          // constraints.hpp:56 default: smoothing (1: single-pose ablation)
   p->max_num_keyscans = 50;          // keyscanner.hpp:55-64
   p->max_steps_unused_keyscan = 10;
   p->max_num_recent_scans = 10;

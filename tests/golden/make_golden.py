@@ -61,17 +61,24 @@ def main():
     np.savez_compressed(os.path.join(HERE, "linearize_small.npz"), n_plane=np_, plane_pi=ppi, plane_ni=pni,
                         plane_pj=ppj, n_point=nt, point_pi=tpi, point_pj=tpj, poses_i=Pi, poses_j=Pj, sigma=0.1,
                         G=G, err=err, G_single=G1, err_single=err1)
-    # 4. register_scan on a 6-scan 16x256 stream (single-pose mode)
-    est = O.Estimator(O.default_params(p), 1)
-    scans, poses, stats = [], [], []
-    for k in range(6):
-        s, _, _ = synth.make_scan("tiny", k, world=world)
-        Tp, st, _ = est.register_scan(s.numpy())
-        scans.append(s.numpy())
-        poses.append(Tp)
-        stats.append(st)
-    np.savez_compressed(os.path.join(HERE, "stream_tiny.npz"), scans=np.stack(scans), poses=np.stack(poses),
-                        stats=np.stack(stats), params=json.dumps(p))
+    # 4. register_scan on a 6-scan 16x256 stream (single-pose ablation mode) and on a
+    #    16-scan stream in the default smoothing mode (marginalization from scan 11 on)
+    #    (a small window — 4 recent scans, 3 keyscans — so keyscans get marginalized)
+    for name, n, single, win in (("stream_tiny.npz", 6, 1, (10, 50)), ("stream_tiny_smooth.npz", 16, 0, (4, 3))):
+        prm = O.default_params(p)
+        prm.disable_smoothing = single
+        prm.max_num_recent_scans, prm.max_num_keyscans = win
+        est = O.Estimator(prm, 1)
+        scans, poses, stats = [], [], []
+        for k in range(n):
+            s, _, _ = synth.make_scan("tiny", k, world=world)
+            Tp, st, _ = est.register_scan(s.numpy())
+            scans.append(s.numpy())
+            poses.append(Tp)
+            stats.append(st)
+        np.savez_compressed(os.path.join(HERE, name), scans=np.stack(scans), poses=np.stack(poses),
+                            stats=np.stack(stats), params=json.dumps(p), disable_smoothing=single,
+                            window=np.array(win))
     print("golden fixtures written to", HERE)
 
 

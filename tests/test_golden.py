@@ -55,10 +55,14 @@ def test_oracle_reproduces_linearize(oracle):
     assert np.array_equal(G1, g["G_single"]) and np.array_equal(err1, g["err_single"])
 
 
-def test_oracle_reproduces_stream(oracle):
-    g = load("stream_tiny.npz")
+@pytest.mark.parametrize("name", ["stream_tiny.npz", "stream_tiny_smooth.npz"])
+def test_oracle_reproduces_stream(oracle, name):
+    g = load(name)
     p = json.loads(str(g["params"]))
-    est = oracle.Estimator(oracle.default_params(p), 1)
+    prm = oracle.default_params(p)
+    prm.disable_smoothing = int(g["disable_smoothing"])
+    prm.max_num_recent_scans, prm.max_num_keyscans = (int(v) for v in g["window"])
+    est = oracle.Estimator(prm, 1)
     for k in range(len(g["scans"])):
         T, st, _ = est.register_scan(g["scans"][k])
         assert np.array_equal(T, g["poses"][k])
@@ -118,9 +122,13 @@ def test_gpu_linearize_golden(fmx_mod):
 
 
 @pytest.mark.gpu
-def test_gpu_stream_golden(fmx_mod):
-    g = load("stream_tiny.npz")
-    ctx = _ctx(fmx_mod, json.loads(str(g["params"])))
+@pytest.mark.parametrize("name", ["stream_tiny.npz", "stream_tiny_smooth.npz"])
+def test_gpu_stream_golden(fmx_mod, name):
+    g = load(name)
+    rec, key = (int(v) for v in g["window"])
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(
+        extraction=fmx_mod.KeypointExtractionParams(**json.loads(str(g["params"]))),
+        disable_smoothing=bool(g["disable_smoothing"]), max_num_recent_scans=rec, max_num_keyscans=key))
     for k in range(len(g["scans"])):
         ctx.register_scan(g["scans"][k])
         assert np.abs(ctx.current_pose() - g["poses"][k]).max() < 1e-6

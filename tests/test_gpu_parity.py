@@ -135,13 +135,21 @@ def test_linearize_matches_oracle(fmx_mod, oracle, single):
     assert np.allclose(e2, er, rtol=1e-10, atol=0)
 
 
-def test_register_stream_matches_oracle(fmx_mod, oracle):
+@pytest.mark.parametrize("single,n,window", [(True, 8, (10, 50)), (False, 8, (10, 50)), (False, 20, (4, 3))])
+def test_register_stream_matches_oracle(fmx_mod, oracle, single, n, window):
+    """register_scan in the single-pose ablation and the default smoothing mode (the
+    small window marginalizes keyscans from scan ~5 on)."""
     geo = synth.GEOMETRIES["tiny"]
     p = synth.default_params(geo)
     world = synth.World()
-    ctx = _ctx(fmx_mod, p)
-    oest = oracle.Estimator(oracle.default_params(p))
-    for k in range(8):
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p),
+                                                  disable_smoothing=single, max_num_recent_scans=window[0],
+                                                  max_num_keyscans=window[1]))
+    prm = oracle.default_params(p)
+    prm.disable_smoothing = int(single)
+    prm.max_num_recent_scans, prm.max_num_keyscans = window
+    oest = oracle.Estimator(prm)
+    for k in range(n):
         s, T, _ = synth.make_scan("tiny", k, world=world)
         ctx.register_scan(s.to("cuda:0"))
         Tg = ctx.current_pose()
