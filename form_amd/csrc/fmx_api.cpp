@@ -499,12 +499,15 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
       table.resize(12 * ((size_t)K + 1));
       for (int k = 0; k < K; ++k) std::memcpy(&table[12 * k], x[slot.at(c->map_scans[k])].m, 12 * sizeof(double));
       std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
+      HostScope hs(10);
       win_linearize_current(c, table.data(), sigma, G);
       match_counts_fetch(c, false);  // the match finished before the linearization
       for (int k = 0; k < K; ++k)
         if (c->cnt_pl[k] + c->cnt_pt[k] == 0) std::fill(G + (size_t)k * kPairG, G + (size_t)(k + 1) * kPairG, 0.0);
     };
+    HostScope* hs_lm = new HostScope(8);
     const WinLMResult R = window_lm(g, window_poses(e));
+    delete hs_lm;
     lm_it += R.iters;
     lins += R.lins;
     const Pose after = R.x[slot.at(j)];
@@ -528,9 +531,12 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
   g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
     table.resize(12 * keys.size());
     for (size_t k = 0; k < keys.size(); ++k) std::memcpy(&table[12 * k], x[k].m, 12 * sizeof(double));
+    HostScope hs(10);
     win_linearize_stored(c, table.data(), (int)keys.size(), sigma, G);
   };
+  HostScope* hs_lm = new HostScope(9);
   const WinLMResult R = window_lm(g, window_poses(e));
+  delete hs_lm;
   lm_it += R.iters;
   lins += R.lins;
   for (size_t k = 0; k < keys.size(); ++k) e.values[keys[k]] = R.x[k];  // update_values
@@ -543,6 +549,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
 // marginalized keys (priors, marginal factors, FeatureFactors), linearized at
 // m_values, are eliminated onto the remaining keys as a LinearContainerFactor.
 void smooth_marginalize(fmx_ctx::Est& e, const std::vector<uint64_t>& marg) {
+  HostScope hs(11);
   std::set<uint64_t> M;
   for (uint64_t m : marg)
     if (e.values.count(m)) M.insert(m);
@@ -903,7 +910,7 @@ void fmx_destroy(fmx_ctx* c) {
     auto& W = c->win;
     for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }
     W.chunks.release(); W.chunk_range.release(); W.partials.release(); W.dposes.release();
-    W.pticket.release(); W.dticket.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
+    W.pticket.release(); W.dticket.release(); W.dbg.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);

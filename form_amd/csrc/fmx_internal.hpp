@@ -178,10 +178,8 @@ struct Chunk {
   uint32_t end;
 };
 // Linearize chunk sizes: rows strided over the 64 lanes of one wave.
-constexpr int kPlaneChunk = 256;   // plane rows per chunk of the sorted match
-constexpr int kPointChunk = 128;   // point pairs per chunk (three rows each)
-constexpr int kWinPlaneRows = 256;  // window store chunks
-constexpr int kWinPointPairs = 128;
+constexpr int kPlaneChunk = 1024;  // plane rows per chunk (one 16-wave block of the window kernel)
+constexpr int kPointChunk = 1024;  // point pairs per chunk (three rows each)
 
 // ---- smoothing-mode window store (window.hip)
 constexpr int kWinMaxArgPoses = 36;  // pose table by value up to this many poses
@@ -212,6 +210,7 @@ struct WinStore {
   bool chunks_valid = false;
   // launch scratch
   DBuf<double> partials, dposes;
+  DBuf<uint64_t> dbg;  // FMX_WIN_TIMING stamps
   DBuf<uint32_t> pticket, dticket;
   HBuf<double> hG, hposes;
   HBuf<uint32_t> hmeta;
@@ -327,13 +326,14 @@ namespace fmx {
 // printed to stderr at exit.  Diagnostic only.
 struct HostTiming {
   bool on = std::getenv("FMX_HOST_TIMING") != nullptr;
-  double t[8] = {0};
-  uint64_t n[8] = {0};
+  double t[14] = {0};
+  uint64_t n[14] = {0};
   ~HostTiming() {
     if (!on) return;
-    static const char* names[8] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop", "insert+tail",
-                                   "map_host_prep", "map_launches"};
-    for (int i = 0; i < 8; ++i)
+    static const char* names[14] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop",
+                                    "insert+tail", "map_host_prep", "map_launches", "fast_lm", "full_lm",
+                                    "lin_callback", "marginalize", "win_launch_call", "win_wait"};
+    for (int i = 0; i < 14; ++i)
       if (n[i]) fprintf(stderr, "host %-14s %10.1f us total %8llu calls %8.2f us/call\n", names[i], t[i] * 1e6,
                         (unsigned long long)n[i], t[i] * 1e6 / n[i]);
     fprintf(stderr, "host device-buffer reallocations %llu\n", (unsigned long long)dbuf_reallocs());

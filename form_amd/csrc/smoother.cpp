@@ -79,65 +79,167 @@ double DenseSys::add_linf(const LinF& L, const std::vector<Pose>& xk) {
     at(col[r], D) += g;
     at(D, col[r]) += g;
   }
-  const double f = I[(size_t)n * m + n] + dGd - 2.0 * dg;
+  const double f = I[(size_t)n * m + n] + (dGd - 2.0 * dg);
   at(D, D) += f;
   return 0.5 * f;
 }
 
 namespace {
 
-// In-place Cholesky of an n x n SPD matrix (row-major, lower factor) + solve.
-bool chol_solve(std::vector<double>& H, const double* g, double* x, int n) {
-  for (int j = 0; j < n; ++j) {
-    double* Hj = &H[(size_t)j * n];
-    double s = Hj[j];
-    for (int k = 0; k < j; ++k) s -= Hj[k] * Hj[k];
-    if (!(s > 0)) return false;
-    const double ljj = std::sqrt(s);
-    Hj[j] = ljj;
-    for (int i = j + 1; i < n; ++i) {
-      double* Hi = &H[(size_t)i * n];
-      double t = Hi[j];
-      for (int k = 0; k < j; ++k) t -= Hi[k] * Hj[k];
-      Hi[j] = t / ljj;
+// Cholesky solve of an n x n SPD system (row-major; factor U = L^T kept in the upper
+// triangle).  Right-looking, blocked by 6 (one pose): a 6-row panel is factored,
+// then each trailing row takes the panel's 6 updates with one load/store per element.
+// Every element still receives its updates k = 0, 1, ... in order, so the factor is
+// bit-identical to the left-looking dot-product form (the oracle's).
+// AVX2 clone dispatched at run time: lanes hold independent elements and there is
+// no FMA contraction (-ffp-contract=off), so both clones round identically.
+__attribute__((target_clones("avx2", "default"))) bool chol_solve(std::vector<double>& A, const double* g, double* x,
+                                                                   int n) {
+  constexpr int B = 6;
+  double* a = A.data();
+  for (int kb = 0; kb < n; kb += B) {
+    const int ke = std::min(n, kb + B);
+    for (int k = kb; k < ke; ++k) {  // panel
+      double* __restrict Uk = a + (size_t)k * n;
+      const double s = Uk[k];
+      if (!(s > 0)) return false;
+      const double ukk = std::sqrt(s);
+      Uk[k] = ukk;
+      for (int m = k + 1; m < n; ++m) Uk[m] = Uk[m] / ukk;
+      for (int i = k + 1; i < ke; ++i) {
+        double* __restrict Ai = a + (size_t)i * n;
+        const double uki = Uk[i];
+        for (int m = i; m < n; ++m) Ai[m] -= uki * Uk[m];
+      }
+    }
+    if (ke - kb == B) {  // trailing rows: 6 ordered updates per element
+      const double* U[B];
+      for (int t = 0; t < B; ++t) U[t] = a + (size_t)(kb + t) * n;
+      for (int i = ke; i < n; ++i) {
+        double* __restrict Ai = a + (size_t)i * n;
+        double u[B];
+        for (int t = 0; t < B; ++t) u[t] = U[t][i];
+        for (int m = i; m < n; ++m) {
+          double v = Ai[m];
+          for (int t = 0; t < B; ++t) v -= u[t] * U[t][m];
+          Ai[m] = v;
+        }
+      }
+    } else {
+      for (int k = kb; k < ke; ++k) {
+        const double* Uk = a + (size_t)k * n;
+        for (int i = ke; i < n; ++i) {
+          double* Ai = a + (size_t)i * n;
+          const double uki = Uk[i];
+          for (int m = i; m < n; ++m) Ai[m] -= uki * Uk[m];
+        }
+      }
     }
   }
-  std::vector<double> y(n);
-  for (int i = 0; i < n; ++i) {
-    const double* Hi = &H[(size_t)i * n];
-    double s = g[i];
-    for (int k = 0; k < i; ++k) s -= Hi[k] * y[k];
-    y[i] = s / Hi[i];
+  std::vector<double> y(g, g + n);  // forward: U^T y = g
+  for (int k = 0; k < n; ++k) {
+    const double* Uk = a + (size_t)k * n;
+    y[k] = y[k] / Uk[k];
+    const double yk = y[k];
+    for (int m = k + 1; m < n; ++m) y[m] -= Uk[m] * yk;
   }
-  for (int i = n - 1; i >= 0; --i) {
+  for (int i = n - 1; i >= 0; --i) {  // back: U x = y
+    const double* Ui = a + (size_t)i * n;
     double s = y[i];
-    for (int k = i + 1; k < n; ++k) s -= H[(size_t)k * n + i] * x[k];
-    x[i] = s / H[(size_t)i * n + i];
+    for (int k = i + 1; k < n; ++k) s -= Ui[k] * x[k];
+    x[i] = s / Ui[i];
   }
   return true;
 }
 
-// NonlinearFactorGraph::linearize at x into S; returns the graph error.
-double linearize_all(const WinGraph& g, const std::vector<Pose>& x, DenseSys& S, std::vector<double>& G, int& lins) {
-  S.init(g.keys);
-  G.assign(g.pairs.size() * kPairG, 0.0);
-  if (!g.pairs.empty()) {
-    g.lin_pairs(x, G.data());
-    ++lins;
+// NonlinearFactorGraph::linearize at x into S; returns the graph error.  The
+// x-independent information blocks (prior H = I/sigma^2, the linear factors' G) are
+// summed once per LM run into `base` in factor order; each linearization starts from
+// a copy of it and adds the rest (rhs / constant terms, then the pairs) in the same
+// factor order, so every element sees the same sequence of additions as a fresh sum.
+struct Assembler {
+  const WinGraph& g;
+  DenseSys base;
+  explicit Assembler(const WinGraph& gr) : g(gr) {
+    base.init(g.keys);
+    const int D = base.D;
+    for (const PriorF* P : g.priors) {
+      const double inv = 1.0 / P->sigma;
+      const int s = base.slot.at(P->key);
+      for (int k = 0; k < 6; ++k) base.at(6 * s + k, 6 * s + k) += inv * inv;
+    }
+    for (const LinF* L : g.lins) {
+      const int n = 6 * (int)L->keys.size(), m = n + 1;
+      std::vector<int> col(n);
+      for (size_t k = 0; k < L->keys.size(); ++k)
+        for (int e = 0; e < 6; ++e) col[6 * k + e] = 6 * base.slot.at(L->keys[k]) + e;
+      const double* I = L->info.data();
+      for (int r = 0; r < n; ++r) {
+        double* row = &base.A[(size_t)col[r] * (D + 1)];
+        for (int c = 0; c < n; ++c) row[col[c]] += I[(size_t)r * m + c];
+      }
+    }
   }
-  double err = 0;
-  for (const PriorF* P : g.priors) err += S.add_prior(*P, x[S.slot.at(P->key)]);
-  for (const LinF* L : g.lins) {
-    std::vector<Pose> xk;
-    for (uint64_t k : L->keys) xk.push_back(x[S.slot.at(k)]);
-    err += S.add_linf(*L, xk);
+  double run(const std::vector<Pose>& x, DenseSys& S, std::vector<double>& G, int& lins) const {
+    if (S.D != base.D || S.keys != base.keys) S = base;
+    else std::memcpy(S.A.data(), base.A.data(), base.A.size() * sizeof(double));
+    G.assign(g.pairs.size() * kPairG, 0.0);
+    if (!g.pairs.empty()) {
+      g.lin_pairs(x, G.data());
+      ++lins;
+    }
+    const int D = S.D;
+    double err = 0;
+    for (const PriorF* P : g.priors) {  // rhs part of DenseSys::add_prior
+      double l[6];
+      logmap(compose(inverse(x[S.slot.at(P->key)]), P->mean), l);
+      const double inv = 1.0 / P->sigma;
+      const int s = S.slot.at(P->key);
+      double f = 0;
+      for (int k = 0; k < 6; ++k) {
+        const double b = l[k] * inv;
+        S.at(6 * s + k, D) += inv * b;
+        S.at(D, 6 * s + k) += inv * b;
+        f += b * b;
+      }
+      S.at(D, D) += f;
+      err += 0.5 * f;
+    }
+    for (const LinF* L : g.lins) {  // rhs part of DenseSys::add_linf
+      const int n = 6 * (int)L->keys.size(), m = n + 1;
+      double d[6 * 64];
+      std::vector<double> dv;
+      double* dp = d;
+      if (n > 6 * 64) {
+        dv.resize(n);
+        dp = dv.data();
+      }
+      for (size_t k = 0; k < L->keys.size(); ++k)
+        logmap(compose(inverse(L->lin[k]), x[S.slot.at(L->keys[k])]), dp + 6 * k);
+      const double* I = L->info.data();
+      double dGd = 0, dg = 0;
+      for (int r = 0; r < n; ++r) {
+        const double* Ir = I + (size_t)r * m;
+        double sr = 0;
+        for (int c = 0; c < n; ++c) sr += Ir[c] * dp[c];
+        const int cr = 6 * S.slot.at(L->keys[r / 6]) + r % 6;
+        const double gr = Ir[n] - sr;
+        S.at(cr, D) += gr;
+        S.at(D, cr) += gr;
+        dGd += dp[r] * sr;
+        dg += dp[r] * Ir[n];
+      }
+      const double f = I[(size_t)n * m + n] + (dGd - 2.0 * dg);
+      S.at(D, D) += f;
+      err += 0.5 * f;
+    }
+    for (size_t p = 0; p < g.pairs.size(); ++p) {
+      S.add_pair(g.pairs[p].first, g.pairs[p].second, &G[p * kPairG]);
+      err += G[p * kPairG + 91];
+    }
+    return err;
   }
-  for (size_t p = 0; p < g.pairs.size(); ++p) {
-    S.add_pair(g.pairs[p].first, g.pairs[p].second, &G[p * kPairG]);
-    err += G[p * kPairG + 91];
-  }
-  return err;
-}
+};
 
 }  // namespace
 
@@ -148,9 +250,10 @@ double linearize_all(const WinGraph& g, const std::vector<Pose>& x, DenseSys& S,
 WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
   WinLMResult R;
   R.x = x0;
+  const Assembler asmb(g);
   DenseSys S, Sn;
   std::vector<double> Gn;
-  double err = linearize_all(g, R.x, S, R.G, R.lins);
+  double err = asmb.run(R.x, S, R.G, R.lins);
   if (err <= 0.0) return R;
   double lambda = 1e-5;
   const int D = S.D;
@@ -181,7 +284,7 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
         if (linChange >= 0) {
           xn.resize(R.x.size());
           for (size_t k = 0; k < R.x.size(); ++k) xn[k] = compose(R.x[k], expmap(&dx[6 * k]));
-          nerr = linearize_all(g, xn, Sn, Gn, R.lins);
+          nerr = asmb.run(xn, Sn, Gn, R.lins);
           const double costChange = err - nerr;
           if (linChange > DBL_EPSILON * oldLin) success = (costChange / linChange) > 1e-3;
           else success = true;

@@ -17,8 +17,8 @@
 // pairs in ONE launch, 13 x 13 augmented information (91 doubles) + error per pair.
 //
 // k_win_linearize: one wave per chunk (<= kWinPlaneRows plane rows or kWinPointPairs
-// point pairs of one pair, strided over the lanes), fp64 register accumulation of the
-// 91 sums, wave reduce-scatter (entries 0..63 -> lane, 64..90 -> lane pairs), agent-
+// point pairs of one pair, 64 per step, the next step's rows loaded while one
+// computes), the 13 x 13 sums on the fp64 matrix cores (stage_and_mfma), agent-
 // scope partial stores (visible across XCD L2s), a per-pair ticket whose last chunk
 // sums the pair's partials in chunk order (deterministic) and stores that pair's G to
 // pinned host memory (write-through) and drains; a ticket over pairs lets the last
@@ -28,6 +28,8 @@
 #include "fmx_internal.hpp"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace fmx {
@@ -35,44 +37,13 @@ namespace {
 
 #include "factor_rows.hpp"
 
-constexpr int kWinWaves = 4;  // waves per block, one chunk each
-constexpr int kWinLd = 96;    // doubles per chunk partial (91 used)
-constexpr int kWinG = 92;     // per pair: 91 G entries + error
+constexpr int kWinWaves = 16;   // waves per block: one chunk of 16 x 64 rows per block
+constexpr int kFinBatch = 16;   // chunk partials in flight per thread in the pair finisher
+constexpr int kWinLd = 96;      // doubles per chunk partial (91 used)
+constexpr int kWinG = 92;       // per pair: 91 G entries + error
+constexpr int kLdsStride = 13;  // doubles per staged row (13 entries; the pad lanes read 0)
 
-// v[0..63] summed over the wave; afterwards lane l holds entry l in v[0].
-__device__ __forceinline__ double wave_reduce_scatter64(double (&v)[64]) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const int half = 32 >> k;
-    const bool hi = (lane >> (5 - k)) & 1;
-#pragma unroll
-    for (int j = 0; j < half; ++j) {
-      const double a = v[j], b = v[j + half];
-      const double send = hi ? a : b;
-      const double keep = hi ? b : a;
-      v[j] = keep + __shfl_xor(send, half, 64);
-    }
-  }
-  return v[0];
-}
-// v[0..31] summed over the wave; afterwards lanes 2i and 2i+1 hold entry i.
-__device__ __forceinline__ double wave_reduce_scatter32w(double (&v)[32]) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const int half = 16 >> k;
-    const bool hi = (lane >> (5 - k)) & 1;
-#pragma unroll
-    for (int j = 0; j < half; ++j) {
-      const double a = v[j], b = v[j + half];
-      const double send = hi ? a : b;
-      const double keep = hi ? b : a;
-      v[j] = keep + __shfl_xor(send, 32 >> k, 64);
-    }
-  }
-  return v[0] + __shfl_xor(v[0], 1, 64);
-}
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void agent_store(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
@@ -102,17 +73,61 @@ struct WinArgs {
   double* hostG;         // pinned mapped [pair][kWinG]
   uint32_t* flag;
   uint32_t seq;
+  uint64_t* dbg;  // FMX_WIN_TIMING: per-wave s_memrealtime stamps [chunk][8], else null
 };
 
+#define WSTAMP(i)                                                            \
+  do {                                                                       \
+    if (a.dbg && threadIdx.x == 0) a.dbg[(size_t)ch * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+// The augmented information of a chunk, sum_rows a a^T with a = [H_i H_j -r] / sigma
+// (13 wide, padded to 16), is a 16 x 16 x rows fp64 GEMM: one v_mfma_f64_16x16x4_f64
+// per 4 rows.  Each lane builds one row's a-vector (64 rows per wave step), stages
+// its 13 entries in LDS, and lane l feeds a_{4t + l/16}[l % 16] (0 for l % 16 >= 13)
+// as BOTH operands of MFMA t (A[i][k] = a_k[i], B[k][j] = a_k[j]); the 16 x 16 result
+// accumulates in 4 registers per lane (row (l >> 4) + 4 r, column l & 15): no
+// cross-lane reduction, no 91 accumulators.  The 16 operand reads are issued before
+// the MFMA chain (one LDS wait per step).
+__device__ __forceinline__ void stage_and_mfma(double* __restrict__ rows /* this wave's LDS */, const double (&av)[13],
+                                               bool valid, f64x4 (&acc)[4]) {
+  const int lane = lane_id();
+  double* mine = rows + lane * kLdsStride;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) mine[i] = valid ? av[i] : 0.0;
+  __builtin_amdgcn_wave_barrier();
+  const int col = lane & 15;
+  const double* src = rows + (lane >> 4) * kLdsStride + (col < 13 ? col : 0);
+  double v[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] = src[4 * t * kLdsStride];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {  // four independent chains: a dependent f64 MFMA waits ~3x its issue time
+    const double x = col < 13 ? v[t] : 0.0;
+    acc[t & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, acc[t & 3], 0, 0, 0);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One block (kWinWaves waves) per chunk (<= kPlaneChunk plane rows or kPointChunk
+// point pairs of one pair); wave w takes rows [64 w, 64 w + 64) of it, one step.
+// The waves' 16 x 16 sums meet in LDS (fixed wave order).  A pair of one chunk: the
+// block writes G to pinned host memory itself; more: block partials (agent-scope
+// stores), a per-pair ticket, the pair's last chunk sums the partials in chunk order.
+// Then a ticket over the pairs with rows lets the last finisher publish the word.
 __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, WinPoses wp) {
-  const int w = threadIdx.x / kWave, lane = lane_id();
-  const uint32_t ch = blockIdx.x * kWinWaves + w;
+  __shared__ double s_rows[kWinWaves][kWave * kLdsStride];
+  __shared__ double s_g[kWinWaves][92];
+  __shared__ uint32_t s_t;
+  const int w = threadIdx.x / kWave, lane = lane_id(), tid = threadIdx.x;
+  const uint32_t ch = blockIdx.x;
   const uint32_t nch = a.n_chunks ? *a.n_chunks : a.n_chunks_host;
   if (nch == 0) {  // nothing to linearize: publish at once
-    if (blockIdx.x == 0 && threadIdx.x == 0) publish_flag(a.flag, a.seq);
+    if (blockIdx.x == 0 && tid == 0) publish_flag(a.flag, a.seq);
     return;
   }
   if (ch >= nch) return;
+  WSTAMP(0);
   const Chunk d = a.chunks[ch];
   const uint32_t type = d.type & 0xFFu;
   const int slot = (int)d.pair;
@@ -126,82 +141,104 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
   }
   const double* Ti = a.dposes ? a.dposes + 12 * pi : wp.m[pi];
   const double* Tj = a.dposes ? a.dposes + 12 * pj : wp.m[pj];
-  double acc[91];
+  f64x4 accs[4];
 #pragma unroll
-  for (int i = 0; i < 91; ++i) acc[i] = 0.0;
-  double H[12];
+  for (int i = 0; i < 4; ++i) accs[i] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const uint32_t row = d.begin + w * kWave + lane;
+  if (d.begin + w * kWave < d.end) {  // wave-uniform: this wave has rows
+    WSTAMP(7);
+    double* rows = s_rows[w];
+    double H[12];
 #pragma unroll
-  for (int i = 0; i < 12; ++i) H[i] = 0.0;
-  if (type == 0) {
-    for (uint32_t row = d.begin + lane; row < d.end; row += kWave) {
-      const double* c = a.c_pl + row;
-      const size_t ld = a.ld_pl;
-      const double pi3[3] = {c[0], c[ld], c[2 * ld]};
-      const double ni3[3] = {c[3 * ld], c[4 * ld], c[5 * ld]};
-      const double pj3[3] = {c[6 * ld], c[7 * ld], c[8 * ld]};
-      double r;
-      plane_row<0>(Ti, Tj, pi3, ni3, pj3, r, H);
-      accum_row<0>(H, r, a.inv, acc);
-    }
-  } else {
-    for (uint32_t row = d.begin + lane; row < d.end; row += kWave) {
-      const double* c = a.c_pt + row;
-      const size_t ld = a.ld_pt;
-      const double pi3[3] = {c[0], c[ld], c[2 * ld]};
-      const double pj3[3] = {c[3 * ld], c[4 * ld], c[5 * ld]};
+    for (int i = 0; i < 12; ++i) H[i] = 0.0;
+    double av[13];
+    const bool valid = row < d.end;
+    if (type == 0) {
+      double c[9];
+      if (valid) {
+#pragma unroll
+        for (int q = 0; q < 9; ++q) c[q] = a.c_pl[row + q * a.ld_pl];
+        const double pi3[3] = {c[0], c[1], c[2]}, ni3[3] = {c[3], c[4], c[5]}, pj3[3] = {c[6], c[7], c[8]};
+        double r;
+        plane_row<0>(Ti, Tj, pi3, ni3, pj3, r, H);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) av[q] = H[q] * a.inv;
+        av[12] = -r * a.inv;
+      }
+      stage_and_mfma(rows, av, valid, accs);
+    } else {
+      double c[6] = {0, 0, 0, 0, 0, 0};
+      if (valid) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) c[q] = a.c_pt[row + q * a.ld_pt];
+      }
+      const double pi3[3] = {c[0], c[1], c[2]}, pj3[3] = {c[3], c[4], c[5]};
       double wpi[3], wpj[3];
       d_xform(Ti, pi3[0], pi3[1], pi3[2], wpi);
       d_xform(Tj, pj3[0], pj3[1], pj3[2], wpj);
 #pragma unroll
       for (int ax = 0; ax < 3; ++ax) {
-        double r;
-        point_row<0>(Ti, Tj, pi3, pj3, wpi, wpj, ax, r, H);
-        accum_row<0>(H, r, a.inv, acc);
+        if (valid) {
+          double r;
+          point_row<0>(Ti, Tj, pi3, pj3, wpi, wpj, ax, r, H);
+#pragma unroll
+          for (int q = 0; q < 12; ++q) av[q] = H[q] * a.inv;
+          av[12] = -r * a.inv;
+        }
+        stage_and_mfma(rows, av, valid, accs);
       }
     }
   }
-  // wave sums: entries 0..63 -> lane, 64..90 -> lanes 2i, 2i+1
-  double v64[64], v32[32];
+  // wave sums (packed upper 13 x 13) -> LDS; block sum in wave order
+  const f64x4 acc = (accs[0] + accs[1]) + (accs[2] + accs[3]);
+  {
+    const int col = lane & 15;
 #pragma unroll
-  for (int i = 0; i < 64; ++i) v64[i] = acc[i];
-#pragma unroll
-  for (int i = 0; i < 32; ++i) v32[i] = i < 27 ? acc[64 + i] : 0.0;
-  const double e0 = wave_reduce_scatter64(v64);
-  const double e1 = wave_reduce_scatter32w(v32);
-  double* P = a.partials + (size_t)ch * kWinLd;
-  agent_store(P + lane, e0);
-  if ((lane & 1) == 0 && (lane >> 1) < 27) agent_store(P + 64 + (lane >> 1), e1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // the pair's last chunk sums its chunk partials in chunk order
-  const uint32_t cb = a.chunk_range[slot], ce = a.chunk_range[slot + 1];
-  uint32_t t = 0;
-  if (lane == 0) t = __hip_atomic_fetch_add(a.pair_ticket + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __shfl(t, 0, 64);
-  if (t != ce - cb - 1) return;
-  // chunk partials in chunk order, loads batched 8 deep (adding 0.0 past the end is exact)
-  double s0 = 0.0, s1 = 0.0;
-  for (uint32_t c0 = cb; c0 < ce; c0 += 8) {
-    double x0[8], x1[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint32_t c = c0 + u;
-      const double* Pc = a.partials + (size_t)c * kWinLd;
-      x0[u] = c < ce ? agent_load(Pc + lane) : 0.0;
-      x1[u] = (c < ce && lane < 27) ? agent_load(Pc + 64 + lane) : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      s0 += x0[u];
-      s1 += x1[u];
+    for (int r = 0; r < 4; ++r) {
+      const int rr = (lane >> 4) + 4 * r;
+      if (rr <= col && col < 13) s_g[w][rr * 13 - rr * (rr - 1) / 2 + (col - rr)] = acc[r];
     }
   }
+  __syncthreads();
+  WSTAMP(1);
+  double bsum = 0.0;
+  if (tid < 91) {
+    bsum = s_g[0][tid];
+#pragma unroll
+    for (int i = 1; i < kWinWaves; ++i) bsum += s_g[i][tid];
+  }
+  const uint32_t cb = a.chunk_range[slot], ce = a.chunk_range[slot + 1];
+  if (ce - cb > 1) {
+    if (tid < 91) agent_store(a.partials + (size_t)ch * kWinLd + tid, bsum);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_t = __hip_atomic_fetch_add(a.pair_ticket + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    WSTAMP(2);
+    if (s_t != ce - cb - 1) return;
+    // the pair's last chunk: partials in chunk order, kFinBatch loads in flight per thread
+    if (tid < 91) {
+      bsum = 0.0;
+      for (uint32_t c0 = cb; c0 < ce; c0 += kFinBatch) {
+        double x[kFinBatch];
+#pragma unroll
+        for (int u = 0; u < kFinBatch; ++u)
+          x[u] = c0 + u < ce ? agent_load(a.partials + (size_t)(c0 + u) * kWinLd + tid) : 0.0;
+#pragma unroll
+        for (int u = 0; u < kFinBatch; ++u) bsum += x[u];
+      }
+    }
+    if (tid == 0) __hip_atomic_store(a.pair_ticket + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  WSTAMP(3);
   // G of this pair straight to pinned host memory (write-through), error = 0.5 G[12][12]
   double* G = a.hostG + (size_t)slot * kWinG;
-  host_store(G + lane, s0);
-  if (lane < 27) host_store(G + 64 + lane, s1);
-  if (lane == 26) host_store(G + 91, 0.5 * s1);
-  if (lane == 0) __hip_atomic_store(a.pair_ticket + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < 91) host_store(G + tid, bsum);
+  if (tid == 90) host_store(G + 91, 0.5 * bsum);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pair's host stores are performed
+  __syncthreads();
+  WSTAMP(4);
+  if (w != 0) return;
   // pairs with rows (the others have no chunk and never finish; the host zeroes them)
   uint32_t n_ne = 0;
   for (int k0 = 0; k0 < a.npairs; k0 += kWave) {
@@ -209,14 +246,17 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
     const bool ne = k < a.npairs && a.chunk_range[k + 1] > a.chunk_range[k];
     n_ne += (uint32_t)__popcll(__ballot(ne));
   }
+  uint32_t t = 0;
   if (lane == 0) t = __hip_atomic_fetch_add(a.done_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   t = __shfl(t, 0, 64);
+  WSTAMP(5);
   if (t != n_ne - 1) return;
   // every pair finisher drained its host stores before taking its ticket: publish
   if (lane == 0) {
     __hip_atomic_store(a.done_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     publish_flag(a.flag, a.seq);
   }
+  WSTAMP(6);
 }
 
 // Copy n_pl plane rows (9 comps) and n_pt point pairs (6 comps) between SoA buffers.
@@ -246,6 +286,46 @@ void rows_copy(hipStream_t st, const double* spl, size_t lds_pl, uint64_t so_pl,
   FMX_HIP(hipGetLastError());
 }
 
+// FMX_WIN_TIMING diagnostics: per launch, the spread of the waves' stamps relative to
+// the first wave start (us, 100 MHz s_memrealtime), averaged over launches at exit.
+struct WinTiming {
+  double sum[8] = {0}, n = 0, span = 0;
+  ~WinTiming() {
+    if (n == 0) return;
+    static const char* nm[8] = {"start(max)", "computed", "ticket", "fin_loaded", "fin_stored", "done_ticket",
+                                "published", "chunk_read"};
+    fprintf(stderr, "k_win_linearize timing over %.0f launches (us after the first wave start, max over waves):\n", n);
+    for (int i = 0; i < 8; ++i) fprintf(stderr, "  %-12s %8.2f\n", nm[i], sum[i] / n);
+    fprintf(stderr, "  span         %8.2f\n", span / n);
+  }
+};
+static WinTiming& win_timing() {
+  static WinTiming t;
+  return t;
+}
+bool win_timing_on() {
+  static const bool on = std::getenv("FMX_WIN_TIMING") != nullptr;
+  return on;
+}
+void win_timing_collect(fmx_ctx* c, uint32_t grid_chunks) {
+  WinStore& W = c->win;
+  FMX_HIP(hipStreamSynchronize(c->stream));
+  std::vector<uint64_t> h((size_t)grid_chunks * 8);
+  FMX_HIP(hipMemcpy(h.data(), W.dbg.p, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  uint64_t t0 = ~0ull, mx[8] = {0};
+  for (uint32_t ch = 0; ch < grid_chunks; ++ch)
+    if (h[ch * 8]) t0 = std::min(t0, h[ch * 8]);
+  if (t0 == ~0ull) return;
+  for (uint32_t ch = 0; ch < grid_chunks; ++ch)
+    for (int i = 0; i < 8; ++i)
+      if (h[ch * 8 + i]) mx[i] = std::max(mx[i], h[ch * 8 + i] - t0);
+  WinTiming& T = win_timing();
+  for (int i = 0; i < 8; ++i) T.sum[i] += mx[i] * 0.01;
+  T.span += *std::max_element(mx, mx + 7) * 0.01;
+  T.n += 1;
+  FMX_HIP(hipMemset(W.dbg.p, 0, h.size() * sizeof(uint64_t)));
+}
+
 // Launch k_win_linearize, wait for its word, copy npairs x 92 doubles out.
 void win_launch(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double* G_out,
                 double bytes) {
@@ -273,14 +353,27 @@ void win_launch(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses
   a.hostG = W.hG.d;
   a.seq = next_flag(c);
   a.flag = c->h_flag.d;
-  const uint32_t blocks = std::max<uint32_t>((grid_chunks + kWinWaves - 1) / kWinWaves, 1);
+  a.dbg = nullptr;
+  if (win_timing_on()) {
+    if (W.dbg.cap < (size_t)grid_chunks * 8) {
+      W.dbg.ensure((size_t)grid_chunks * 8);
+      FMX_HIP(hipMemset(W.dbg.p, 0, W.dbg.cap * sizeof(uint64_t)));
+    }
+    a.dbg = W.dbg.p;
+  }
+  const uint32_t blocks = std::max<uint32_t>(grid_chunks, 1);
   {
+    HostScope hs(12);
     ProfScope ps(c->prof, PROF_WINDOW, bytes, st);
     hipLaunchKernelGGL(k_win_linearize, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
     FMX_HIP(hipGetLastError());
   }
-  wait_flag(c, c->h_flag.p, a.seq);
+  {
+    HostScope hs(13);
+    wait_flag(c, c->h_flag.p, a.seq);
+  }
   if (G_out) std::memcpy(G_out, W.hG.p, (size_t)a.npairs * kWinG * sizeof(double));
+  if (a.dbg) win_timing_collect(c, grid_chunks);
 }
 
 }  // namespace
@@ -400,6 +493,8 @@ void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vecto
   std::map<uint64_t, uint32_t> slot;
   for (size_t k = 0; k < keys.size(); ++k) slot[keys[k]] = (uint32_t)k;
   if (keys.size() > 0xFFF) throw StatusError(FMX_E_INVAL, "window larger than 4095 poses");
+  if (W.tail_pl > 0xFFFFFFFFull || W.tail_pt > 0xFFFFFFFFull)
+    throw StatusError(FMX_E_OOM, "window store exceeds 2^32 rows");
   std::vector<Chunk> ch;
   std::vector<uint32_t> cr(prs.size() + 1);
   uint64_t rows_pl = 0, rows_pt = 0;
@@ -407,18 +502,16 @@ void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vecto
     const WinPair& p = prs[k];
     cr[k] = (uint32_t)ch.size();
     const uint32_t tag = (slot.at(p.i) << 8) | (slot.at(p.j) << 20);
-    for (uint32_t r = 0; r < p.pl_n; r += kWinPlaneRows)
+    for (uint32_t r = 0; r < p.pl_n; r += kPlaneChunk)
       ch.push_back(Chunk{0u | tag, (uint32_t)k, (uint32_t)(p.pl_off + r),
-                         (uint32_t)(p.pl_off + std::min<uint32_t>(p.pl_n, r + kWinPlaneRows))});
-    for (uint32_t r = 0; r < p.pt_n; r += kWinPointPairs)
+                         (uint32_t)(p.pl_off + std::min<uint32_t>(p.pl_n, r + kPlaneChunk))});
+    for (uint32_t r = 0; r < p.pt_n; r += kPointChunk)
       ch.push_back(Chunk{1u | tag, (uint32_t)k, (uint32_t)(p.pt_off + r),
-                         (uint32_t)(p.pt_off + std::min<uint32_t>(p.pt_n, r + kWinPointPairs))});
+                         (uint32_t)(p.pt_off + std::min<uint32_t>(p.pt_n, r + kPointChunk))});
     rows_pl += p.pl_n;
     rows_pt += p.pt_n;
   }
   cr[prs.size()] = (uint32_t)ch.size();
-  if (W.tail_pl > 0xFFFFFFFFull || W.tail_pt > 0xFFFFFFFFull)
-    throw StatusError(FMX_E_OOM, "window store exceeds 2^32 rows");
   const size_t nch = ch.size();
   W.chunks.ensure(nch + 1);
   W.chunk_range.ensure(prs.size() + 2);
