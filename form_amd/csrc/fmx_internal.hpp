@@ -178,8 +178,11 @@ struct Chunk {
   uint32_t end;
 };
 // Linearize chunk sizes: rows strided over the 64 lanes of one wave.
-constexpr int kPlaneChunk = 1024;  // plane rows per chunk (one 16-wave block of the window kernel)
-constexpr int kPointChunk = 1024;  // point pairs per chunk (three rows each)
+#ifndef FMX_WIN_ROWS
+#define FMX_WIN_ROWS 1024  // rows per window-kernel block (one 64-row step per wave)
+#endif
+constexpr int kPlaneChunk = FMX_WIN_ROWS;  // plane rows per chunk (one block of the window kernel)
+constexpr int kPointChunk = FMX_WIN_ROWS;  // point pairs per chunk (three rows each)
 
 // ---- smoothing-mode window store (window.hip)
 constexpr int kWinMaxArgPoses = 36;  // pose table by value up to this many poses

@@ -37,7 +37,8 @@ namespace {
 
 #include "factor_rows.hpp"
 
-constexpr int kWinWaves = 16;   // waves per block: one chunk of 16 x 64 rows per block
+constexpr int kWinWaves = kPlaneChunk / kWave;  // waves per block: one chunk, one 64-row step per wave
+static_assert(kPlaneChunk == kPointChunk && kPlaneChunk % kWave == 0 && kWinWaves <= 16, "window chunking");
 constexpr int kFinBatch = 16;   // chunk partials in flight per thread in the pair finisher
 constexpr int kWinLd = 96;      // doubles per chunk partial (91 used)
 constexpr int kWinG = 92;       // per pair: 91 G entries + error

@@ -10,6 +10,7 @@ for rep in $(seq 1 ${REPS:-3}); do
     name=${spec%%:*}; envs=${spec#*:}
     unset FMX_LIB FMX_DEVICE_LM FMX_MAP_SIDE FMX_MAP_INLINE
     case $name in prev*) export FMX_LIB=$PWD/form_amd/ab/libfmx_prev.so;; esac
+    [ -f form_amd/ab/libfmx_$name.so ] && export FMX_LIB=$PWD/form_amd/ab/libfmx_$name.so
     for kv in ${envs//,/ }; do export "$kv"; done
     timeout -k 10 400 python bench.py --workload ${WORKLOAD:-c4} --steps ${STEPS:-30} --warmup 10 --no-cpu-baseline > gpurun_out/abn_$name$rep.json 2> gpurun_out/abn_$name$rep.err || { tail -20 gpurun_out/abn_$name$rep.err; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/abn_$name$rep.json')); print('$name', d['value'], d['ms_per_step'], {k: v for k, v in d['kernels_ms_per_step'].items() if v})"

@@ -8,7 +8,7 @@ cat gpurun_out/bench.json
 if [ "${PROF:-1}" = "1" ]; then
   export TMPDIR=/tmp
   rm -rf gpurun_out/prof
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 30 --warmup 10 --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err || { tail -20 gpurun_out/prof.err; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --kernel-include-regex "fmx::" -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 30 --warmup 10 --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err || { tail -20 gpurun_out/prof.err; exit 1; }
   find gpurun_out/prof -name "*kernel_trace.csv" -delete
   find gpurun_out/prof -name "*stats.csv" | head -5
   cut -d, -f1-8 $(find gpurun_out/prof -name "*kernel_stats.csv" | head -1) | head -25

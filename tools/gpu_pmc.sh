@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-RX='k_match|k_extract_rows|k_normals|k_closest|k_fit|k_linearize|k_map_insert|k_map_scatter|k_insert'
+RX='k_match|k_extract_rows|k_normals|k_closest|k_fit|k_linearize|k_map_insert|k_map_scatter|k_insert|k_win_linearize|k_pair_scatter'
 i=0
 for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))

@@ -32,6 +32,8 @@ KMAP = {
     "k_map_insert": "map_build_insert",
     "k_map_scatter": "map_build_scatter",
     "k_insert": "insert",
+    "k_win_linearize": "window",  # smoothing mode: many pairs per launch
+    "k_pair_scatter": "pair_sort",
 }
 
 
