@@ -179,7 +179,7 @@ struct Chunk {
 };
 // Linearize chunk sizes: rows strided over the 64 lanes of one wave.
 #ifndef FMX_WIN_ROWS
-#define FMX_WIN_ROWS 1024  // rows per window-kernel block (one 64-row step per wave)
+#define FMX_WIN_ROWS 256  // rows per window-kernel block (one 64-row step per wave)
 #endif
 constexpr int kPlaneChunk = FMX_WIN_ROWS;  // plane rows per chunk (one block of the window kernel)
 constexpr int kPointChunk = FMX_WIN_ROWS;  // point pairs per chunk (three rows each)

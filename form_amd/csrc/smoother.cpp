@@ -4,6 +4,16 @@
 
 #include <algorithm>
 #include <cstring>
+#ifdef FMX_LM_PROF
+#include <chrono>
+namespace fmxh { double g_lm_prof[4]; }
+static double lmnow() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+#define LMP_BEGIN(i) const double _lmp##i = lmnow()
+#define LMP_END(i) fmxh::g_lm_prof[i] += lmnow() - _lmp##i
+#else
+#define LMP_BEGIN(i)
+#define LMP_END(i)
+#endif
 
 namespace fmxh {
 
@@ -84,8 +94,6 @@ double DenseSys::add_linf(const LinF& L, const std::vector<Pose>& xk) {
   return 0.5 * f;
 }
 
-namespace {
-
 // Cholesky solve of an n x n SPD system (row-major; factor U = L^T kept in the upper
 // triangle).  Right-looking, blocked by 6 (one pose): a 6-row panel is factored,
 // then each trailing row takes the panel's 6 updates with one load/store per element.
@@ -151,6 +159,8 @@ __attribute__((target_clones("avx2", "default"))) bool chol_solve(std::vector<do
   }
   return true;
 }
+
+namespace {
 
 // NonlinearFactorGraph::linearize at x into S; returns the graph error.  The
 // x-independent information blocks (prior H = I/sigma^2, the linear factors' G) are
@@ -267,7 +277,9 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
     for (;;) {
       Hd = H;
       for (int r = 0; r < D; ++r) Hd[(size_t)r * D + r] += lambda;
+      LMP_BEGIN(0);
       const bool ok = chol_solve(Hd, gg.data(), dx.data(), D);
+      LMP_END(0);
       bool success = false, stop = false;
       std::vector<Pose> xn;
       double nerr = err;
@@ -284,7 +296,9 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
         if (linChange >= 0) {
           xn.resize(R.x.size());
           for (size_t k = 0; k < R.x.size(); ++k) xn[k] = compose(R.x[k], expmap(&dx[6 * k]));
+          LMP_BEGIN(1);
           nerr = asmb.run(xn, Sn, Gn, R.lins);
+          LMP_END(1);
           const double costChange = err - nerr;
           if (linChange > DBL_EPSILON * oldLin) success = (costChange / linChange) > 1e-3;
           else success = true;

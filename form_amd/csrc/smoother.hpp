@@ -64,6 +64,10 @@ struct DenseSys {
   double add_linf(const LinF& L, const std::vector<Pose>& xk);            // x per L.keys
 };
 
+// Solve A x = g for SPD A (n x n row-major, overwritten by the factor); false if A is
+// not positive definite.
+bool chol_solve(std::vector<double>& A, const double* g, double* x, int n);
+
 // Schur complement eliminating the first nm columns of an n-column augmented system;
 // out = (n - nm + 1)^2.  False if the eliminated block is not positive definite.
 bool schur_marginal(const std::vector<double>& A, int n, int nm, std::vector<double>& out);

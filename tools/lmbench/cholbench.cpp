@@ -1,0 +1,18 @@
+#include <chrono>
+#include <cstdio>
+#include <vector>
+#include <random>
+#include <cstring>
+namespace fmxh { bool chol_solve(std::vector<double>& A, const double* g, double* x, int n); }
+static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+int main(int argc, char** argv) {
+  int n = argc > 1 ? atoi(argv[1]) : 72;
+  std::mt19937_64 rng(1); std::normal_distribution<double> nd;
+  std::vector<double> A((size_t)n*n, 0.0), g(n), x(n);
+  for (int r = 0; r < 2*n; ++r) { std::vector<double> a(n); for (auto& v : a) v = nd(rng); for (int i=0;i<n;++i) for (int j=0;j<n;++j) A[i*n+j]+=a[i]*a[j]; }
+  for (auto& v : g) v = nd(rng);
+  std::vector<double> B;
+  int reps = 20000; double t0 = now();
+  for (int r = 0; r < reps; ++r) { B = A; fmxh::chol_solve(B, g.data(), x.data(), n); }
+  printf("n=%d chol_solve %.2f us\n", n, (now()-t0)/reps*1e6);
+}
