@@ -270,6 +270,7 @@ struct fmx_ctx {
   fmx::DBuf<double4> m_pi, m_ni;
   fmx::DBuf<uint8_t> m_ins;
   fmx::DBuf<uint32_t> hist, hist_off;
+  fmx::DBuf<uint32_t> thist;  // tiled pair sort: per-(type, pair, tile) counts, self-resetting
   bool have_match = false;
 
   // ---- sorted correspondences (pair-major SoA) + chunk table

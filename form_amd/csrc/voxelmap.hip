@@ -176,7 +176,9 @@ struct MatchArgs {
   double max_d2, min_d2;
   uint32_t nq_pl, nq_pt, nb_pl, nb_pt;  // queries; planar / point blocks
   int K;
-  int sorted;  // 1: per-block pair histogram for the pair sort; 0: per-pair counts only
+  int sorted;  // 1: pair histogram for the pair sort; 0: per-pair counts only
+  int tiles;   // sorted: 1 = per-(pair, tile) counts scanned by the last block (k_pair_scatter_t)
+  uint32_t ntl_pl, ntl_pt;  // tiles (kTileBlocks match blocks each) per type
 };
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
@@ -187,6 +189,114 @@ struct MatchArgs {
 constexpr int kGroup = 8;  // lanes per query (16 made the kernel 15% faster but register_scan slower)
 constexpr int kQPB = 32;  // queries per block: 256 threads, so every block of a scan is resident at once
 constexpr int kMatchThreads = kQPB * kGroup;  // 256
+// Tiled pair sort: a tile = kTileBlocks match blocks of one type = 1024 queries, one
+// k_pair_scatter_t block; the match counts matches per (type, pair, tile).
+constexpr int kTileBlocks = 32;
+constexpr int kTileQ = kTileBlocks * kQPB;  // 1024
+constexpr int kTileMaxPairs = 256;          // LDS bound of the tiled path (wider windows: per-block path)
+
+// Outputs of the tiled pair sort's last-block pass (consumed by later launches).
+struct SortOut {
+  uint32_t* hist_off;     // [type][pair][tile] exclusive offsets (each type from 0)
+  uint32_t* pair_counts;  // [type][K]
+  uint32_t* pair_base;    // [type][K]
+  uint32_t* chunk_range;  // [K + 1]
+  Chunk* chunks;
+  uint32_t* n_chunks;
+};
+
+// Exclusive scan of one value per thread over a kMatchThreads block; total returned.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* ws, uint32_t& total) {
+  const uint32_t incl = wave_incl_scan(v);
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == 63) ws[w] = incl;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (int i = 0; i < kMatchThreads / kWave; ++i) {
+    if (i < w) off += ws[i];
+    tot += ws[i];
+  }
+  __syncthreads();
+  total = tot;
+  return off + incl - v;
+}
+
+// The match kernel's last block, tiled sort: scan the (type, pair, tile) counts
+// (read and reset), then what k_pair_base does: per-pair counts and first rows, host
+// copy of the counts, the linearize chunk table.  K <= kTileMaxPairs.
+__device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist, const SortOut& so,
+                               uint32_t* __restrict__ host_counts) {
+  __shared__ uint32_t ws[kMatchThreads / kWave];
+  __shared__ uint32_t s_pb[2][kTileMaxPairs + 1];  // per type: first row of pair k, [K] = total
+  __shared__ uint32_t s_cr[kTileMaxPairs + 1];
+  const int K = a.K;
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t ntl = t ? a.ntl_pt : a.ntl_pl;
+    const size_t base = t ? (size_t)K * a.ntl_pl : 0;
+    const uint32_t n = (uint32_t)K * ntl;
+    uint32_t carry = 0;
+    for (uint32_t s0 = 0; s0 < n; s0 += kMatchThreads) {
+      const uint32_t i = s0 + threadIdx.x;
+      const uint32_t v = i < n ? __hip_atomic_exchange(thist + base + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      uint32_t tot;
+      const uint32_t ex = block_excl_scan(v, ws, tot);
+      if (i < n) {
+        so.hist_off[base + i] = carry + ex;
+        if (i % ntl == 0) s_pb[t][i / ntl] = carry + ex;
+      }
+      carry += tot;
+    }
+    for (int k = threadIdx.x; k < K; k += kMatchThreads)
+      if (ntl == 0) s_pb[t][k] = 0;
+    if (threadIdx.x == 0) s_pb[t][K] = carry;
+  }
+  __syncthreads();
+  uint32_t carry = 0;
+  for (int k0 = 0; k0 < K; k0 += kMatchThreads) {
+    const int k = k0 + threadIdx.x;
+    uint32_t nch = 0;
+    if (k < K) {
+      const uint32_t b_pl = s_pb[0][k], npl = s_pb[0][k + 1] - b_pl;
+      const uint32_t b_pt = s_pb[1][k], npt = s_pb[1][k + 1] - b_pt;
+      so.pair_counts[k] = npl;
+      so.pair_counts[K + k] = npt;
+      host_store(host_counts + k, npl);  // mapped host memory
+      host_store(host_counts + K + k, npt);
+      so.pair_base[k] = b_pl;
+      so.pair_base[K + k] = b_pt;
+      nch = (npl + kPlaneChunk - 1) / kPlaneChunk + (npt + kPointChunk - 1) / kPointChunk;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(nch, ws, tot);
+    if (k < K) s_cr[k] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) s_cr[K] = carry;
+  __syncthreads();
+  for (int k = threadIdx.x; k <= K; k += kMatchThreads) so.chunk_range[k] = s_cr[k];
+  // descriptors: chunk -> pair by binary search over s_cr
+  for (uint32_t ci = threadIdx.x; ci < carry; ci += kMatchThreads) {
+    int lo = 0, hi = K - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_cr[mid] <= ci) lo = mid;
+      else hi = mid - 1;
+    }
+    const int k = lo;
+    const uint32_t j = ci - s_cr[k];
+    const uint32_t b_pl = s_pb[0][k], npl = s_pb[0][k + 1] - b_pl;
+    const uint32_t b_pt = s_pb[1][k], npt = s_pb[1][k + 1] - b_pt;
+    const uint32_t ncpl = (npl + kPlaneChunk - 1) / kPlaneChunk;
+    if (j < ncpl) {
+      const uint32_t r = j * kPlaneChunk;
+      so.chunks[ci] = Chunk{0, (uint32_t)k, b_pl + r, b_pl + min(npl, r + kPlaneChunk)};
+    } else {
+      const uint32_t r = (j - ncpl) * kPointChunk;
+      so.chunks[ci] = Chunk{1, (uint32_t)k, b_pt + r, b_pt + min(npt, r + kPointChunk)};
+    }
+  }
+  if (threadIdx.x == 0) *so.n_chunks = carry;
+}
 
 __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
@@ -198,7 +308,8 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
                                                          uint32_t* __restrict__ work, const IcpDev* __restrict__ icp,
                                                          uint32_t* __restrict__ mcnt, uint32_t* __restrict__ mticket,
                                                          uint32_t* __restrict__ host_counts,
-                                                         uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off) {
+                                                         uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off,
+                                                         uint32_t* __restrict__ thist, SortOut so) {
   extern __shared__ uint32_t s_hist[];  // [K]
 #ifdef FMX_MATCH_TIMING
   uint64_t mtime[6];
@@ -428,7 +539,16 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
     __hip_atomic_store(ins_blk + blockIdx.x, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int t = planar ? 0 : 1;
-  if (a.sorted) {
+  if (a.sorted && a.tiles) {
+    // per-(type, pair, tile) counts: agent-scope adds, scanned by the last block
+    const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.ntl_pl;
+    const uint32_t ntl = planar ? a.ntl_pl : a.ntl_pt;
+    const uint32_t tile = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) / kTileBlocks;
+    for (int k = threadIdx.x; k < a.K; k += kMatchThreads)
+      if (s_hist[k])
+        __hip_atomic_fetch_add(thist + hbase + (size_t)k * ntl + tile, s_hist[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+  } else if (a.sorted) {
     // pair-major layout [type][pair][block]: one exclusive scan gives every block's
     // destination offset (k_pair_base / k_pair_scatter)
     const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.nb_pl;
@@ -480,6 +600,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     }
     if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, carry);
   }
+  if (a.sorted && a.tiles) pair_sort_tail(a, thist, so, host_counts);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef FMX_MATCH_TIMING
   if (threadIdx.x == 0) printf("MLAST %d %llu\n", (int)blockIdx.x, (unsigned long long)wall_clock64());
@@ -614,6 +735,70 @@ __global__ __launch_bounds__(kQPB) void k_pair_scatter(uint32_t nq_pl, uint32_t 
                               : hist_off[npl_all + (size_t)pair * nb_pt + (blockIdx.x - nb_pl)] - tot_pl + rank;
   (void)pair_base;
   (void)t;
+  const size_t gq = planar ? qi : nq_pl + qi;
+  const double4 pi = m_pi[gq];
+  if (planar) {
+    const double4 ni = m_ni[qi];
+    const float4 pj = q_pl[qi];
+    c_pl[0 * ld_pl + dst] = pi.x; c_pl[1 * ld_pl + dst] = pi.y; c_pl[2 * ld_pl + dst] = pi.z;
+    c_pl[3 * ld_pl + dst] = ni.x; c_pl[4 * ld_pl + dst] = ni.y; c_pl[5 * ld_pl + dst] = ni.z;
+    c_pl[6 * ld_pl + dst] = (double)pj.x; c_pl[7 * ld_pl + dst] = (double)pj.y;
+    c_pl[8 * ld_pl + dst] = (double)pj.z;
+  } else {
+    const float4 pj = q_pt[qi];
+    c_pt[0 * ld_pt + dst] = pi.x; c_pt[1 * ld_pt + dst] = pi.y; c_pt[2 * ld_pt + dst] = pi.z;
+    c_pt[3 * ld_pt + dst] = (double)pj.x; c_pt[4 * ld_pt + dst] = (double)pj.y;
+    c_pt[5 * ld_pt + dst] = (double)pj.z;
+  }
+}
+
+// Tiled stable scatter: one 1024-thread block per tile (kTileBlocks match blocks of
+// one type); a query's row = its (pair, tile) offset + the matches of that pair in
+// earlier waves of the tile + its ballot rank in its wave.  Query order within a pair.
+__global__ __launch_bounds__(kTileQ) void k_pair_scatter_t(uint32_t nq_pl, uint32_t nq_pt, uint32_t ntl_pl,
+                                                         uint32_t ntl_pt, int K, const int32_t* __restrict__ m_pair,
+                                                         const double4* __restrict__ m_pi,
+                                                         const double4* __restrict__ m_ni,
+                                                         const float4* __restrict__ q_pl,
+                                                         const float4* __restrict__ q_pt,
+                                                         const uint32_t* __restrict__ hist_off,
+                                                         double* __restrict__ c_pl, size_t ld_pl,
+                                                         double* __restrict__ c_pt, size_t ld_pt) {
+  __shared__ uint32_t s_cnt[kTileQ / kWave][kTileMaxPairs];
+  const bool planar = blockIdx.x < ntl_pl;
+  const uint32_t tile = planar ? blockIdx.x : blockIdx.x - ntl_pl;
+  const uint32_t qi = tile * kTileQ + threadIdx.x;
+  const uint32_t nq = planar ? nq_pl : nq_pt;
+  const int w = threadIdx.x / kWave;
+  for (int i = threadIdx.x; i < (kTileQ / kWave) * K; i += kTileQ) s_cnt[i / K][i % K] = 0;
+  __syncthreads();
+  const int32_t pair = qi < nq ? m_pair[planar ? qi : nq_pl + qi] : -1;
+  uint32_t rank = 0;
+  bool todo = pair >= 0;
+  while (__ballot(todo)) {
+    const int lead = __ffsll((unsigned long long)__ballot(todo)) - 1;
+    const int v = __shfl(pair, lead, 64);
+    const uint64_t m = __ballot(todo && pair == v);
+    if (todo && pair == v) {
+      rank = __popcll(m & lanemask_lt());
+      todo = false;
+    }
+    if (lane_id() == lead) s_cnt[w][v] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += kTileQ) {  // per pair: exclusive scan over the waves
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < kTileQ / kWave; ++i) {
+      const uint32_t c = s_cnt[i][k];
+      s_cnt[i][k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  if (pair < 0) return;
+  const size_t hb = planar ? (size_t)pair * ntl_pl + tile : (size_t)K * ntl_pl + (size_t)pair * ntl_pt + tile;
+  const uint32_t dst = hist_off[hb] + s_cnt[w][pair] + rank;
   const size_t gq = planar ? qi : nq_pl + qi;
   const double4 pi = m_pi[gq];
   if (planar) {
@@ -812,6 +997,10 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   a.nb_pt = nb_pt;
   a.K = (int)c->K;
   a.sorted = sorted ? 1 : 0;
+  static const bool old_sort = std::getenv("FMX_PAIR_SORT_BLOCKS") != nullptr;  // A/B: per-block histogram path
+  a.tiles = sorted && !old_sort && c->K <= (uint32_t)kTileMaxPairs ? 1 : 0;
+  a.ntl_pl = (a.nb_pl + kTileBlocks - 1) / kTileBlocks;
+  a.ntl_pt = (nb_pt + kTileBlocks - 1) / kTileBlocks;
   const uint32_t nq = c->n_qpl + c->n_qpt;
   c->m_pair.ensure(nq + 1);
   c->m_d2.ensure(nq + 1);
@@ -839,6 +1028,9 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   ensure_zeroed(c->mticket, 1, st);
   c->ins_blk.ensure(nb + 1);
   c->ins_off.ensure(nb + 1);
+  ensure_zeroed(c->thist, (size_t)K * (a.ntl_pl + a.ntl_pt) + 1, st);
+  c->hist_off.ensure((size_t)K * (a.ntl_pl + a.ntl_pt) + 1);
+  const SortOut so{c->hist_off.p, c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p};
   c->h_counts.ensure(2 * (size_t)K + 4);
   auto view = [&](int t) {  // type t's table section over the shared record arrays
     VoxMap& M = c->map;
@@ -855,7 +1047,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
                        c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
                        c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, icp, c->mcnt.p, c->mticket.p, c->h_counts.d,
-                       c->ins_blk.p, c->ins_off.p);
+                       c->ins_blk.p, c->ins_off.p, c->thist.p, so);
     FMX_HIP(hipGetLastError());
   }
   // no queries: no launch, so zero the counts and insert totals the kernel would write
@@ -864,6 +1056,17 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->match_nb = nb;
   if (!sorted) {  // counts come from the match kernel's last block
     c->n_qo = nq;
+  } else if (a.tiles) {  // offsets, counts and chunk table from the match kernel's last block
+    ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
+    if (nb == 0) {  // no launch: an empty chunk table
+      FMX_HIP(hipMemsetAsync(c->n_chunks.p, 0, sizeof(uint32_t), st));
+      FMX_HIP(hipMemsetAsync(c->chunk_range.p, 0, (size_t)(a.K + 1) * sizeof(uint32_t), st));
+    } else if (c->K > 0) {
+      hipLaunchKernelGGL(k_pair_scatter_t, dim3(a.ntl_pl + a.ntl_pt), dim3(kTileQ), 0, st, c->n_qpl, c->n_qpt,
+                         a.ntl_pl, a.ntl_pt, a.K, c->m_pair.p, c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p,
+                         c->hist_off.p, c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
+      FMX_HIP(hipGetLastError());
+    }
   } else {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
     const size_t nh = (size_t)a.K * nb;

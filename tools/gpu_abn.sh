@@ -8,7 +8,7 @@ V=${VARIANTS:-"prev: new:"}
 for rep in $(seq 1 ${REPS:-3}); do
   for spec in $V; do
     name=${spec%%:*}; envs=${spec#*:}
-    unset FMX_LIB FMX_DEVICE_LM FMX_MAP_SIDE FMX_MAP_INLINE
+    for v in $(env | grep -o "^FMX_[A-Z_]*"); do unset $v; done
     case $name in prev*) export FMX_LIB=$PWD/form_amd/ab/libfmx_prev.so;; esac
     [ -f form_amd/ab/libfmx_$name.so ] && export FMX_LIB=$PWD/form_amd/ab/libfmx_$name.so
     for kv in ${envs//,/ }; do export "$kv"; done
@@ -20,7 +20,7 @@ python - <<'PY'
 import glob, json, re, collections
 best = collections.defaultdict(float)
 for f in glob.glob('gpurun_out/abn_*.json'):
-    name = re.match(r'gpurun_out/abn_(.*?)(\d+)\.json', f).group(1)
+    name = re.match(r'gpurun_out/abn_(.*)(\d)\.json', f).group(1)
     best[name] = max(best[name], json.load(open(f))['value'])
 print('BEST', dict(best))
 PY
