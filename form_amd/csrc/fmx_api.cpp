@@ -471,6 +471,24 @@ LinF fast_linear(const fmx_ctx::Est& e) {
   return L;
 }
 
+// The window graph's pair linearization: split (launch, host terms, wait) unless
+// FMX_LIN_SERIAL (A/B: launch and wait back to back, host terms after).
+template <class B, class E>
+void set_lin(WinGraph& g, B begin, E end) {
+  static const bool serial = std::getenv("FMX_LIN_SERIAL") != nullptr;
+  g.lin_pairs = [begin, end](const std::vector<Pose>& x, double* G) {
+    begin(x);
+    end(G);
+  };
+  if (serial) {
+    g.lin_begin = nullptr;
+    g.lin_end = nullptr;
+  } else {
+    g.lin_begin = begin;
+    g.lin_end = end;
+  }
+}
+
 // ICP loop (form.cpp:67-89) + optimize(false) (form.cpp:92-93) in smoothing mode:
 // every LM runs over all window poses; the current scan's FeatureFactors linearize
 // from the sorted match, the stored pairs from the window store (window.hip).
@@ -495,16 +513,22 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
     g.pairs.clear();
     for (uint32_t k = 0; k < c->K; ++k) g.pairs.push_back({slot.at(c->map_scans[k]), slot.at(j)});
     const int K = (int)c->K;
-    g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
+    // split form: launch, the host assembles the non-pair terms, then wait (smoother.hpp)
+    auto lin_begin = [&](const std::vector<Pose>& x) {
       table.resize(12 * ((size_t)K + 1));
       for (int k = 0; k < K; ++k) std::memcpy(&table[12 * k], x[slot.at(c->map_scans[k])].m, 12 * sizeof(double));
       std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
       HostScope hs(10);
-      win_linearize_current(c, table.data(), sigma, G);
+      win_linearize_current(c, table.data(), sigma, nullptr);
+    };
+    auto lin_end = [&](double* G) {
+      HostScope hs(10);
+      win_finish(c, G);
       match_counts_fetch(c, false);  // the match finished before the linearization
       for (int k = 0; k < K; ++k)
         if (c->cnt_pl[k] + c->cnt_pt[k] == 0) std::fill(G + (size_t)k * kPairG, G + (size_t)(k + 1) * kPairG, 0.0);
     };
+    set_lin(g, lin_begin, lin_end);
     HostScope* hs_lm = new HostScope(8);
     const WinLMResult R = window_lm(g, window_poses(e));
     delete hs_lm;
@@ -528,12 +552,17 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
   g.pairs.clear();
   for (auto& p : prs) g.pairs.push_back({slot.at(p.i), slot.at(p.j)});
   if (!prs.empty()) win_set_pairs(c, prs, keys);
-  g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
+  auto lin_begin = [&](const std::vector<Pose>& x) {
     table.resize(12 * keys.size());
     for (size_t k = 0; k < keys.size(); ++k) std::memcpy(&table[12 * k], x[k].m, 12 * sizeof(double));
     HostScope hs(10);
-    win_linearize_stored(c, table.data(), (int)keys.size(), sigma, G);
+    win_linearize_stored(c, table.data(), (int)keys.size(), sigma, nullptr);
   };
+  auto lin_end = [&](double* G) {
+    HostScope hs(10);
+    win_finish(c, G);
+  };
+  set_lin(g, lin_begin, lin_end);
   HostScope* hs_lm = new HostScope(9);
   const WinLMResult R = window_lm(g, window_poses(e));
   delete hs_lm;

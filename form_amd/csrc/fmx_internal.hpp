@@ -215,6 +215,9 @@ struct WinStore {
   DBuf<double> partials, dposes;
   DBuf<uint64_t> dbg;  // FMX_WIN_TIMING stamps
   DBuf<uint32_t> pticket, dticket;
+  bool pending = false;  // a k_win_linearize launched by win_start, not yet finished
+  uint32_t pending_seq = 0, pending_grid = 0;
+  int pending_np = 0;
   HBuf<double> hG, hposes;
   HBuf<uint32_t> hmeta;
 };
@@ -446,4 +449,5 @@ std::vector<WinPair> win_pairs(fmx_ctx* c);
 void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vector<uint64_t>& keys);
 void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out);
 void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
+void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* called with G_out = null
 }  // namespace fmx

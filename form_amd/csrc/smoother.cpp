@@ -2,7 +2,11 @@
 // Host code; built with -ffp-contract=off like the rest of the pose algebra.
 #include "smoother.hpp"
 
+#include <immintrin.h>
+
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #ifdef FMX_LM_PROF
 #include <chrono>
@@ -96,43 +100,150 @@ double DenseSys::add_linf(const LinF& L, const std::vector<Pose>& xk) {
 
 // Cholesky solve of an n x n SPD system (row-major; factor U = L^T kept in the upper
 // triangle).  Right-looking, blocked by 6 (one pose): a 6-row panel is factored,
-// then each trailing row takes the panel's 6 updates with one load/store per element.
-// Every element still receives its updates k = 0, 1, ... in order, so the factor is
-// bit-identical to the left-looking dot-product form (the oracle's).
-// AVX2 clone dispatched at run time: lanes hold independent elements and there is
-// no FMA contraction (-ffp-contract=off), so both clones round identically.
-__attribute__((target_clones("avx2", "default"))) bool chol_solve(std::vector<double>& A, const double* g, double* x,
-                                                                   int n) {
-  constexpr int B = 6;
-  double* a = A.data();
-  for (int kb = 0; kb < n; kb += B) {
-    const int ke = std::min(n, kb + B);
-    for (int k = kb; k < ke; ++k) {  // panel
-      double* __restrict Uk = a + (size_t)k * n;
-      const double s = Uk[k];
-      if (!(s > 0)) return false;
-      const double ukk = std::sqrt(s);
-      Uk[k] = ukk;
-      for (int m = k + 1; m < n; ++m) Uk[m] = Uk[m] / ukk;
-      for (int i = k + 1; i < ke; ++i) {
-        double* __restrict Ai = a + (size_t)i * n;
-        const double uki = Uk[i];
-        for (int m = i; m < n; ++m) Ai[m] -= uki * Uk[m];
-      }
+// then the trailing rows take the panel's 6 updates with one load/store per element
+// (every element still receives its updates k = 0, 1, ... in order).
+// Two paths, chosen once per process: on AVX2+FMA hosts the trailing update runs two
+// rows per pass (each panel load feeds both) with fused multiply-adds and the back
+// substitution keeps 4 partial sums; elsewhere the plain scalar form, which rounds
+// like the oracle's left-looking dot products.  Both are deterministic on a given
+// host; they differ from each other (and from the oracle) by FMA rounding only.
+namespace {
+
+constexpr int kCholB = 6;
+
+void chol_panel(double* a, int n, int kb, int ke, bool& ok) {
+  for (int k = kb; k < ke; ++k) {
+    double* __restrict Uk = a + (size_t)k * n;
+    const double s = Uk[k];
+    if (!(s > 0)) {
+      ok = false;
+      return;
     }
-    if (ke - kb == B) {  // trailing rows: 6 ordered updates per element
-      const double* U[B];
-      for (int t = 0; t < B; ++t) U[t] = a + (size_t)(kb + t) * n;
-      for (int i = ke; i < n; ++i) {
-        double* __restrict Ai = a + (size_t)i * n;
-        double u[B];
-        for (int t = 0; t < B; ++t) u[t] = U[t][i];
-        for (int m = i; m < n; ++m) {
-          double v = Ai[m];
-          for (int t = 0; t < B; ++t) v -= u[t] * U[t][m];
-          Ai[m] = v;
-        }
+    const double ukk = std::sqrt(s);
+    Uk[k] = ukk;
+    for (int m = k + 1; m < n; ++m) Uk[m] = Uk[m] / ukk;
+    for (int i = k + 1; i < ke; ++i) {
+      double* __restrict Ai = a + (size_t)i * n;
+      const double uki = Uk[i];
+      for (int m = i; m < n; ++m) Ai[m] -= uki * Uk[m];
+    }
+  }
+}
+// FMA form of the panel: scale by the reciprocal, fused updates.
+__attribute__((target("avx2,fma"))) void chol_panel_fma(double* a, int n, int kb, int ke, bool& ok) {
+  for (int k = kb; k < ke; ++k) {
+    double* __restrict Uk = a + (size_t)k * n;
+    const double s = Uk[k];
+    if (!(s > 0)) {
+      ok = false;
+      return;
+    }
+    const double ukk = std::sqrt(s), r = 1.0 / ukk;
+    Uk[k] = ukk;
+    for (int m = k + 1; m < n; ++m) Uk[m] = Uk[m] * r;
+    for (int i = k + 1; i < ke; ++i) {
+      double* __restrict Ai = a + (size_t)i * n;
+      const double uki = Uk[i];
+      for (int m = i; m < n; ++m) Ai[m] = std::fma(-uki, Uk[m], Ai[m]);
+    }
+  }
+}
+
+void chol_trail_plain(double* a, int n, int kb, int ke) {
+  const double* U[kCholB];
+  for (int t = 0; t < kCholB; ++t) U[t] = a + (size_t)(kb + t) * n;
+  for (int i = ke; i < n; ++i) {
+    double* __restrict Ai = a + (size_t)i * n;
+    double u[kCholB];
+    for (int t = 0; t < kCholB; ++t) u[t] = U[t][i];
+    for (int m = i; m < n; ++m) {
+      double v = Ai[m];
+      for (int t = 0; t < kCholB; ++t) v -= u[t] * U[t][m];
+      Ai[m] = v;
+    }
+  }
+}
+
+__attribute__((target("avx2,fma"))) void chol_trail_fma(double* a, int n, int kb, int ke) {
+  const double* U[kCholB];
+  for (int t = 0; t < kCholB; ++t) U[t] = a + (size_t)(kb + t) * n;
+  int i = ke;
+  for (; i + 2 <= n; i += 2) {
+    double* __restrict A0 = a + (size_t)i * n;
+    double* __restrict A1 = A0 + n;
+    double u0[kCholB], u1[kCholB];
+    __m256d b0[kCholB], b1[kCholB];
+    for (int t = 0; t < kCholB; ++t) {
+      u0[t] = U[t][i];
+      u1[t] = U[t][i + 1];
+      b0[t] = _mm256_set1_pd(u0[t]);
+      b1[t] = _mm256_set1_pd(u1[t]);
+    }
+    {
+      double v = A0[i];
+      for (int t = 0; t < kCholB; ++t) v = std::fma(-u0[t], U[t][i], v);
+      A0[i] = v;
+    }
+    int m = i + 1;
+    for (; m + 4 <= n; m += 4) {
+      __m256d x0 = _mm256_loadu_pd(A0 + m), x1 = _mm256_loadu_pd(A1 + m);
+      for (int t = 0; t < kCholB; ++t) {
+        const __m256d uu = _mm256_loadu_pd(U[t] + m);
+        x0 = _mm256_fnmadd_pd(b0[t], uu, x0);
+        x1 = _mm256_fnmadd_pd(b1[t], uu, x1);
       }
+      _mm256_storeu_pd(A0 + m, x0);
+      _mm256_storeu_pd(A1 + m, x1);
+    }
+    for (; m < n; ++m) {
+      double v0 = A0[m], v1 = A1[m];
+      for (int t = 0; t < kCholB; ++t) {
+        v0 = std::fma(-u0[t], U[t][m], v0);
+        v1 = std::fma(-u1[t], U[t][m], v1);
+      }
+      A0[m] = v0;
+      A1[m] = v1;
+    }
+  }
+  for (; i < n; ++i) {
+    double* __restrict Ai = a + (size_t)i * n;
+    for (int m = i; m < n; ++m) {
+      double v = Ai[m];
+      for (int t = 0; t < kCholB; ++t) v = std::fma(-U[t][i], U[t][m], v);
+      Ai[m] = v;
+    }
+  }
+}
+
+__attribute__((target("avx2,fma"))) void chol_back_fma(const double* a, int n, const double* y, double* x) {
+  for (int i = n - 1; i >= 0; --i) {  // U x = y
+    const double* Ui = a + (size_t)i * n;
+    __m256d acc = _mm256_setzero_pd();
+    int k = i + 1;
+    for (; k + 4 <= n; k += 4) acc = _mm256_fmadd_pd(_mm256_loadu_pd(Ui + k), _mm256_loadu_pd(x + k), acc);
+    double p[4];
+    _mm256_storeu_pd(p, acc);
+    double s = y[i] - ((p[0] + p[1]) + (p[2] + p[3]));
+    for (; k < n; ++k) s = std::fma(-Ui[k], x[k], s);
+    x[i] = s / Ui[i];
+  }
+}
+
+}  // namespace
+
+bool chol_solve(std::vector<double>& A, const double* g, double* x, int n) {
+  static const bool fma = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma") &&
+                          std::getenv("FMX_CHOL_PLAIN") == nullptr;
+  double* a = A.data();
+  for (int kb = 0; kb < n; kb += kCholB) {
+    const int ke = std::min(n, kb + kCholB);
+    bool ok = true;
+    if (fma) chol_panel_fma(a, n, kb, ke, ok);
+    else chol_panel(a, n, kb, ke, ok);
+    if (!ok) return false;
+    if (ke - kb == kCholB) {
+      if (fma) chol_trail_fma(a, n, kb, ke);
+      else chol_trail_plain(a, n, kb, ke);
     } else {
       for (int k = kb; k < ke; ++k) {
         const double* Uk = a + (size_t)k * n;
@@ -150,6 +261,10 @@ __attribute__((target_clones("avx2", "default"))) bool chol_solve(std::vector<do
     y[k] = y[k] / Uk[k];
     const double yk = y[k];
     for (int m = k + 1; m < n; ++m) y[m] -= Uk[m] * yk;
+  }
+  if (fma) {
+    chol_back_fma(a, n, y.data(), x);
+    return true;
   }
   for (int i = n - 1; i >= 0; --i) {  // back: U x = y
     const double* Ui = a + (size_t)i * n;
@@ -194,7 +309,9 @@ struct Assembler {
     if (S.D != base.D || S.keys != base.keys) S = base;
     else std::memcpy(S.A.data(), base.A.data(), base.A.size() * sizeof(double));
     G.assign(g.pairs.size() * kPairG, 0.0);
-    if (!g.pairs.empty()) {
+    const bool split = !g.pairs.empty() && g.lin_begin;
+    if (split) g.lin_begin(x);  // device work overlaps the host terms below
+    else if (!g.pairs.empty()) {
       g.lin_pairs(x, G.data());
       ++lins;
     }
@@ -242,6 +359,10 @@ struct Assembler {
       const double f = I[(size_t)n * m + n] + (dGd - 2.0 * dg);
       S.at(D, D) += f;
       err += 0.5 * f;
+    }
+    if (split) {
+      g.lin_end(G.data());
+      ++lins;
     }
     for (size_t p = 0; p < g.pairs.size(); ++p) {
       S.add_pair(g.pairs[p].first, g.pairs[p].second, &G[p * kPairG]);

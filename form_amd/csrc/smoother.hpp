@@ -40,6 +40,11 @@ struct WinGraph {
   std::vector<std::pair<int, int>> pairs;  // pair slot -> (key slot i, key slot j)
   // DenseFactor::linearize of every pair at x (key-slot order): G[npairs][kPairG]
   std::function<void(const std::vector<Pose>& x, double* G)> lin_pairs;
+  // Optional split form (used when lin_begin is set): lin_begin(x) starts the device
+  // linearization, the host assembles the x-dependent non-pair terms, lin_end(G)
+  // waits for it and fills G.
+  std::function<void(const std::vector<Pose>& x)> lin_begin;
+  std::function<void(double* G)> lin_end;
 };
 
 struct WinLMResult {

@@ -327,10 +327,11 @@ void win_timing_collect(fmx_ctx* c, uint32_t grid_chunks) {
   FMX_HIP(hipMemset(W.dbg.p, 0, h.size() * sizeof(uint64_t)));
 }
 
-// Launch k_win_linearize, wait for its word, copy npairs x 92 doubles out.
-void win_launch(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double* G_out,
-                double bytes) {
+// Launch k_win_linearize (win_start); wait for its word and copy npairs x 92 doubles
+// out (win_finish).  The host assembles the x-dependent non-pair terms in between.
+void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double bytes) {
   WinStore& W = c->win;
+  if (W.pending) win_finish(c, nullptr);  // an abandoned one (error path): drain it first
   hipStream_t st = c->stream;
   WinPoses wp;
   if (nposes <= kWinMaxArgPoses) {
@@ -369,14 +370,27 @@ void win_launch(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses
     hipLaunchKernelGGL(k_win_linearize, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
     FMX_HIP(hipGetLastError());
   }
-  {
-    HostScope hs(13);
-    wait_flag(c, c->h_flag.p, a.seq);
-  }
-  if (G_out) std::memcpy(G_out, W.hG.p, (size_t)a.npairs * kWinG * sizeof(double));
-  if (a.dbg) win_timing_collect(c, grid_chunks);
+  W.pending = true;
+  W.pending_seq = a.seq;
+  W.pending_np = a.npairs;
+  W.pending_grid = grid_chunks;
 }
 
+}  // namespace
+
+void win_finish(fmx_ctx* c, double* G_out) {
+  WinStore& W = c->win;
+  if (!W.pending) throw StatusError(FMX_E_STATE, "win_finish: no window linearization in flight");
+  W.pending = false;
+  {
+    HostScope hs(13);
+    wait_flag(c, c->h_flag.p, W.pending_seq);
+  }
+  if (G_out) std::memcpy(G_out, W.hG.p, (size_t)W.pending_np * kWinG * sizeof(double));
+  if (win_timing_on()) win_timing_collect(c, W.pending_grid);
+}
+
+namespace {
 }  // namespace
 
 // ---------------------------------------------------------------- store maintenance
@@ -531,7 +545,8 @@ void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vecto
 }
 
 // DenseFactor::linearize of every pair of the last win_set_pairs at poses[key slot]:
-// G_out[npairs][92] = 91 packed-upper 13 x 13 entries + error.
+// G_out[npairs][92] = 91 packed-upper 13 x 13 entries + error.  G_out null: launch
+// only; win_finish(c, G_out) waits and copies.
 void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out) {
   WinStore& W = c->win;
   if (!W.chunks_valid) throw StatusError(FMX_E_STATE, "win_linearize_stored: pair set not uploaded");
@@ -547,7 +562,8 @@ void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double si
   a.ld_pt = W.cap_pt;
   a.implicit_j = -1;
   a.inv = 1.0 / sigma;
-  win_launch(c, a, W.nch, poses, nposes, G_out, 72.0 * W.rows_pl + 48.0 * W.rows_pt + 8.0 * kWinG * W.npairs);
+  win_start(c, a, W.nch, poses, nposes, 72.0 * W.rows_pl + 48.0 * W.rows_pt + 8.0 * kWinG * W.npairs);
+  if (G_out) win_finish(c, G_out);
 }
 
 // Same for the current scan's K pairs straight from the sorted match (device-built
@@ -566,8 +582,8 @@ void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double
   a.implicit_j = (int)c->K;
   a.inv = 1.0 / sigma;
   // exact row counts arrive with the match counts; the byte model uses the last known
-  win_launch(c, a, c->max_chunks, poses, (int)c->K + 1, G_out,
-             72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K);
+  win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K);
+  if (G_out) win_finish(c, G_out);
 }
 
 }  // namespace fmx
