@@ -63,7 +63,7 @@ typedef struct fmx_params {
   double new_pose_threshold;
   uint32_t max_num_rematches;
   double planar_constraint_sigma;  /* ConstraintManager::Params, constraints.hpp:54-70 */
-  int32_t disable_smoothing;       /* host adapter implements the single-pose mode */
+  int32_t disable_smoothing;       /* 0 (default): window smoothing; 1: single-pose ablation */
   int64_t max_num_keyscans;        /* KeyScanner::Params, keyscanner.hpp:55-64 */
   int64_t max_steps_unused_keyscan;
   uint32_t max_num_recent_scans;
@@ -164,10 +164,13 @@ fmx_status fmx_error(fmx_ctx* ctx, const double* poses_i34, const double* poses_
                      double sigma, double* err);
 
 /* ---------------- host adapter: Estimator::register_scan -------------------
- * form::Estimator::register_scan (form/form.hpp:82-83, form.cpp:40-114) with the
- * smoother in single-pose mode (ConstraintManager disable_smoothing path,
- * constraints.cpp:103-111, 235-250): predict, extract, map build, ICP loop
- * (match + LM), final LM, insert_matches, keyscan selection, marginalization. */
+ * form::Estimator::register_scan (form/form.hpp:82-83, form.cpp:40-114): predict,
+ * extract, map build, ICP loop (match + LM), final LM, insert_matches, keyscan
+ * selection, marginalization.  The smoother runs in ConstraintManager's default
+ * smoothing mode (LM over every window pose, constraints.cpp:103-118, 252-308,
+ * marginal LinearContainerFactors, constraints.cpp:120-203) or, with
+ * params.disable_smoothing, in the single-pose ablation (constraints.cpp:103-111,
+ * 235-250).  Every FeatureFactor linearization runs on the device. */
 fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, int src_on_device,
                              fmx_feature_counts* out);
 /* Estimator::current_lidar_estimate (form/form.hpp:79). */
