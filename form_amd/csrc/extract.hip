@@ -1432,28 +1432,28 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
                        c->h_u32.d, c->h_flag.d, seq);
   }
   FMX_HIP(hipGetLastError());
-  // totals (planar-with-normal, points, selected) were written to mapped host memory;
-  // the caller may queue independent work (register_scan: the map build on the side
-  // stream) before the host blocks on them
-  if (while_waiting) while_waiting();
-  wait_flag(c, c->h_flag.p, seq);
-  const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
-  // sized for the worst case, not the totals just read: a wrong total can then never
-  // turn into an out-of-bounds write
+  // k_write_features needs only the device row offsets, and its outputs are sized for
+  // the worst case (so a wrong total can never become an out-of-bounds write): it is
+  // queued before the host blocks on the totals (written to mapped host memory by
+  // k_row_scan), and so is any independent work of the caller (register_scan: the
+  // map build on the side stream)
   const size_t max_pl = (size_t)R * a.cap_pl, max_pt = (size_t)R * a.cap_pt;
-  if (npl > max_pl || npt > max_pt || nsel > max_pl) throw StatusError(FMX_E_HIP, "implausible feature totals");
   c->q_pl_pos.ensure(max_pl + 1);
   c->q_pl_nrm.ensure(max_pl + 1);
   c->q_pl_idx.ensure(max_pl + 1);
   c->q_pt_pos.ensure(max_pt + 1);
   c->q_pt_idx.ensure(max_pt + 1);
   {
-    ProfScope ps(c->prof, PROF_COMPACT, 32.0 * npl + 16.0 * npt, st);
+    ProfScope ps(c->prof, PROF_COMPACT, 32.0 * c->n_qpl + 16.0 * c->n_qpt, st);  // byte model: last totals
     hipLaunchKernelGGL(k_write_features, dim3(R), dim3(256), 0, st, d_scan, a, c->row_counts.p, c->row_off.p,
                        c->sel_slots.p, c->pt_slots.p, c->nrm_slots.p, c->q_pl_pos.p, c->q_pl_nrm.p,
                        c->q_pl_idx.p, c->q_pt_pos.p, c->q_pt_idx.p);
   }
   FMX_HIP(hipGetLastError());
+  if (while_waiting) while_waiting();
+  wait_flag(c, c->h_flag.p, seq);
+  const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
+  if (npl > max_pl || npt > max_pt || nsel > max_pl) throw StatusError(FMX_E_HIP, "implausible feature totals");
   c->n_qpl = npl;
   c->n_qpt = npt;
   c->n_sel = nsel;

@@ -938,7 +938,7 @@ void fmx_destroy(fmx_ctx* c) {
   {
     auto& W = c->win;
     for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }
-    W.chunks.release(); W.chunk_range.release(); W.partials.release(); W.dposes.release();
+    W.meta.release(); if (W.meta_ev) (void)hipEventDestroy(W.meta_ev); W.partials.release(); W.dposes.release();
     W.pticket.release(); W.dticket.release(); W.dbg.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);

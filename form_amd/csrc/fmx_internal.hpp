@@ -205,8 +205,11 @@ struct WinStore {
   uint64_t cap_pl = 0, cap_pt = 0, tail_pl = 0, tail_pt = 0;
   std::map<uint64_t, WinSeg> segs;
   // uploaded pair set (win_set_pairs)
-  DBuf<Chunk> chunks;
-  DBuf<uint32_t> chunk_range;
+  DBuf<uint32_t> meta;  // [chunks (4 words each)][chunk_range]
+  const Chunk* chunks_p = nullptr;
+  const uint32_t* chunk_range_p = nullptr;
+  hipEvent_t meta_ev = nullptr;  // the last upload from hmeta
+  bool meta_ev_pending = false;
   uint32_t nch = 0;
   int npairs = 0;
   uint64_t rows_pl = 0, rows_pt = 0;

@@ -528,15 +528,20 @@ void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vecto
   }
   cr[prs.size()] = (uint32_t)ch.size();
   const size_t nch = ch.size();
-  W.chunks.ensure(nch + 1);
-  W.chunk_range.ensure(prs.size() + 2);
-  W.hmeta.ensure(4 * nch + prs.size() + 2);
+  // one upload: [chunks (4 words each)][chunk_range]; the pinned staging buffer is
+  // reused only after the previous upload's event (no stream synchronization)
+  const size_t words = 4 * nch + cr.size();
+  if (W.meta_ev_pending) FMX_HIP(hipEventSynchronize(W.meta_ev));
+  W.meta.ensure(words + 4);
+  W.hmeta.ensure(words + 4);
   std::memcpy(W.hmeta.p, ch.data(), nch * sizeof(Chunk));
   std::memcpy(W.hmeta.p + 4 * nch, cr.data(), cr.size() * sizeof(uint32_t));
-  if (nch) FMX_HIP(hipMemcpyAsync(W.chunks.p, W.hmeta.p, nch * sizeof(Chunk), hipMemcpyHostToDevice, st));
-  FMX_HIP(hipMemcpyAsync(W.chunk_range.p, W.hmeta.p + 4 * nch, cr.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                         st));
-  FMX_HIP(hipStreamSynchronize(st));  // the staging buffer is reused by the next upload
+  FMX_HIP(hipMemcpyAsync(W.meta.p, W.hmeta.p, words * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (!W.meta_ev) FMX_HIP(hipEventCreateWithFlags(&W.meta_ev, hipEventDisableTiming));
+  FMX_HIP(hipEventRecord(W.meta_ev, st));
+  W.meta_ev_pending = true;
+  W.chunks_p = reinterpret_cast<const Chunk*>(W.meta.p);
+  W.chunk_range_p = W.meta.p + 4 * nch;
   W.nch = (uint32_t)nch;
   W.npairs = (int)prs.size();
   W.rows_pl = rows_pl;
@@ -551,10 +556,10 @@ void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double si
   WinStore& W = c->win;
   if (!W.chunks_valid) throw StatusError(FMX_E_STATE, "win_linearize_stored: pair set not uploaded");
   WinArgs a{};
-  a.chunks = W.chunks.p;
+  a.chunks = W.chunks_p;
   a.n_chunks = nullptr;
   a.n_chunks_host = W.nch;
-  a.chunk_range = W.chunk_range.p;
+  a.chunk_range = W.chunk_range_p;
   a.npairs = W.npairs;
   a.c_pl = W.pl[W.cur].p;
   a.ld_pl = W.cap_pl;
