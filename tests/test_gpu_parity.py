@@ -177,3 +177,70 @@ def test_ate_gpu_vs_oracle(fmx_mod, oracle):
     a_gpu, a_cpu = metrics.ate_rmse(gpu, gt), metrics.ate_rmse(cpu, gt)
     assert abs(a_gpu - a_cpu) < 1e-3, (a_gpu, a_cpu)
     assert a_gpu < 0.05, a_gpu  # the registration tracks the synthetic trajectory
+
+
+def _xf(T, p):
+    return p @ T[:, :3].T + T[:, 3]
+
+
+def _inv(T):
+    R = T[:, :3].T
+    return np.hstack([R, -(R @ T[:, 3])[:, None]])
+
+
+@pytest.mark.parametrize("K", [5, 300])
+def test_match_sort_then_linearize(fmx_mod, oracle, K):
+    """The sorted match (fmx_match: pair-major correspondences + chunk table) feeds
+    fmx_linearize: per-pair counts equal the query-order assignments, and every pair's
+    13x13 information equals the oracle's over that pair's rows in query order.  K = 5
+    runs the tiled sort (per-(pair, tile) counts scanned by the match's last block);
+    K = 300 > 256 the per-block histogram path."""
+    rng = np.random.default_rng(11 + K)
+    p = synth.default_params(synth.GEOMETRIES["tiny"])
+    ctx = _ctx(fmx_mod, p)
+    n_pl, n_pt = max(9000 // K, 4), max(3000 // K, 2)
+    poses = [perturb(np.eye(4)[:3], rng, 0.05, 1.0) for _ in range(K)]
+    world_pl, world_pt = [], []
+    for k in range(K):
+        wp = rng.uniform([-10, -10, -1.5], [10, 10, 1.5], (n_pl, 3))
+        wn = rng.normal(size=(n_pl, 3))
+        wn /= np.linalg.norm(wn, axis=1, keepdims=True)
+        wt = rng.uniform([-10, -10, -1.5], [10, 10, 1.5], (n_pt, 3))
+        Ti = _inv(poses[k])
+        pl = np.hstack([_xf(Ti, wp), wn @ Ti[:, :3].T]).astype(np.float32)
+        ctx.keypoints_add(k, pl, _xf(Ti, wt).astype(np.float32))
+        world_pl.append(wp)
+        world_pt.append(wt)
+    ctx.map_build(np.arange(K), np.stack(poses), 0.8)
+    Tj = perturb(np.eye(4)[:3], rng, 0.02, 0.5)
+    Tjinv = _inv(Tj)
+    qw_pl = np.concatenate(world_pl)[rng.choice(K * n_pl, 2500, replace=False)] + rng.normal(scale=0.05, size=(2500, 3))
+    qw_pt = np.concatenate(world_pt)[rng.choice(K * n_pt, 700, replace=False)] + rng.normal(scale=0.05, size=(700, 3))
+    q_pl = np.hstack([_xf(Tjinv, qw_pl), np.tile([0, 0, 1.0], (2500, 1))]).astype(np.float32)
+    q_pt = _xf(Tjinv, qw_pt).astype(np.float32)
+    ctx.set_queries(q_pl, q_pt, K)
+    cpl, cpt = ctx.match(Tj, 0.8)
+    got = ctx.match_download()
+    pair = got["pair"]
+    npl = len(q_pl)
+    assert (pair >= 0).sum() > 1000
+    assert np.array_equal(cpl, np.bincount(pair[:npl][pair[:npl] >= 0], minlength=K))
+    assert np.array_equal(cpt, np.bincount(pair[npl:][pair[npl:] >= 0], minlength=K))
+    # the oracle over the same rows, pair-major, query order within a pair
+    ppi, pni, ppj, tpi, tpj = [], [], [], [], []
+    for k in range(K):
+        m = pair[:npl] == k
+        ppi.append(got["pi"][:npl][m])
+        pni.append(got["ni"][m])
+        ppj.append(q_pl[m, :3].astype(np.float64))
+        mt = pair[npl:] == k
+        tpi.append(got["pi"][npl:][mt])
+        tpj.append(q_pt[mt].astype(np.float64))
+    Pi = np.stack(poses).reshape(K, 12)
+    Pj = np.tile(Tj.reshape(12), (K, 1))
+    G, err = ctx.linearize(Pi, Pj, 0.1, False)
+    Gr, er = oracle.linearize(cpl, np.concatenate(ppi), np.concatenate(pni), np.concatenate(ppj), cpt,
+                              np.concatenate(tpi), np.concatenate(tpj), Pi, Pj, 0.1, False)
+    scale = np.abs(Gr).max(axis=1, keepdims=True) + 1e-300
+    assert np.all(np.abs(G - Gr) <= 1e-10 * scale)
+    assert np.allclose(err, er, rtol=1e-10, atol=0)
