@@ -185,10 +185,13 @@ constexpr int kPlaneChunk = FMX_WIN_ROWS;  // plane rows per chunk (one block of
 constexpr int kPointChunk = FMX_WIN_ROWS;  // point pairs per chunk (three rows each)
 
 // ---- smoothing-mode window store (window.hip)
-constexpr int kWinMaxArgPoses = 36;  // pose table by value up to this many poses
-struct WinPoses {
-  double m[kWinMaxArgPoses][12];
+constexpr int kWinMaxArgPoses = 36;    // pose table by value up to this many poses
+constexpr int kWinSmallArgPoses = 16;  // ... in a smaller kernel-argument block up to this many
+template <int N>
+struct WinPosesN {
+  double m[N][12];
 };
+using WinPoses = WinPosesN<kWinMaxArgPoses>;
 struct WinPair {  // one FeatureFactor(X(i), X(j))'s rows in the arena
   uint64_t i, j;
   uint64_t pl_off, pt_off;

@@ -388,16 +388,16 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
   if (err <= 0.0) return R;
   double lambda = 1e-5;
   const int D = S.D;
-  std::vector<double> H((size_t)D * D), gg(D), Hd, dx(D);
+  std::vector<double> gg(D), Hd((size_t)D * D), dx(D);
   auto iterate = [&]() {
-    for (int r = 0; r < D; ++r) {
-      std::memcpy(&H[(size_t)r * D], &S.A[(size_t)r * (D + 1)], D * sizeof(double));
-      gg[r] = S.at(r, D);
-    }
+    // H is the leading D x D block of S.A (row stride D + 1), read in place
+    for (int r = 0; r < D; ++r) gg[r] = S.at(r, D);
     const double cc = S.at(D, D), oldLin = 0.5 * cc;
     for (;;) {
-      Hd = H;
-      for (int r = 0; r < D; ++r) Hd[(size_t)r * D + r] += lambda;
+      for (int r = 0; r < D; ++r) {
+        std::memcpy(&Hd[(size_t)r * D], &S.A[(size_t)r * (D + 1)], D * sizeof(double));
+        Hd[(size_t)r * D + r] += lambda;
+      }
       LMP_BEGIN(0);
       const bool ok = chol_solve(Hd, gg.data(), dx.data(), D);
       LMP_END(0);
@@ -408,7 +408,7 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
         double dHd = 0, dg = 0;
         for (int r = 0; r < D; ++r) {
           double h = 0;
-          const double* Hr = &H[(size_t)r * D];
+          const double* Hr = &S.A[(size_t)r * (D + 1)];
           for (int c = 0; c < D; ++c) h += Hr[c] * dx[c];
           dHd += dx[r] * h;
           dg += dx[r] * gg[r];

@@ -116,7 +116,9 @@ __device__ __forceinline__ void stage_and_mfma(double* __restrict__ rows /* this
 // block writes G to pinned host memory itself; more: block partials (agent-scope
 // stores), a per-pair ticket, the pair's last chunk sums the partials in chunk order.
 // Then a ticket over the pairs with rows lets the last finisher publish the word.
-__global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, WinPoses wp) {
+// NP: by-value pose capacity (kernel-argument bytes: a smaller block launches faster)
+template <int NP>
+__global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, WinPosesN<NP> wp) {
   __shared__ double s_rows[kWinWaves][kWave * kLdsStride];
   __shared__ double s_g[kWinWaves][92];
   __shared__ uint32_t s_t;
@@ -334,7 +336,11 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
   if (W.pending) win_finish(c, nullptr);  // an abandoned one (error path): drain it first
   hipStream_t st = c->stream;
   WinPoses wp;
-  if (nposes <= kWinMaxArgPoses) {
+  WinPosesN<kWinSmallArgPoses> wps;
+  if (nposes <= kWinSmallArgPoses) {
+    std::memcpy(wps.m, poses, (size_t)nposes * 12 * sizeof(double));
+    a.dposes = nullptr;
+  } else if (nposes <= kWinMaxArgPoses) {
     std::memcpy(wp.m, poses, (size_t)nposes * 12 * sizeof(double));
     a.dposes = nullptr;
   } else {
@@ -367,7 +373,10 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
   {
     HostScope hs(12);
     ProfScope ps(c->prof, PROF_WINDOW, bytes, st);
-    hipLaunchKernelGGL(k_win_linearize, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
+    if (nposes <= kWinSmallArgPoses)
+      hipLaunchKernelGGL(k_win_linearize<kWinSmallArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wps);
+    else
+      hipLaunchKernelGGL(k_win_linearize<kWinMaxArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
     FMX_HIP(hipGetLastError());
   }
   W.pending = true;
