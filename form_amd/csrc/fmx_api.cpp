@@ -923,7 +923,7 @@ void fmx_destroy(fmx_ctx* c) {
   }
   {
     auto& M = c->map;
-    M.table.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
+    M.table.release(); M.bcnt.release(); M.bcur.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
     M.rseg.release(); M.pos.release(); M.nrm.release(); M.seg.release(); M.rid.release();
   }
   c->h_mapposes.release(); c->map_blob.release();

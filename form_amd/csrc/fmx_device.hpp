@@ -246,10 +246,27 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {  // splitmix64 finalizer
 }
 
 // Hash slot: {key, first record, record count}; 16 B, one probe = one 16-B load.
+// (FMX_MAP_SLOTS build: one slot per voxel.)
 struct alignas(16) Slot {
   unsigned long long key;
   uint32_t first;
   uint32_t count;
 };
+
+// Brick: the 2 x 2 x 2 cells (x, y, z) >> 1 of one 64-B bucket — the 27-cell
+// neighbourhood of any cell lies in at most 8 bricks, and neighbouring queries share
+// them.  Records of cell c (c = (x & 1) | (y & 1) << 1 | (z & 1) << 2) are
+// [beg[c], beg[c + 1]); empty buckets have key 0.  pad[0] of the extra bucket after
+// the table is the map's range-error word.
+struct alignas(64) Brick {
+  unsigned long long key;  // pack_key of the brick coordinates
+  uint32_t beg[9];
+  uint32_t pad[5];
+};
+static_assert(sizeof(Brick) == 64, "brick = 64 B");
+__device__ __forceinline__ uint64_t brick_key(int x, int y, int z) { return pack_key(x >> 1, y >> 1, z >> 1); }
+__device__ __forceinline__ uint32_t brick_cell(int x, int y, int z) {
+  return (uint32_t)((x & 1) | ((y & 1) << 1) | ((z & 1) << 2));
+}
 
 }  // namespace fmx

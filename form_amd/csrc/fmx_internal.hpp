@@ -137,7 +137,8 @@ struct Pool {
 // range-error word; records (build order and voxel-sorted) planar [0, n[0]) then
 // point [n[0], n[0] + n[1]); normals for planar records only.
 struct VoxMap {
-  DBuf<uint4> table;            // fmx::Slot
+  DBuf<uint4> table;            // fmx::Brick (fmx::Slot in the FMX_MAP_SLOTS build)
+  DBuf<uint32_t> bcnt, bcur;    // per brick cell: record count, scatter cursor (build only)
   uint64_t cap[2] = {0, 0};     // powers of two
   uint32_t n[2] = {0, 0};
   DBuf<double4> tpos, tnrm;     // transformed records, build order

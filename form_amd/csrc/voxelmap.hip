@@ -55,9 +55,11 @@ struct BuildArgs {
   const double* poses;
   uint32_t n0, n;  // planar records, all records
   double w;
-  Slot* table;
+  Slot* table;      // FMX_MAP_SLOTS
+  Brick* bricks;    // brick layout (default)
+  uint32_t* bcnt;   // [brick][8] record counts
   uint64_t mask[2];
-  uint64_t off1;  // first point slot
+  uint64_t off1;  // first point slot / brick
   double4* tpos;
   double4* tnrm;  // [n0]
   uint32_t* rslot;
@@ -91,6 +93,7 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
     a.rslot[rec] = 0xFFFFFFFFu;
     return;
   }
+#ifdef FMX_MAP_SLOTS
   const unsigned long long key = pack_key(cx, cy, cz);
   Slot* table = a.table + (t == 0 ? 0 : a.off1);
   const uint64_t mask = a.mask[t];
@@ -102,6 +105,20 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   }
   atomicAdd(&table[h].count, 1u);
   a.rslot[rec] = (uint32_t)((t == 0 ? 0 : a.off1) + h);
+#else
+  const unsigned long long key = brick_key(cx, cy, cz);
+  Brick* bricks = a.bricks + (t == 0 ? 0 : a.off1);
+  const uint64_t mask = a.mask[t];
+  uint64_t h = mix64(key) & mask;
+  for (;;) {  // the table has more buckets than records: an empty one always exists
+    const unsigned long long prev = atomicCAS(&bricks[h].key, 0ull, key);
+    if (prev == 0ull || prev == key) break;
+    h = (h + 1) & mask;
+  }
+  const uint32_t cell = (uint32_t)(((t == 0 ? 0 : a.off1) + h) * 8 + brick_cell(cx, cy, cz));
+  atomicAdd(a.bcnt + cell, 1u);
+  a.rslot[rec] = cell;
+#endif
 }
 
 struct CountIn {
@@ -112,6 +129,22 @@ struct FirstOut {
   Slot* t;
   __device__ void operator()(size_t i, uint32_t v) const { t[i].first = v; }
 };
+// Brick layout: scanned over [brick][cell] (+ one zero entry past the end), the
+// prefix is cell (i / 8, i % 8)'s first record, the scatter cursor, and the previous
+// brick's end marker beg[8] at every brick boundary.
+struct BrickCountIn {
+  const uint32_t* c;
+  __device__ uint32_t operator()(size_t i) const { return c[i]; }
+};
+struct BrickFirstOut {
+  Brick* b;
+  uint32_t* cur;
+  __device__ void operator()(size_t i, uint32_t v) const {
+    cur[i] = v;
+    b[i >> 3].beg[i & 7] = v;
+    if ((i & 7) == 0 && i > 0) b[(i >> 3) - 1].beg[8] = v;
+  }
+};
 
 // After the scatter each slot's `first` has advanced by `count`: records of a voxel
 // are [first - count, first).  Planar slots precede point slots in the scan, so
@@ -120,13 +153,18 @@ __global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec,
                                                      const uint32_t* __restrict__ rseg,
                                                      const double4* __restrict__ tpos,
                                                      const double4* __restrict__ tnrm, Slot* __restrict__ table,
+                                                     uint32_t* __restrict__ cursor,
                                                      double4* __restrict__ pos, double4* __restrict__ nrm,
                                                      uint32_t* __restrict__ seg, uint32_t* __restrict__ rid) {
   const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
   if (rec >= nrec) return;
   const uint32_t s = rslot[rec];
   if (s == 0xFFFFFFFFu) return;
+#ifdef FMX_MAP_SLOTS
   const uint32_t o = atomicAdd(&table[s].first, 1u);
+#else
+  const uint32_t o = atomicAdd(cursor + s, 1u);  // brick cell cursor
+#endif
   const double4 tp = tpos[rec];
   pos[o] = make_double4(tp.x, tp.y, tp.z, (double)rec);  // .w: build order (k_match tie-break)
   if (rec < n0) nrm[o] = tnrm[rec];
@@ -135,7 +173,8 @@ __global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec,
 }
 
 struct MapView {
-  const Slot* table;
+  const Slot* table;    // FMX_MAP_SLOTS
+  const Brick* bricks;  // brick layout
   uint64_t mask;
   const double4* pos;
   const double4* nrm;
@@ -189,6 +228,10 @@ struct MatchArgs {
 constexpr int kGroup = 8;  // lanes per query (16 made the kernel 15% faster but register_scan slower)
 constexpr int kQPB = 32;  // queries per block: 256 threads, so every block of a scan is resident at once
 constexpr int kMatchThreads = kQPB * kGroup;  // 256
+#ifndef FMX_SMALL_CELL
+#define FMX_SMALL_CELL 2
+#endif
+constexpr int kSmallCell = FMX_SMALL_CELL;  // neighbour cells with at most this many records: one lane folds them
 // Tiled pair sort: a tile = kTileBlocks match blocks of one type = 1024 queries, one
 // k_pair_scatter_t block; the match counts matches per (type, pair, tile).
 constexpr int kTileBlocks = 32;
@@ -337,6 +380,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     const double hi[3] = {(bx + 1) * a.w - wq[0], (by + 1) * a.w - wq[1], (bz + 1) * a.w - wq[2]};
     double best = a.bound;
     uint32_t best_rid = 0xFFFFFFFFu, best_i = 0xFFFFFFFFu;
+#ifdef FMX_MAP_SLOTS
     auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count) {
       const unsigned long long key = pack_key(bx + sx, by + sy, bz + sz);
       uint64_t h = mix64(key) & M.mask;
@@ -354,6 +398,30 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         h = (h + 1) & M.mask;
       }
     };
+#else
+    // one bucket read per probe: key and the cell's two boundaries in flight together
+    auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count) {
+      const int X = bx + sx, Y = by + sy, Z = bz + sz;
+      const unsigned long long key = brick_key(X, Y, Z);
+      const uint32_t ci = brick_cell(X, Y, Z);
+      uint64_t h = mix64(key) & M.mask;
+      first = 0;
+      count = 0;
+      for (;;) {
+        ++n_probe;
+        const Brick* b = M.bricks + h;
+        const unsigned long long k = b->key;
+        const uint32_t b0 = b->beg[ci], b1 = b->beg[ci + 1];
+        if (k == key) {
+          first = b0;
+          count = b1 - b0;
+          return;
+        }
+        if (k == 0ull) return;
+        h = (h + 1) & M.mask;
+      }
+    };
+#endif
     // a record is one double4: world position + its build order in .w (exact in a
     // double), so a candidate test is one 32-B load
     auto fold = [&](const double4& p, uint32_t i) {
@@ -444,7 +512,27 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
             vlb = lb;
           }
         }
+#ifndef FMX_MATCH_SERIAL_CELLS
+        // small cells (<= kSmallCell records): the lane that probed one folds its
+        // records itself, every lane's loads in flight together, one group min after;
+        // the argmin on (d^2, build order) does not depend on the folding order
+        const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
+        if (small) {
+          double4 pr[kSmallCell];
+#pragma unroll
+          for (int u = 0; u < kSmallCell; ++u)
+            if (u < (int)vc) pr[u] = M.pos[vf + u];
+#pragma unroll
+          for (int u = 0; u < kSmallCell; ++u)
+            if (u < (int)vc) fold(pr[u], vf + u);
+          n_cand += vc;
+        }
+        const int gsh = (lane_id() / kGroup) * kGroup;
+        if ((__ballot(small) >> gsh) & ((1ull << kGroup) - 1)) group_min();
+        uint64_t live = __ballot(vc > (uint32_t)kSmallCell);  // larger cells: walked by the group
+#else
         uint64_t live = __ballot(vc != 0);  // wave-wide mask; this group's lanes
+#endif
         live = (live >> ((lane_id() / kGroup) * kGroup)) & ((1ull << kGroup) - 1);
         while (live) {
           const int l = __ffsll((unsigned long long)live) - 1;
@@ -918,6 +1006,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   // for zeroing, insert, count scan and scatter
   VoxMap& M = c->map;
   const uint32_t n = nrec[0] + nrec[1];
+#ifdef FMX_MAP_SLOTS
   for (int t = 0; t < 2; ++t) {
     M.n[t] = nrec[t];
     M.cap[t] = next_pow2(std::max<uint64_t>(2ull * nrec[t], 1024));  // load factor <= 0.5
@@ -926,6 +1015,24 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   M.table.ensure(slots + 1);
   c->map_err_p = reinterpret_cast<uint32_t*>(M.table.p + slots);
   FMX_HIP(hipMemsetAsync(M.table.p, 0, (slots + 1) * sizeof(Slot), st));
+  const double table_bytes = 16.0 * (double)slots;
+#else
+  // bricks: more buckets than records, so an empty bucket always ends a probe (a
+  // brick holds >= 1 record; real scans fill a few percent of the buckets)
+  for (int t = 0; t < 2; ++t) {
+    M.n[t] = nrec[t];
+    M.cap[t] = next_pow2(std::max<uint64_t>((uint64_t)nrec[t] + 1, 256));
+  }
+  const uint64_t slots = M.cap[0] + M.cap[1];  // buckets
+  M.table.ensure(4 * (slots + 1));
+  Brick* bricks = reinterpret_cast<Brick*>(M.table.p);
+  c->map_err_p = &bricks[slots].pad[0];
+  FMX_HIP(hipMemsetAsync(M.table.p, 0, (slots + 1) * sizeof(Brick), st));
+  M.bcnt.ensure(8 * slots + 1);
+  M.bcur.ensure(8 * slots + 1);
+  FMX_HIP(hipMemsetAsync(M.bcnt.p, 0, (8 * slots + 1) * sizeof(uint32_t), st));
+  const double table_bytes = 64.0 * (double)slots;
+#endif
   M.tpos.ensure(n + 1);
   M.tnrm.ensure(nrec[0] + 1);
   M.rslot.ensure(n + 1);
@@ -934,7 +1041,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   M.nrm.ensure(nrec[0] + 1);
   M.seg.ensure(n + 1);
   M.rid.ensure(n + 1);
-  const double bytes = 2.0 * 32.0 * nrec[0] + 2.0 * 16.0 * nrec[1] + 16.0 * (double)slots;
+  const double bytes = 2.0 * 32.0 * nrec[0] + 2.0 * 16.0 * nrec[1] + table_bytes;
   ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
   HostScope* hs_l = new HostScope(7);
   if (n > 0) {
@@ -950,6 +1057,8 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     ba.n = n;
     ba.w = c->cell_w;
     ba.table = reinterpret_cast<Slot*>(M.table.p);
+    ba.bricks = reinterpret_cast<Brick*>(M.table.p);
+    ba.bcnt = M.bcnt.p;
     ba.mask[0] = M.cap[0] - 1;
     ba.mask[1] = M.cap[1] - 1;
     ba.off1 = M.cap[0];
@@ -960,12 +1069,19 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     ba.err = c->map_err_p;
     hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, ba);
     FMX_HIP(hipGetLastError());
-    c->scan_scratch.ensure(scan_scratch_size(slots) + 4);
     c->dev_u32.ensure(8);
+#ifdef FMX_MAP_SLOTS
+    c->scan_scratch.ensure(scan_scratch_size(slots) + 4);
     exclusive_scan(CountIn{reinterpret_cast<const Slot*>(M.table.p)}, FirstOut{reinterpret_cast<Slot*>(M.table.p)},
                    slots, c->scan_scratch.p, c->dev_u32.p + 4, st);
+#else
+    c->scan_scratch.ensure(scan_scratch_size(8 * slots + 1) + 4);
+    exclusive_scan(BrickCountIn{M.bcnt.p}, BrickFirstOut{reinterpret_cast<Brick*>(M.table.p), M.bcur.p}, 8 * slots + 1,
+                   c->scan_scratch.p, c->dev_u32.p + 4, st);
+#endif
     hipLaunchKernelGGL(k_map_scatter, dim3((n + 255) / 256), dim3(256), 0, st, nrec[0], n, M.rslot.p, M.rseg.p,
-                       M.tpos.p, M.tnrm.p, reinterpret_cast<Slot*>(M.table.p), M.pos.p, M.nrm.p, M.seg.p, M.rid.p);
+                       M.tpos.p, M.tnrm.p, reinterpret_cast<Slot*>(M.table.p), M.bcur.p, M.pos.p, M.nrm.p, M.seg.p,
+                       M.rid.p);
     FMX_HIP(hipGetLastError());
   }
   delete hs_l;
@@ -1034,7 +1150,8 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->h_counts.ensure(2 * (size_t)K + 4);
   auto view = [&](int t) {  // type t's table section over the shared record arrays
     VoxMap& M = c->map;
-    return MapView{reinterpret_cast<const Slot*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
+    return MapView{reinterpret_cast<const Slot*>(M.table.p) + (t == 0 ? 0 : M.cap[0]),
+                   reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
                    M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
   };
   // Algorithmic bytes of a match launch: query read (16 B) +
