@@ -229,11 +229,158 @@ __attribute__((target("avx2,fma"))) void chol_back_fma(const double* a, int n, c
   }
 }
 
+// AVX-512 form (the GPU box's EPYC has it): panel of 8 rows, every trailing row
+// updated as whole 8-wide column vectors starting at the vector that holds its
+// diagonal — the few entries left of the diagonal are lower-triangle scratch the
+// factor never reads, so no scalar heads or tails (masked loads for n % 8).  Two
+// trailing rows per pass share each panel load.  Same update order per element as
+// the AVX2 form (k ascending), FMA rounding.
+__attribute__((target("avx512f,fma"))) inline __mmask8 tail_mask(int left) {
+  return left >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << left) - 1u);
+}
+
+template <int NB>
+__attribute__((target("avx512f,fma"))) void chol_trail_512(double* a, int n, int kb, int ke, int nb) {
+  const int nt = NB > 0 ? NB : nb;
+  const double* U[8];
+  for (int t = 0; t < nt; ++t) U[t] = a + (size_t)(kb + t) * n;
+  int i = ke;
+  for (; i + 2 <= n; i += 2) {
+    double* __restrict A0 = a + (size_t)i * n;
+    double* __restrict A1 = A0 + n;
+    __m512d b0[8], b1[8];
+    for (int t = 0; t < nt; ++t) {
+      b0[t] = _mm512_set1_pd(U[t][i]);
+      b1[t] = _mm512_set1_pd(U[t][i + 1]);
+    }
+    int m = i & ~7;
+    for (; m + 16 <= n; m += 16) {  // two column vectors: four independent FMA chains
+      __m512d x0 = _mm512_loadu_pd(A0 + m), x1 = _mm512_loadu_pd(A1 + m);
+      __m512d y0 = _mm512_loadu_pd(A0 + m + 8), y1 = _mm512_loadu_pd(A1 + m + 8);
+      for (int t = 0; t < nt; ++t) {
+        const __m512d uu = _mm512_loadu_pd(U[t] + m), vv = _mm512_loadu_pd(U[t] + m + 8);
+        x0 = _mm512_fnmadd_pd(b0[t], uu, x0);
+        x1 = _mm512_fnmadd_pd(b1[t], uu, x1);
+        y0 = _mm512_fnmadd_pd(b0[t], vv, y0);
+        y1 = _mm512_fnmadd_pd(b1[t], vv, y1);
+      }
+      _mm512_storeu_pd(A0 + m, x0);
+      _mm512_storeu_pd(A1 + m, x1);
+      _mm512_storeu_pd(A0 + m + 8, y0);
+      _mm512_storeu_pd(A1 + m + 8, y1);
+    }
+    for (; m < n; m += 8) {
+      const __mmask8 k = tail_mask(n - m);
+      __m512d x0 = _mm512_maskz_loadu_pd(k, A0 + m), x1 = _mm512_maskz_loadu_pd(k, A1 + m);
+      for (int t = 0; t < nt; ++t) {
+        const __m512d uu = _mm512_maskz_loadu_pd(k, U[t] + m);
+        x0 = _mm512_fnmadd_pd(b0[t], uu, x0);
+        x1 = _mm512_fnmadd_pd(b1[t], uu, x1);
+      }
+      _mm512_mask_storeu_pd(A0 + m, k, x0);
+      _mm512_mask_storeu_pd(A1 + m, k, x1);
+    }
+  }
+  for (; i < n; ++i) {
+    double* __restrict A0 = a + (size_t)i * n;
+    __m512d b0[8];
+    for (int t = 0; t < nt; ++t) b0[t] = _mm512_set1_pd(U[t][i]);
+    for (int m = i & ~7; m < n; m += 8) {
+      const __mmask8 k = tail_mask(n - m);
+      __m512d x0 = _mm512_maskz_loadu_pd(k, A0 + m);
+      for (int t = 0; t < nt; ++t) x0 = _mm512_fnmadd_pd(b0[t], _mm512_maskz_loadu_pd(k, U[t] + m), x0);
+      _mm512_mask_storeu_pd(A0 + m, k, x0);
+    }
+  }
+}
+
+__attribute__((target("avx512f,fma"))) bool chol_solve_512(double* a, const double* g, double* x, int n) {
+  for (int kb = 0; kb < n; kb += 8) {
+    const int ke = std::min(n, kb + 8);
+    for (int k = kb; k < ke; ++k) {  // panel
+      double* __restrict Uk = a + (size_t)k * n;
+      const double s = Uk[k];
+      if (!(s > 0)) return false;
+      const double ukk = std::sqrt(s);
+      const __m512d r = _mm512_set1_pd(1.0 / ukk);
+      for (int m = k & ~7; m < n; m += 8) {
+        const __mmask8 msk = tail_mask(n - m);
+        _mm512_mask_storeu_pd(Uk + m, msk, _mm512_mul_pd(_mm512_maskz_loadu_pd(msk, Uk + m), r));
+      }
+      Uk[k] = ukk;
+      for (int i = k + 1; i < ke; ++i) {
+        double* __restrict Ai = a + (size_t)i * n;
+        const __m512d u = _mm512_set1_pd(Uk[i]);
+        for (int m = i & ~7; m < n; m += 8) {
+          const __mmask8 msk = tail_mask(n - m);
+          _mm512_mask_storeu_pd(Ai + m, msk,
+                                _mm512_fnmadd_pd(u, _mm512_maskz_loadu_pd(msk, Uk + m), _mm512_maskz_loadu_pd(msk, Ai + m)));
+        }
+      }
+    }
+    if (ke < n) {
+      if (ke - kb == 8) chol_trail_512<8>(a, n, kb, ke, 8);
+      else chol_trail_512<0>(a, n, kb, ke, ke - kb);
+    }
+  }
+  // forward U^T y = g (y in x), then back U x = y
+  std::memcpy(x, g, (size_t)n * sizeof(double));
+  for (int k = 0; k < n; ++k) {
+    const double* Uk = a + (size_t)k * n;
+    const double yk = x[k] / Uk[k];
+    x[k] = yk;
+    const __m512d b = _mm512_set1_pd(yk);
+    int m = k + 1;
+    for (; m < n; m += 8) {
+      const __mmask8 msk = tail_mask(n - m);
+      _mm512_mask_storeu_pd(x + m, msk, _mm512_fnmadd_pd(b, _mm512_maskz_loadu_pd(msk, Uk + m), _mm512_maskz_loadu_pd(msk, x + m)));
+    }
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    const double* Ui = a + (size_t)i * n;
+    __m512d acc = _mm512_setzero_pd();
+    for (int k = i + 1; k < n; k += 8) {
+      const __mmask8 msk = tail_mask(n - k);
+      acc = _mm512_fmadd_pd(_mm512_maskz_loadu_pd(msk, Ui + k), _mm512_maskz_loadu_pd(msk, x + k), acc);
+    }
+    x[i] = (x[i] - _mm512_reduce_add_pd(acc)) / Ui[i];
+  }
+  return true;
+}
+
+__attribute__((target("avx512f,fma"))) double dot_512(const double* p, const double* q, int n) {
+  __m512d acc = _mm512_setzero_pd();
+  for (int k = 0; k < n; k += 8) {
+    const __mmask8 msk = tail_mask(n - k);
+    acc = _mm512_fmadd_pd(_mm512_maskz_loadu_pd(msk, p + k), _mm512_maskz_loadu_pd(msk, q + k), acc);
+  }
+  return _mm512_reduce_add_pd(acc);
+}
+
+// 0 plain, 1 AVX2+FMA, 2 AVX-512 (FMX_CHOL_PLAIN / FMX_CHOL_AVX2 force the lower ones)
+int simd_level() {
+  static const int lv = [] {
+    if (std::getenv("FMX_CHOL_PLAIN")) return 0;
+    const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+    if (avx2 && __builtin_cpu_supports("avx512f") && !std::getenv("FMX_CHOL_AVX2")) return 2;
+    return avx2 ? 1 : 0;
+  }();
+  return lv;
+}
+
 }  // namespace
 
+// sum_k p[k] q[k]: vector partial sums on AVX-512 hosts, left to right otherwise
+double dot(const double* p, const double* q, int n) {
+  if (simd_level() == 2) return dot_512(p, q, n);
+  double s = 0;
+  for (int k = 0; k < n; ++k) s += p[k] * q[k];
+  return s;
+}
+
 bool chol_solve(std::vector<double>& A, const double* g, double* x, int n) {
-  static const bool fma = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma") &&
-                          std::getenv("FMX_CHOL_PLAIN") == nullptr;
+  if (simd_level() == 2) return chol_solve_512(A.data(), g, x, n);
+  const bool fma = simd_level() == 1;
   double* a = A.data();
   for (int kb = 0; kb < n; kb += kCholB) {
     const int ke = std::min(n, kb + kCholB);
@@ -306,12 +453,12 @@ struct Assembler {
     }
   }
   double run(const std::vector<Pose>& x, DenseSys& S, std::vector<double>& G, int& lins) const {
+    const bool split = !g.pairs.empty() && g.lin_begin;
+    if (split) g.lin_begin(x);  // device work overlaps everything below up to lin_end
     if (S.D != base.D || S.keys != base.keys) S = base;
     else std::memcpy(S.A.data(), base.A.data(), base.A.size() * sizeof(double));
     G.assign(g.pairs.size() * kPairG, 0.0);
-    const bool split = !g.pairs.empty() && g.lin_begin;
-    if (split) g.lin_begin(x);  // device work overlaps the host terms below
-    else if (!g.pairs.empty()) {
+    if (!split && !g.pairs.empty()) {
       g.lin_pairs(x, G.data());
       ++lins;
     }
@@ -407,9 +554,7 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
       if (ok) {
         double dHd = 0, dg = 0;
         for (int r = 0; r < D; ++r) {
-          double h = 0;
-          const double* Hr = &S.A[(size_t)r * (D + 1)];
-          for (int c = 0; c < D; ++c) h += Hr[c] * dx[c];
+          const double h = dot(&S.A[(size_t)r * (D + 1)], dx.data(), D);
           dHd += dx[r] * h;
           dg += dx[r] * gg[r];
         }

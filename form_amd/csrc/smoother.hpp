@@ -72,6 +72,8 @@ struct DenseSys {
 // Solve A x = g for SPD A (n x n row-major, overwritten by the factor); false if A is
 // not positive definite.
 bool chol_solve(std::vector<double>& A, const double* g, double* x, int n);
+// sum_k p[k] q[k] (vector partial sums on AVX-512 hosts)
+double dot(const double* p, const double* q, int n);
 
 // Schur complement eliminating the first nm columns of an n-column augmented system;
 // out = (n - nm + 1)^2.  False if the eliminated block is not positive definite.
