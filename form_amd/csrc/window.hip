@@ -219,17 +219,36 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
     __syncthreads();
     WSTAMP(2);
     if (s_t != ce - cb - 1) return;
-    // the pair's last chunk: partials in chunk order, kFinBatch loads in flight per thread
-    if (tid < 91) {
-      bsum = 0.0;
-      for (uint32_t c0 = cb; c0 < ce; c0 += kFinBatch) {
-        double x[kFinBatch];
+    // the pair's last chunk sums the partials: wave w takes chunks cb + w, cb + w + W,
+    // ... (in order) for entries lane and lane + 64, 2 x kFinBatch loads in flight per
+    // lane; the W wave sums then meet in LDS in wave order (a fixed order: deterministic)
+    {
+      const int e1 = lane + kWave;
+      const bool has1 = e1 < 91;
+      double s0 = 0.0, s1 = 0.0;
+      for (uint32_t c0 = cb + w; c0 < ce; c0 += kFinBatch * kWinWaves) {
+        double x0[kFinBatch], x1[kFinBatch];
 #pragma unroll
-        for (int u = 0; u < kFinBatch; ++u)
-          x[u] = c0 + u < ce ? agent_load(a.partials + (size_t)(c0 + u) * kWinLd + tid) : 0.0;
+        for (int u = 0; u < kFinBatch; ++u) {
+          const uint32_t cc = c0 + u * kWinWaves;
+          const double* src = a.partials + (size_t)cc * kWinLd;
+          x0[u] = cc < ce ? agent_load(src + lane) : 0.0;
+          x1[u] = cc < ce && has1 ? agent_load(src + e1) : 0.0;
+        }
 #pragma unroll
-        for (int u = 0; u < kFinBatch; ++u) bsum += x[u];
+        for (int u = 0; u < kFinBatch; ++u) {
+          s0 += x0[u];
+          s1 += x1[u];
+        }
       }
+      s_g[w][lane] = s0;
+      if (has1) s_g[w][e1] = s1;
+    }
+    __syncthreads();
+    if (tid < 91) {
+      bsum = s_g[0][tid];
+#pragma unroll
+      for (int i = 1; i < kWinWaves; ++i) bsum += s_g[i][tid];
     }
     if (tid == 0) __hip_atomic_store(a.pair_ticket + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
