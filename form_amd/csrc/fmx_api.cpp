@@ -295,6 +295,11 @@ struct fmx_ctx::Est {
   // every stored pair's linearization at `values` (the last full LM's final state),
   // keyed (j, i): m_fast_linear and marginalize reuse it
   std::map<std::pair<uint64_t, uint64_t>, std::vector<double>> gcache;
+  // keyscan step + marginalization of the last registered scan, deferred to the next
+  // register_scan where it runs while that scan's extraction kernels execute
+  bool tail_pending = false;
+  uint64_t tail_j = 0;
+  uint32_t tail_nfeat = 0;
 };
 
 namespace {
@@ -656,6 +661,32 @@ void remove_scan(fmx_ctx* c, uint64_t s) {  // KeypointMap::remove (map.tpp:112-
   for (int t = 0; t < 2; ++t) c->pool[t].ranges.erase(s);
 }
 
+// The tail of register_scan (form.cpp:104-111): keyscan selection + marginalization
+// of the last registered scan.  It changes only host-side window state (which scans
+// and factors remain), never the registered poses, so register_scan defers it to the
+// next call (where it overlaps that scan's extraction); entry points that read the
+// keypoint pool run it first.
+void finish_tail(fmx_ctx* c, fmx_ctx::Est& e) {
+  if (!e.tail_pending) return;
+  e.tail_pending = false;
+  HostScope hs(5);
+  const fmx_params& P = c->P;
+  auto marg = e.ks.step(e.tail_j, e.tail_nfeat, [&](uint64_t i) {
+    return num_recent_connections(e, i, e.ks.oldest_rf());
+  });
+  if (!P.disable_smoothing) smooth_marginalize(e, marg);
+  for (uint64_t m : marg) {
+    if (!P.disable_smoothing) win_remove(c, m);
+    e.values.erase(m);
+    e.cons.erase(m);
+    for (auto& [jj, mm] : e.cons) mm.erase(m);
+    remove_scan(c, m);
+  }
+}
+void finish_tail(fmx_ctx* c) {
+  if (c->est) finish_tail(c, *c->est);
+}
+
 void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
   HostScope hs_all(0);
   if (!c->est) {
@@ -664,29 +695,36 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   }
   fmx_ctx::Est& e = *c->est;
   const fmx_params& P = c->P;
-  // step(prediction) (constraints.cpp:206-223)
-  const Pose pred = predict_next(e);
   const size_t RC = (size_t)P.extraction.num_rows * (size_t)P.extraction.num_columns;
   if (n != RC)
     throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " + std::to_string(RC) +
                                       " != " + std::to_string(n));
-  if (e.init) ++e.scan;
-  e.init = true;
-  const uint64_t j = e.scan;
-  e.values[j] = pred;
-  if (j == 0) e.priors.push_back(PriorF{0, pred, 1e-3});  // addPrior (constraints.cpp:217-220)
-  auto& cj = e.cons[j];
-  for (auto& [i, T] : e.values)
-    if (i != j) cj[i] = {0, 0};
-  // to_voxel_map x2, voxel width = max_dist_matching (form.cpp:61-65).  The map holds
-  // only earlier scans at their current estimates, so it does not depend on this
-  // scan's features.
-  std::set<uint64_t> sset;
-  for (int t = 0; t < 2; ++t)
-    for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
-  std::vector<uint64_t> scans(sset.begin(), sset.end());
-  std::vector<double> poses(12 * scans.size());
-  for (size_t k = 0; k < scans.size(); ++k) std::memcpy(&poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double));
+  const uint64_t j = e.init ? e.scan + 1 : 0;
+  // Host work that only needs the estimator state runs while this scan's extraction
+  // kernels execute: the previous scan's deferred tail (keyscan step +
+  // marginalization), then step(prediction) (constraints.cpp:206-223) and the map
+  // build inputs.  to_voxel_map x2, voxel width = max_dist_matching (form.cpp:61-65):
+  // the map holds only earlier scans at their current estimates, so it does not
+  // depend on this scan's features.
+  std::vector<uint64_t> scans;
+  std::vector<double> poses;
+  auto prepare = [&] {
+    finish_tail(c, e);
+    const Pose pred = predict_next(e);
+    e.scan = j;
+    e.init = true;
+    e.values[j] = pred;
+    if (j == 0) e.priors.push_back(PriorF{0, pred, 1e-3});  // addPrior (constraints.cpp:217-220)
+    auto& cj = e.cons[j];
+    for (auto& [i, T] : e.values)
+      if (i != j) cj[i] = {0, 0};
+    std::set<uint64_t> sset;
+    for (int t = 0; t < 2; ++t)
+      for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
+    scans.assign(sset.begin(), sset.end());
+    poses.resize(12 * scans.size());
+    for (size_t k = 0; k < scans.size(); ++k) std::memcpy(&poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double));
+  };
   // The map build goes to the side stream and is queued while the extraction kernels
   // run (extraction occupies one CU per scan line, so the build's kernels take the
   // idle CUs, and its host launch cost hides behind the extraction wait).
@@ -694,6 +732,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   static const bool inline_map = std::getenv("FMX_MAP_INLINE") != nullptr;
   fmx_feature_counts fc{};
   if (inline_map) {
+    prepare();
     {
       HostScope hs_map(3);
       run_map_build(c, scans, poses.data(), P.max_dist_matching);
@@ -704,6 +743,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
     HostScope hs_ex(2);
     do_extract(c, xyzw, n, j, on_dev, &fc, [&] {
+      prepare();
       HostScope hs_map(3);
       FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
       run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
@@ -711,6 +751,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     });
     FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   }
+  auto& cj = e.cons[j];
   HostScope* hs_icp = new HostScope(4);
   uint64_t icp = 0, lm_it = 0, lins = 0;
   static const bool host_lm = std::getenv("FMX_DEVICE_LM") == nullptr;  // default: host LM
@@ -811,18 +852,10 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   ensure_pool_room(c, 0, c->n_qpl);
   ensure_pool_room(c, 1, c->n_qpt);
   run_insert(c, j, nin);
-  // keyscan selection + marginalization (form.cpp:104-111)
-  auto marg = e.ks.step(j, fc.planar + fc.point, [&](uint64_t i) {
-    return num_recent_connections(e, i, e.ks.oldest_rf());
-  });
-  if (!P.disable_smoothing) smooth_marginalize(e, marg);
-  for (uint64_t m : marg) {
-    if (!P.disable_smoothing) win_remove(c, m);
-    e.values.erase(m);
-    e.cons.erase(m);
-    for (auto& [jj, mm] : e.cons) mm.erase(m);
-    remove_scan(c, m);
-  }
+  // keyscan selection + marginalization (form.cpp:104-111): deferred (finish_tail)
+  e.tail_pending = true;
+  e.tail_j = j;
+  e.tail_nfeat = fc.planar + fc.point;
   c->stats[0] = icp;
   c->stats[1] = lm_it;
   c->stats[2] = mpl;
@@ -996,6 +1029,7 @@ fmx_status fmx_set_queries(fmx_ctx* c, uint64_t scan, const float* planar, uint3
 fmx_status fmx_keypoints_add(fmx_ctx* c, uint64_t scan, const float* planar, uint32_t npl, const float* point,
                              uint32_t npt) {
   return guard(c, [&] {
+    finish_tail(c);
     if ((npl && !planar) || (npt && !point)) throw StatusError(FMX_E_INVAL, "null features");
     pool_add(c, 0, scan, planar, npl);
     pool_add(c, 1, scan, point, npt);
@@ -1005,6 +1039,7 @@ fmx_status fmx_keypoints_add(fmx_ctx* c, uint64_t scan, const float* planar, uin
 fmx_status fmx_keypoints_add_device(fmx_ctx* c, uint64_t scan, const float* plp, const float* pln, uint32_t npl,
                                     const float* ptp, uint32_t npt) {
   return guard(c, [&] {
+    finish_tail(c);
     if ((npl && (!plp || !pln)) || (npt && !ptp)) throw StatusError(FMX_E_INVAL, "null features");
     pool_add_device(c, 0, scan, plp, pln, npl);
     pool_add_device(c, 1, scan, ptp, nullptr, npt);
@@ -1020,11 +1055,12 @@ fmx_status fmx_set_queries_device(fmx_ctx* c, uint64_t scan, const float* plp, c
 }
 
 fmx_status fmx_keypoints_remove(fmx_ctx* c, uint64_t scan) {
-  return guard(c, [&] { remove_scan(c, scan); });
+  return guard(c, [&] { finish_tail(c); remove_scan(c, scan); });
 }
 
 fmx_status fmx_map_build(fmx_ctx* c, const uint64_t* scans, const double* poses, uint32_t n, double w) {
   return guard(c, [&] {
+    finish_tail(c);
     if (n && (!scans || !poses)) throw StatusError(FMX_E_INVAL, "null scans/poses");
     if (!(w > 0)) throw StatusError(FMX_E_INVAL, "voxel width must be > 0");
     std::vector<uint64_t> s(scans, scans + n);
