@@ -497,7 +497,8 @@ void set_lin(WinGraph& g, B begin, E end) {
 // ICP loop (form.cpp:67-89) + optimize(false) (form.cpp:92-93) in smoothing mode:
 // every LM runs over all window poses; the current scan's FeatureFactors linearize
 // from the sorted match, the stored pairs from the window store (window.hip).
-void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uint64_t& lm_it, uint64_t& lins) {
+void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uint64_t& lm_it, uint64_t& lins,
+                     bool& inserted) {
   const fmx_params& P = c->P;
   const double sigma = P.planar_constraint_sigma;
   const LinF fast = fast_linear(e);
@@ -550,6 +551,13 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
   // the last match is the scan's constraint set: into the window store
   match_counts_fetch(c);
   win_persist(c, j);
+  // insert_matches (form.cpp:98-100) reads only the last match (local keypoints and
+  // their NN distances), not the poses optimize(false) moves: its kernel goes ahead of
+  // the full LM, off the scan's tail
+  ensure_pool_room(c, 0, c->n_qpl);
+  ensure_pool_room(c, 1, c->n_qpt);
+  run_insert(c, j, nullptr);
+  inserted = true;
   // optimize(false): every stored pair's FeatureFactor (constraints.cpp:294-305)
   const std::vector<WinPair> prs = win_pairs(c);
   g.lins.clear();
@@ -574,9 +582,16 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
   lm_it += R.iters;
   lins += R.lins;
   for (size_t k = 0; k < keys.size(); ++k) e.values[keys[k]] = R.x[k];  // update_values
-  e.gcache.clear();
-  for (size_t p = 0; p < prs.size(); ++p)
-    e.gcache[{prs[p].j, prs[p].i}].assign(R.G.begin() + p * kPairG, R.G.begin() + (p + 1) * kPairG);
+  // gcache = exactly the stored pairs' G at the new values: entries are overwritten in
+  // place (their vectors keep their storage), stale ones erased
+  std::set<std::pair<uint64_t, uint64_t>> live;
+  for (size_t p = 0; p < prs.size(); ++p) {
+    const std::pair<uint64_t, uint64_t> k{prs[p].j, prs[p].i};
+    e.gcache[k].assign(R.G.begin() + p * kPairG, R.G.begin() + (p + 1) * kPairG);
+    live.insert(k);
+  }
+  for (auto it = e.gcache.begin(); it != e.gcache.end();)
+    it = live.count(it->first) ? std::next(it) : e.gcache.erase(it);
 }
 
 // ConstraintManager::marginalize (constraints.cpp:120-203): the factors touching the
@@ -754,9 +769,10 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   auto& cj = e.cons[j];
   HostScope* hs_icp = new HostScope(4);
   uint64_t icp = 0, lm_it = 0, lins = 0;
+  bool inserted = false;
   static const bool host_lm = std::getenv("FMX_DEVICE_LM") == nullptr;  // default: host LM
   if (!P.disable_smoothing) {
-    smooth_register(c, e, j, icp, lm_it, lins);
+    smooth_register(c, e, j, icp, lm_it, lins, inserted);
   } else if (host_lm) {
     // ICP loop (form.cpp:67-89) with the LM on the host (one sync per linearization)
     DeviceLM lm{c, e, P.planar_constraint_sigma};
@@ -848,10 +864,11 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     mpt += c->cnt_pt[k];
   }
   // insert_matches (form.cpp:98-100) from the last match
-  uint32_t nin[2] = {0, 0};
-  ensure_pool_room(c, 0, c->n_qpl);
-  ensure_pool_room(c, 1, c->n_qpt);
-  run_insert(c, j, nin);
+  if (!inserted) {
+    ensure_pool_room(c, 0, c->n_qpl);
+    ensure_pool_room(c, 1, c->n_qpt);
+    run_insert(c, j, nullptr);
+  }
   // keyscan selection + marginalization (form.cpp:104-111): deferred (finish_tail)
   e.tail_pending = true;
   e.tail_j = j;

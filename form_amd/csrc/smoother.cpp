@@ -452,9 +452,11 @@ struct Assembler {
       }
     }
   }
-  double run(const std::vector<Pose>& x, DenseSys& S, std::vector<double>& G, int& lins) const {
+  // started: the caller already issued lin_begin(x) (window_lm's first linearization,
+  // launched before this Assembler was built)
+  double run(const std::vector<Pose>& x, DenseSys& S, std::vector<double>& G, int& lins, bool started = false) const {
     const bool split = !g.pairs.empty() && g.lin_begin;
-    if (split) g.lin_begin(x);  // device work overlaps everything below up to lin_end
+    if (split && !started) g.lin_begin(x);  // device work overlaps everything below up to lin_end
     if (S.D != base.D || S.keys != base.keys) S = base;
     else std::memcpy(S.A.data(), base.A.data(), base.A.size() * sizeof(double));
     G.assign(g.pairs.size() * kPairG, 0.0);
@@ -528,10 +530,12 @@ struct Assembler {
 WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
   WinLMResult R;
   R.x = x0;
+  const bool split = !g.pairs.empty() && g.lin_begin;
+  if (split) g.lin_begin(R.x);  // the first linearization runs while the base system is built
   const Assembler asmb(g);
   DenseSys S, Sn;
   std::vector<double> Gn;
-  double err = asmb.run(R.x, S, R.G, R.lins);
+  double err = asmb.run(R.x, S, R.G, R.lins, split);
   if (err <= 0.0) return R;
   double lambda = 1e-5;
   const int D = S.D;
