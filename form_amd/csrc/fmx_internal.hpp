@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <map>
 #include <stdexcept>
 #include <chrono>
@@ -43,9 +44,14 @@ struct DBuf {
   void ensure(size_t n) {
     if (n <= cap) return;
     ++dbuf_reallocs();
+    static const bool log = std::getenv("FMX_REALLOC_LOG") != nullptr;  // diagnostic: regrowths
+    if (log && p) fprintf(stderr, "dbuf regrow %zu -> %zu elements of %zu B\n", cap, n, sizeof(T));
     if (p) (void)hipFree(p);  // synchronizes the device: grow geometrically so it stays rare
     p = nullptr;
-    size_t c = 2 * n + 64;
+    // at least 256k elements (<= 8 MB for the widest element): the per-scan buffers of
+    // a 128 x 2048 stream never regrow once the window has filled (a regrowth's
+    // hipFree serializes the device mid-scan)
+    size_t c = std::max<size_t>(2 * n + 64, (size_t)1 << 18);
     FMX_HIP(hipMalloc(&p, c * sizeof(T)));
     cap = c;
   }
