@@ -51,6 +51,9 @@ def parse():
                     help="ConstraintManager mode: smooth = the reference default (window smoother), "
                          "single = the disable_smoothing ablation (single-pose LM)")
     ap.add_argument("--no-ablation", action="store_true", help="skip the other mode's secondary measurement")
+    ap.add_argument("--no-pin", action="store_true",
+                    help="leave the registering thread unpinned (default: bound to the CPU it runs on for the "
+                         "GPU measurements, released before the CPU baseline)")
     ap.add_argument("--subdiv", type=int, default=None, help="override voxel_subdivision (device map cells per voxel edge)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
@@ -90,6 +93,35 @@ def sum_over_ranks(x, world, local):
     t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def pin_thread(world, local):
+    """Bind the calling (registering) thread to one CPU; returns the previous affinity.
+    register_scan is a host-GPU latency chain (~15 host<->GPU round trips per scan): a
+    thread migrating between cores mid-chain measured up to 12 % slower on some boxes
+    (tools/step_times.py), never faster unpinned.  One rank: the CPU it runs on.  Several
+    ranks: distinct CPUs from each GPU's NUMA-local list (sysfs local_cpulist)."""
+    old = os.sched_getaffinity(0)
+    cpu = None
+    if world > 1:
+        try:
+            pr = torch.cuda.get_device_properties(local)
+            bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+            cpus = []
+            for part in open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                cpus += list(range(int(lo), int(hi or lo) + 1))
+            cands = [c for c in cpus if c in old]
+            cpu = cands[(4 * local) % len(cands)] if cands else None
+        except (OSError, ValueError, AttributeError):
+            cpu = None
+        if cpu is None:
+            return None
+    else:
+        with open("/proc/thread-self/stat") as f:
+            cpu = int(f.read().rsplit(")", 1)[1].split()[36])
+    os.sched_setaffinity(0, {cpu})
+    return old
 
 
 def cpu_baseline(scans_host, params, budget_s, single):
@@ -250,6 +282,7 @@ def main():
                                                voxel_subdivision=a.subdiv or 0, disable_smoothing=single_pose),
                            device=local)
 
+    prev_aff = None if a.no_pin else pin_thread(world, local)
     ablation = None
     if not a.no_ablation:  # the other mode over the same scans (secondary, untimed by the driver)
         actx = new_ctx(not single)
@@ -341,6 +374,8 @@ def main():
     }
     if ablation is not None:
         out["ablation"] = ablation
+    if prev_aff is not None:
+        os.sched_setaffinity(0, prev_aff)  # the CPU baseline's threads use every host core
     if not a.no_cpu_baseline and world == 1:
         host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
         out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s, single)
