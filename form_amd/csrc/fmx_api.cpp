@@ -18,8 +18,41 @@
 
 using namespace fmx;
 
-// ============================================================================ profiling
 namespace fmx {
+
+// ---------------------------------------------------------------- match-path dispatch
+// Lanes per query of k_match: 8 while the whole query set is resident at once (a
+// C4 scan's ~4e4 queries: more lanes shorten each query's chain of dependent loads),
+// 4 for large sets (>= 128k queries, e.g. C5's 2M): they run in several waves of
+// blocks, so more queries per wave raise the loads in flight (C5 match 1.42 -> 1.04 ms,
+// C4 8 lanes 0.22 vs 4 lanes 0.28 ms per scan).  FMX_MATCH_LANES=4|8 forces one.
+int match_group_for(uint64_t nq) {
+  static const int forced = [] {
+    const char* e = std::getenv("FMX_MATCH_LANES");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced == 4 || forced == 8) return forced;
+  return nq >= (128u << 10) ? 4 : 8;
+}
+void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, hipStream_t st) {
+  g8::run_map_build(c, scans, poses34, w, st);  // the same build in both variants
+}
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, const IcpDev* icp,
+               bool sorted) {
+  c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt);
+  if (c->match_group == 4) g4::run_match(c, pose_j34, max_dist, min_dist_map, icp, sorted);
+  else g8::run_match(c, pose_j34, max_dist, min_dist_map, icp, sorted);
+}
+void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
+  if (c->match_group == 4) g4::run_insert(c, scan, n_inserted);
+  else g8::run_insert(c, scan, n_inserted);
+}
+void match_counts_fetch(fmx_ctx* c, bool wait) {
+  if (c->match_group == 4) g4::match_counts_fetch(c, wait);
+  else g8::match_counts_fetch(c, wait);
+}
+
+// ============================================================================ profiling
 static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest", "fit",      "compact",   "map_build",
                                              "match",        "pair_sort", "linearize", "lin_final", "error_eval", "insert", "window"};
 

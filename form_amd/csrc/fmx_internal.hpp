@@ -298,6 +298,7 @@ struct fmx_ctx {
   fmx::DBuf<fmx::Chunk> chunks;
   fmx::DBuf<uint32_t> n_chunks;
   uint32_t max_chunks = 0;
+  int match_group = 8;  // lanes per query of the last run_match (voxelmap.hip g8 / g4)
   bool have_corr = false;
   uint64_t rows_pl = 0, rows_pt = 0;           // correspondences (plane rows, point pairs)
   std::vector<uint32_t> cnt_pl, cnt_pt;         // per pair, host copy after match
@@ -426,6 +427,19 @@ inline uint32_t next_flag(fmx_ctx* c) {
   }
   return ++c->flag_seq;
 }
+// voxelmap.hip is built twice: 8 lanes per query (fmx::g8, per-scan query sets) and 4
+// (fmx::g4, large query sets: more queries in flight per wave); the fmx:: entry points
+// below dispatch on c->match_group, chosen by run_match.
+#define FMX_VM_DECLS                                                                                   \
+  void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, \
+                     hipStream_t st = nullptr);                                                      \
+  void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,            \
+                 const IcpDev* icp = nullptr, bool sorted = true);                                   \
+  void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);                                  \
+  void match_counts_fetch(fmx_ctx* c, bool wait = true);
+namespace g8 { FMX_VM_DECLS }
+namespace g4 { FMX_VM_DECLS }
+#undef FMX_VM_DECLS
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
                  const std::function<void()>& while_waiting = nullptr);

@@ -31,7 +31,14 @@
 #include <cstring>
 #include <type_traits>
 
+#ifndef FMX_VM_NS
+#define FMX_VM_NS g8
+#endif
+
 namespace fmx {
+// This file is compiled twice (Makefile): FMX_MATCH_GROUP 8 -> fmx::g8 and 4 -> fmx::g4;
+// run_match picks one per launch (fmx_api.cpp, match_group_for).
+namespace FMX_VM_NS {
 namespace {
 
 __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
@@ -225,8 +232,11 @@ struct MatchArgs {
 // (d^2, build order).  ~8x the threads of a lane-per-query kernel: at per-scan
 // sizes (~4e4 queries) the chip would otherwise hold ~2 waves per CU and every
 // probe's latency would be exposed.
-constexpr int kGroup = 8;  // lanes per query (16 made the kernel 15% faster but register_scan slower)
-constexpr int kQPB = 32;  // queries per block: 256 threads, so every block of a scan is resident at once
+#ifndef FMX_MATCH_GROUP
+#define FMX_MATCH_GROUP 8
+#endif
+constexpr int kGroup = FMX_MATCH_GROUP;  // lanes per query (16 made the kernel 15% faster but register_scan slower)
+constexpr int kQPB = 256 / kGroup;  // queries per block: 256 threads, so every block of a scan is resident at once
 constexpr int kMatchThreads = kQPB * kGroup;  // 256
 #ifndef FMX_SMALL_CELL
 #define FMX_SMALL_CELL 2
@@ -234,7 +244,7 @@ constexpr int kMatchThreads = kQPB * kGroup;  // 256
 constexpr int kSmallCell = FMX_SMALL_CELL;  // neighbour cells with at most this many records: one lane folds them
 // Tiled pair sort: a tile = kTileBlocks match blocks of one type = 1024 queries, one
 // k_pair_scatter_t block; the match counts matches per (type, pair, tile).
-constexpr int kTileBlocks = 32;
+constexpr int kTileBlocks = 1024 / kQPB;
 constexpr int kTileQ = kTileBlocks * kQPB;  // 1024
 constexpr int kTileMaxPairs = 256;          // LDS bound of the tiled path (wider windows: per-block path)
 
@@ -466,9 +476,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
           best_i = oi;
         }
       };
-      static_assert(kGroup == 8 || kGroup == 16, "DPP reduction assumes 8- or 16-lane groups");
+      static_assert(kGroup == 4 || kGroup == 8 || kGroup == 16, "DPP reduction assumes 4-, 8- or 16-lane groups");
       if constexpr (kGroup == 16) step(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
-      step(std::integral_constant<int, 0x141>{});  // row_half_mirror
+      if constexpr (kGroup >= 8) step(std::integral_constant<int, 0x141>{});  // row_half_mirror
       step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
       step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
     };
@@ -1291,4 +1301,5 @@ void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
   }
 }
 
+}  // namespace FMX_VM_NS
 }  // namespace fmx
