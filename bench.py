@@ -55,8 +55,9 @@ def parse():
                     help="leave the registering thread unpinned (default: bound to the CPU it runs on for the "
                          "GPU measurements, released before the CPU baseline)")
     ap.add_argument("--subdiv", type=int, default=None, help="override voxel_subdivision (device map cells per voxel edge)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output); default "
+                         "profiles/traffic_latest.json (c4) or profiles/traffic_<workload>.json")
     return ap.parse_args()
 
 
@@ -93,6 +94,21 @@ def sum_over_ranks(x, world, local):
     t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def pmc_traffic(a, name):
+    """HBM bytes per launch of kernel class `name` from the committed PMC summary of this
+    workload (tools/gpu_pmc.sh, tools/gpu_c5pmc.sh), or None."""
+    path = a.traffic_json or os.path.join(
+        ROOT, "profiles", "traffic_latest.json" if a.workload == "c4" else f"traffic_{a.workload}.json")
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+        if tj.get("workload") == a.workload and name in tj.get("kernels", {}):
+            return tj["kernels"][name]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
 
 
 def pin_thread(world, local):
@@ -242,7 +258,7 @@ def run_c5(a, rank, world, local):
                    "parallelism": f"query shards x{world} + all_reduce"},
         "mpts_per_s": round(value * a.c5_queries / 1e6, 3),
         "roofline": dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                         frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
+                         frac=round(achieved / HBM_PEAK_GBS, 6), traffic=pmc_traffic(a, name),
                          avg_launch_us=round(avg_ms * 1e3, 3), alg_bytes_per_launch=bytes_per),
         "kernels_ms_per_step": {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()},
         "pose_error_vs_truth": err,
@@ -337,14 +353,7 @@ def main():
     avg_ms = d["ms"] / max(d["launches"], 1)
     bytes_per = d["bytes"] / max(d["launches"], 1)
     achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
-    try:
-        with open(a.traffic_json) as f:
-            tj = json.load(f)
-        if tj.get("workload") == a.workload and name in tj.get("kernels", {}):
-            traffic = tj["kernels"][name]["hbm_bytes_per_launch"]
-    except (OSError, ValueError):
-        pass
+    traffic = pmc_traffic(a, name)
     roof = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, avg_launch_us=round(avg_ms * 1e3, 3),
                 alg_bytes_per_launch=bytes_per)
