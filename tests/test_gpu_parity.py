@@ -119,6 +119,54 @@ def test_match_matches_oracle(fmx_mod, oracle, config, subdiv):
         assert np.array_equal((cpl if t == 0 else cpt), counts)
 
 
+def test_match_large_query_set_matches_oracle(fmx_mod, oracle):
+    """>= 128k queries: run_match takes the 4-lanes-per-query build (fmx::g4, the C5
+    path); same bit-exact contract as the 8-lane path above."""
+    feats = stream_features(oracle, "c2", 6)
+    p = feats[0]["params"]
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p)))
+    w = 0.8
+    omaps = [oracle.VoxelMap(w, 0), oracle.VoxelMap(w, 1)]
+    scans, poses = [], []
+    for k in range(5):
+        f = feats[k]
+        ctx.keypoints_add(k, f["planar"], f["point"])
+        omaps[0].add_scan(k, f["pose"], f["planar"])
+        omaps[1].add_scan(k, f["pose"], f["point"])
+        scans.append(k)
+        poses.append(f["pose"])
+    ctx.map_build(scans, np.stack(poses), w)
+    q = feats[5]
+    rng = np.random.default_rng(7)
+
+    def grow(a, n):  # jittered copies of the scan's features up to n queries
+        reps = -(-n // len(a))
+        b = np.concatenate([a] * reps)[:n].copy()
+        b[:, :3] += rng.normal(0.0, 0.03, (n, 3)).astype(b.dtype)
+        return b
+
+    Qpl, Qpt = grow(q["planar"], 120000), grow(q["point"], 20000)
+    assert len(Qpl) + len(Qpt) >= 128 * 1024
+    ctx.set_queries(Qpl, Qpt, 5)
+    Tj = perturb(q["pose"], np.random.default_rng(2), 0.005, 0.03)
+    cpl, cpt = ctx.match(Tj, w)
+    got = ctx.match_download()
+    npl = len(Qpl)
+    for t, (om, Q) in enumerate(zip(omaps, (Qpl, Qpt))):
+        ref = om.match(Q, Tj)
+        sl = slice(0, npl) if t == 0 else slice(npl, None)
+        acc_ref = ref["found"] & (ref["d2"] < w * w)
+        pair = got["pair"][sl]
+        assert np.array_equal(pair >= 0, acc_ref)
+        assert np.array_equal(pair[acc_ref].astype(np.uint64), ref["scan"][acc_ref])
+        assert np.array_equal(got["d2"][sl][acc_ref], ref["d2"][acc_ref])
+        assert np.array_equal(got["pi"][sl][acc_ref], ref["pi"][acc_ref])
+        if t == 0:
+            assert np.array_equal(got["ni"][acc_ref], ref["ni"][acc_ref])
+        counts = np.bincount(ref["scan"][acc_ref].astype(np.int64), minlength=5)
+        assert np.array_equal((cpl if t == 0 else cpt), counts)
+
+
 @pytest.mark.parametrize("single", [False, True])
 def test_linearize_matches_oracle(fmx_mod, oracle, single):
     rng = np.random.default_rng(7 + int(single))
