@@ -173,9 +173,12 @@ __global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec,
   const uint32_t o = atomicAdd(cursor + s, 1u);  // brick cell cursor
 #endif
   const double4 tp = tpos[rec];
-  pos[o] = make_double4(tp.x, tp.y, tp.z, (double)rec);  // .w: build order (k_match tie-break)
+  const uint32_t sg = rseg[rec];
+  // .w: build order (k_match tie-break) in the low 32 bits, the segment above them
+  // (exact in a double: < 2^53), so the match epilogue needs no seg[] lookup
+  pos[o] = make_double4(tp.x, tp.y, tp.z, (double)rec + 4294967296.0 * (double)sg);
   if (rec < n0) nrm[o] = tnrm[rec];
-  seg[o] = rseg[rec];
+  seg[o] = sg;
   rid[o] = rec;
 }
 
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     auto fold = [&](const double4& p, uint32_t i) {
       const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
       const double d2 = (dx * dx + dz * dz) + dy * dy;
-      const uint32_t rid = (uint32_t)p.w;
+      const uint32_t rid = (uint32_t)(unsigned long long)p.w;  // build order: the low 32 bits
       if (d2 <= best && (d2 < best || rid < best_rid)) {
         best = d2;
         best_rid = rid;
@@ -571,14 +574,14 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       int32_t pair = -1;
       double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
       if (found) {
-        const uint32_t sg = M.seg[best_i];
-        const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
         const double4 p = M.pos[best_i];
+        const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);  // in flight with p
+        const uint32_t sg = (uint32_t)((unsigned long long)p.w >> 32);     // the record's segment
+        const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
         double o[3];
         d_xform(Ti, p.x, p.y, p.z, o);
         pi = make_double4(o[0], o[1], o[2], 0.0);
         if (planar) {
-          const double4 n = M.nrm[best_i];
           d_rot(Ti, n.x, n.y, n.z, o);
           ni = make_double4(o[0], o[1], o[2], 0.0);
         }
