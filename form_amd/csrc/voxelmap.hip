@@ -244,6 +244,15 @@ constexpr int kMatchThreads = kQPB * kGroup;  // 256
 #ifndef FMX_SMALL_CELL
 #define FMX_SMALL_CELL 2
 #endif
+#ifndef FMX_MATCH_SPEC_FACES
+#define FMX_MATCH_SPEC_FACES 1
+#endif
+// face probes issued with the own-voxel probe (needs >= 7 lanes per query)
+constexpr bool kSpecFaces = FMX_MATCH_SPEC_FACES && kGroup >= 8;
+#ifndef FMX_MATCH_SPEC_FRAC
+#define FMX_MATCH_SPEC_FRAC 0.15
+#endif
+constexpr double kSpecFrac = FMX_MATCH_SPEC_FRAC;  // only faces nearer than this fraction of a cell
 constexpr int kSmallCell = FMX_SMALL_CELL;  // neighbour cells with at most this many records: one lane folds them
 // Tiled pair sort: a tile = kTileBlocks match blocks of one type = 1024 queries, one
 // k_pair_scatter_t block; the match counts matches per (type, pair, tile).
@@ -486,11 +495,41 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
     };
     const bool inr = key_in_range(bx, by, bz);
+    // lower bound on d^2 from the query to any point of the cell at shift s
+    auto shift_lb = [&](int s) {
+      double lb = 0.0;
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        const int sa = c_shift[s][ax];
+        const double e = sa > 0 ? hi[ax] + (sa - 1) * a.w : (sa < 0 ? lo[ax] + (-sa - 1) * a.w : 0.0);
+        const double m = fmax(e - 1e-9, 0.0);
+        lb += m * m;
+      }
+      return lb;
+    };
+    // face cells probed speculatively by lanes 1..6 alongside lane 0's own-voxel
+    // probe (one bucket-load latency instead of two); the face pass below still
+    // applies the same bound test, so the cells walked and the result are unchanged
+    uint32_t sf = 0, sc = 0;
+    double slb = INFINITY;
     // phase 1: the query's own voxel (shift 0, visited first by the reference too),
     // its records split over the group's lanes
     if (inr) {
-      uint32_t first, count;
-      if (g == 0) probe(0, 0, 0, first, count);
+      uint32_t first = 0, count = 0;
+      if constexpr (kSpecFaces) {
+        const bool face = g >= 1 && g <= 6;
+        const double lb = face ? shift_lb(g) : 0.0;
+        if (g == 0 || (face && lb <= best && lb <= kSpecFrac * kSpecFrac * a.w * a.w)) {
+          probe(c_shift[g][0], c_shift[g][1], c_shift[g][2], first, count);
+          if (face) {
+            sf = first;
+            sc = count;
+            slb = lb;
+          }
+        }
+      } else {
+        if (g == 0) probe(0, 0, 0, first, count);
+      }
       first = __shfl(first, 0, kGroup);
       count = __shfl(count, 0, kGroup);
       n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
@@ -506,22 +545,21 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     // a pass a lane bounds and probes its shifts in parallel, then the group walks
     // every surviving cell together (records split over the lanes), re-checking each
     // bound against the shared best.
-    auto pass = [&](int s_begin, int s_end) {
+    auto pass = [&](int s_begin, int s_end, bool spec) {
       for (int s0 = s_begin; s0 < s_end; s0 += kGroup) {  // one shift per lane per chunk
         uint32_t vf = 0, vc = 0;
         double vlb = INFINITY;
         const int s = s0 + g;
-        if (inr && s < s_end) {
-          const int sh[3] = {c_shift[s][0], c_shift[s][1], c_shift[s][2]};
-          double lb = 0.0;
-#pragma unroll
-          for (int ax = 0; ax < 3; ++ax) {
-            const double e = sh[ax] > 0 ? hi[ax] + (sh[ax] - 1) * a.w : (sh[ax] < 0 ? lo[ax] + (-sh[ax] - 1) * a.w : 0.0);
-            const double m = fmax(e - 1e-9, 0.0);
-            lb += m * m;
+        if (spec) {  // faces already probed in phase 1 (lane g holds shift g)
+          if (slb <= best) {
+            vf = sf;
+            vc = sc;
+            vlb = slb;
           }
+        } else if (inr && s < s_end) {
+          const double lb = shift_lb(s);
           if (lb <= best) {  // else conservative: no point inside can win
-            probe(sh[0], sh[1], sh[2], vf, vc);
+            probe(c_shift[s][0], c_shift[s][1], c_shift[s][2], vf, vc);
             vlb = lb;
           }
         }
@@ -560,12 +598,12 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         }
       }
     };
-    pass(1, 7);
+    pass(1, 7, kSpecFaces);
 #ifdef FMX_MATCH_TIMING
     mtime[2] = wall_clock64();
 #endif
-    pass(7, 27);
-    if (a.rings >= 2) pass(27, 125);
+    pass(7, 27, false);
+    if (a.rings >= 2) pass(27, 125, false);
 #ifdef FMX_MATCH_TIMING
     mtime[3] = wall_clock64();
 #endif
