@@ -245,9 +245,10 @@ constexpr int kMatchThreads = kQPB * kGroup;  // 256
 #define FMX_SMALL_CELL 2
 #endif
 #ifndef FMX_MATCH_SPEC_FACES
-#define FMX_MATCH_SPEC_FACES 1
+#define FMX_MATCH_SPEC_FACES 0
 #endif
-// face probes issued with the own-voxel probe (needs >= 7 lanes per query)
+// face probes issued with the own-voxel probe (needs >= 7 lanes per query); measured
+// no faster, off by default
 constexpr bool kSpecFaces = FMX_MATCH_SPEC_FACES && kGroup >= 8;
 #ifndef FMX_MATCH_SPEC_FRAC
 #define FMX_MATCH_SPEC_FRAC 0.15
@@ -550,11 +551,17 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         uint32_t vf = 0, vc = 0;
         double vlb = INFINITY;
         const int s = s0 + g;
-        if (spec) {  // faces already probed in phase 1 (lane g holds shift g)
+        if (spec) {  // lane g holds face g: probed in phase 1 if it was near, else now
           if (slb <= best) {
             vf = sf;
             vc = sc;
             vlb = slb;
+          } else if (inr && g >= 1 && g <= 6 && slb == INFINITY) {
+            const double lb = shift_lb(g);
+            if (lb <= best) {
+              probe(c_shift[g][0], c_shift[g][1], c_shift[g][2], vf, vc);
+              vlb = lb;
+            }
           }
         } else if (inr && s < s_end) {
           const double lb = shift_lb(s);
