@@ -78,8 +78,13 @@ def test_extract_edge_cases(fmx_mod, oracle):
     assert np.array_equal(got["point_index"], ref["point_idx"])
 
 
-@pytest.mark.parametrize("config,subdiv", [("tiny", 2), ("c2", 2), ("c2", 1)])
-def test_match_matches_oracle(fmx_mod, oracle, config, subdiv):
+@pytest.mark.parametrize("config,subdiv,rot,trans", [("tiny", 2, 0.005, 0.03), ("c2", 2, 0.005, 0.03),
+                                                     ("c2", 1, 0.005, 0.03), ("c2", 1, 0.02, 0.35),
+                                                     ("c2", 2, 0.02, 0.35)])
+def test_match_matches_oracle(fmx_mod, oracle, config, subdiv, rot, trans):
+    """Bit-exact match against the oracle.  The far-perturbed cases put many nearest
+    neighbours in a neighbouring cell (faces, edges, corners, ring 2), where the
+    kernel's pruned passes must still visit every cell that can win."""
     feats = stream_features(oracle, config, 6)
     p = feats[0]["params"]
     ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p),
@@ -97,7 +102,7 @@ def test_match_matches_oracle(fmx_mod, oracle, config, subdiv):
     ctx.map_build(scans, np.stack(poses), w)
     q = feats[5]
     ctx.set_queries(q["planar"], q["point"], 5)
-    Tj = perturb(q["pose"], np.random.default_rng(1), 0.005, 0.03)
+    Tj = perturb(q["pose"], np.random.default_rng(1), rot, trans)
     cpl, cpt = ctx.match(Tj, w)
     got = ctx.match_download()
     npl = len(q["planar"])
