@@ -1361,8 +1361,7 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   // reach, and the kept lists fit the dead point area of LDS
   const int pps = C / a.S;
   const size_t nwd = (size_t)(C + 63) / 64 + 1;
-  static const bool seq_sel = std::getenv("FMX_SEQ_SECTORS") != nullptr;  // A/B / test switch
-  const bool par = !seq_sel && pps <= 512 && a.S <= 16 && pps >= 2 * a.k &&
+  const bool par = pps <= 512 && a.S <= 16 && pps >= 2 * a.k &&
                    8 * (size_t)C + 8 * nwd + 4 * (size_t)a.S * (a.P + 1) <= 16 * (size_t)C;
   {
     ProfScope ps(c->prof, PROF_EXTRACT_ROWS, 16.0 * N + N, st);
@@ -1385,13 +1384,12 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   FMX_HIP(hipGetLastError());
   const int nslots = R * a.cap_pl;
   const int nblk = (C + 63) / 64;
-  static const bool split_normals = std::getenv("FMX_SPLIT_NORMALS") != nullptr;  // A/B / test switch
   // k_normals: one workgroup per line, rows r-1..r+1 in LDS (160 KB per CU, minus
   // the kernel's few static bytes)
   const size_t lds_n = (size_t)3 * (C + (C >> 6) + 1) * 16 + (size_t)4 * nblk * 16 + (size_t)a.cap_pl * 20 +
                        (size_t)a.cap_pl * nblk * 4;
   constexpr size_t kNrmLdsMax = 160 * 1024 - 256;
-  if (C <= kNrmMaxC && lds_n <= kNrmLdsMax && !split_normals) {
+  if (C <= kNrmMaxC && lds_n <= kNrmLdsMax) {
     if (!c->nrm_attr_set) {
       FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_normals<5>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNrmLdsMax));

@@ -25,23 +25,17 @@ namespace fmx {
 // C4 scan's ~4e4 queries: more lanes shorten each query's chain of dependent loads),
 // 4 for large sets (>= 128k queries, e.g. C5's 2M): they run in several waves of
 // blocks, so more queries per wave raise the loads in flight (C5 match 1.42 -> 1.04 ms,
-// C4 8 lanes 0.22 vs 4 lanes 0.28 ms per scan).  FMX_MATCH_LANES=4|8 forces one.
+// C4 8 lanes 0.22 vs 4 lanes 0.28 ms per scan).
 int match_group_for(uint64_t nq) {
-  static const int forced = [] {
-    const char* e = std::getenv("FMX_MATCH_LANES");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced == 4 || forced == 8) return forced;
   return nq >= (128u << 10) ? 4 : 8;
 }
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, hipStream_t st) {
   g8::run_map_build(c, scans, poses34, w, st);  // the same build in both variants
 }
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, const IcpDev* icp,
-               bool sorted) {
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted) {
   c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt);
-  if (c->match_group == 4) g4::run_match(c, pose_j34, max_dist, min_dist_map, icp, sorted);
-  else g8::run_match(c, pose_j34, max_dist, min_dist_map, icp, sorted);
+  if (c->match_group == 4) g4::run_match(c, pose_j34, max_dist, min_dist_map, sorted);
+  else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted);
 }
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
   if (c->match_group == 4) g4::run_insert(c, scan, n_inserted);
@@ -53,8 +47,8 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
 }
 
 // ============================================================================ profiling
-static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest", "fit",      "compact",   "map_build",
-                                             "match",        "pair_sort", "linearize", "lin_final", "error_eval", "insert", "window"};
+static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest",   "fit",       "compact", "map_build",
+                                             "match",        "pair_sort", "linearize", "insert",  "window"};
 
 ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), bytes(by), st(s) {
   if (!pr.on) return;
@@ -509,22 +503,16 @@ LinF fast_linear(const fmx_ctx::Est& e) {
   return L;
 }
 
-// The window graph's pair linearization: split (launch, host terms, wait) unless
-// FMX_LIN_SERIAL (A/B: launch and wait back to back, host terms after).
+// The window graph's pair linearization in split form: launch, the host assembles the
+// non-pair terms, then wait.
 template <class B, class E>
 void set_lin(WinGraph& g, B begin, E end) {
-  static const bool serial = std::getenv("FMX_LIN_SERIAL") != nullptr;
   g.lin_pairs = [begin, end](const std::vector<Pose>& x, double* G) {
     begin(x);
     end(G);
   };
-  if (serial) {
-    g.lin_begin = nullptr;
-    g.lin_end = nullptr;
-  } else {
-    g.lin_begin = begin;
-    g.lin_end = end;
-  }
+  g.lin_begin = begin;
+  g.lin_end = end;
 }
 
 // ICP loop (form.cpp:67-89) + optimize(false) (form.cpp:92-93) in smoothing mode:
@@ -547,7 +535,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
   for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
     ++icp;
     const Pose before = e.values.at(j);
-    run_match(c, before.m, P.max_dist_matching, P.min_dist_map, nullptr, true);  // pair-major
+    run_match(c, before.m, P.max_dist_matching, P.min_dist_map, true);  // pair-major
     // get_graph(true): the current scan's K pairs (empty ones linearize to zero)
     g.pairs.clear();
     for (uint32_t k = 0; k < c->K; ++k) g.pairs.push_back({slot.at(c->map_scans[k]), slot.at(j)});
@@ -776,19 +764,9 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   // The map build goes to the side stream and is queued while the extraction kernels
   // run (extraction occupies one CU per scan line, so the build's kernels take the
   // idle CUs, and its host launch cost hides behind the extraction wait).
-  // FMX_MAP_INLINE: build on the main stream first (A/B).
-  static const bool inline_map = std::getenv("FMX_MAP_INLINE") != nullptr;
   fmx_feature_counts fc{};
-  if (inline_map) {
-    prepare();
-    {
-      HostScope hs_map(3);
-      run_map_build(c, scans, poses.data(), P.max_dist_matching);
-    }
-    HostScope hs_ex(2);
-    do_extract(c, xyzw, n, j, on_dev, &fc);
-  } else {
-    FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
+  FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
+  {
     HostScope hs_ex(2);
     do_extract(c, xyzw, n, j, on_dev, &fc, [&] {
       prepare();
@@ -797,16 +775,15 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
       FMX_HIP(hipEventRecord(c->ev_join, c->side));
     });
-    FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   }
+  FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   auto& cj = e.cons[j];
   HostScope* hs_icp = new HostScope(4);
   uint64_t icp = 0, lm_it = 0, lins = 0;
   bool inserted = false;
-  static const bool host_lm = std::getenv("FMX_DEVICE_LM") == nullptr;  // default: host LM
   if (!P.disable_smoothing) {
     smooth_register(c, e, j, icp, lm_it, lins, inserted);
-  } else if (host_lm) {
+  } else {
     // ICP loop (form.cpp:67-89) with the LM on the host (one sync per linearization)
     DeviceLM lm{c, e, P.planar_constraint_sigma};
     bool converged = false;
@@ -814,7 +791,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
       ++icp;
       const Pose before = e.values.at(j);
-      run_match(c, before.m, P.max_dist_matching, P.min_dist_map, nullptr, false);  // query order
+      run_match(c, before.m, P.max_dist_matching, P.min_dist_map, false);  // query order
       int li = 0;
       const Pose after = lm.optimize(before, &li);
       lm_it += li;
@@ -841,51 +818,6 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       lm_it += li;
     }
     lins = lm.linearizations;
-  } else {
-    // ICP loop on the device (IcpDev): per iteration the host enqueues begin ->
-    // match -> pair sort -> kRounds x (linearize, LM step) -> end, then reads the
-    // ~0.5 KB state back once.  Kernels of a converged loop exit immediately.
-    constexpr int kRounds = 4;
-    c->icp.ensure(1);
-    c->h_icp.ensure(1);
-    IcpDev& hs = *c->h_icp.p;
-    std::memset(&hs, 0, sizeof(hs));
-    std::memcpy(hs.Tcur, e.values.at(j).m, sizeof(hs.Tcur));
-    hs.ended = -1;
-    hs.K = (int32_t)c->K;
-    FMX_HIP(hipMemcpyAsync(c->icp.p, &hs, sizeof(IcpDev), hipMemcpyHostToDevice, c->stream));
-    // the state comes back through pinned mapped memory (h_icp) behind a flag
-    auto readback = [&](bool end) { icp_launch(c, end ? 1 : 3); };
-    for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
-      icp_launch(c, 0);
-      run_match(c, nullptr, P.max_dist_matching, P.min_dist_map, c->icp.p, false);
-      lm_rounds(c, kRounds);
-      readback(true);
-      for (int more = 0; !hs.icp_done && hs.phase != 2; ++more) {  // LM needs more rounds
-        if (more > 40)  // 160 rounds > GTSAM's 100 LM iterations: the state machine is stuck
-          throw StatusError(FMX_E_STATE, "device LM made no progress (phase " + std::to_string(hs.phase) +
-                                             ", lins " + std::to_string(hs.lins) + ", lm_iters " +
-                                             std::to_string(hs.lm_iters) + ")");
-        lm_rounds(c, kRounds);
-        readback(true);
-      }
-      if (hs.icp_done) break;
-    }
-    if (!hs.icp_done) {  // optimize(false) from the last updated pose
-      icp_launch(c, 2);
-      for (int more = 0; hs.phase != 2; ++more) {
-        if (more > 40) throw StatusError(FMX_E_STATE, "device LM made no progress (final optimize)");
-        lm_rounds(c, kRounds);
-        readback(false);
-      }
-      hs.lm_total += hs.lm_iters;
-    }
-    Pose Tf;
-    std::memcpy(Tf.m, hs.T, sizeof(Tf.m));
-    e.values[j] = Tf;
-    icp = (uint64_t)hs.icp_iters;
-    lm_it = (uint64_t)hs.lm_total;
-    lins = (uint64_t)hs.lins;
   }
   delete hs_icp;
   HostScope hs_tail(5);
@@ -1010,12 +942,12 @@ void fmx_destroy(fmx_ctx* c) {
     M.rseg.release(); M.pos.release(); M.nrm.release(); M.seg.release(); M.rid.release();
   }
   c->h_mapposes.release(); c->map_blob.release();
-  c->blk_lo.release(); c->blk_hi.release(); c->icp.release(); c->h_icp.release(); c->h_work.release();
+  c->blk_lo.release(); c->blk_hi.release(); c->h_work.release();
   c->work.release(); c->pair_base.release();
   c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();
   c->hist.release(); c->hist_off.release(); c->thist.release(); c->c_pl.release(); c->c_pt.release(); c->pair_counts.release();
-  c->chunk_range.release(); c->chunks.release(); c->n_chunks.release(); c->poses_ij.release();
-  c->partials.release(); c->G.release(); c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
+  c->chunk_range.release(); c->chunks.release(); c->n_chunks.release();
+  c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
   {
@@ -1187,7 +1119,7 @@ fmx_status fmx_linearize(fmx_ctx* c, const double* pi, const double* pj, double 
   return guard(c, [&] {
     if (!(sigma > 0)) throw StatusError(FMX_E_INVAL, "sigma must be > 0");
     if (c->K && (!pi || !pj)) throw StatusError(FMX_E_INVAL, "null poses");
-    run_linearize(c, pi, pj, sigma, single ? 1 : 0, G, err);
+    win_linearize_pairs(c, pi, pj, sigma, single ? 1 : 0, G, err);
   });
 }
 
@@ -1195,7 +1127,16 @@ fmx_status fmx_error(fmx_ctx* c, const double* pi, const double* pj, double sigm
   return guard(c, [&] {
     if (!(sigma > 0)) throw StatusError(FMX_E_INVAL, "sigma must be > 0");
     if (c->K && (!pi || !pj)) throw StatusError(FMX_E_INVAL, "null poses");
-    run_linearize(c, pi, pj, sigma, 2, nullptr, err);
+    win_linearize_pairs(c, pi, pj, sigma, 2, nullptr, err);
+  });
+}
+
+fmx_status fmx_linearize_matched(fmx_ctx* c, const double pose_j[12], double sigma, double out[29]) {
+  return guard(c, [&] {
+    if (!(sigma > 0)) throw StatusError(FMX_E_INVAL, "sigma must be > 0");
+    if (!pose_j || !out) throw StatusError(FMX_E_INVAL, "null pose / output");
+    if (!c->have_match) throw StatusError(FMX_E_STATE, "no match results");
+    run_linearize_total(c, pose_j, sigma, out);
   });
 }
 

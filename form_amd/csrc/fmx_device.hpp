@@ -74,7 +74,10 @@ __device__ __forceinline__ T wave_sum(T v) {
 // (buffer_wbl2) would write back every dirty L2 line of the XCD instead.  Plain
 // stores to host memory CAN sit in L2: with plain payload stores and no fence the
 // host once read stale totals behind a fresh word.  Call publish_flag from ONE lane
-// of the wave that made every host_store it covers.
+// of the wave that made every host_store it covers — or, when several waves / blocks
+// made them (k_win_linearize's pair finishers), after each of those waves waited for
+// its own write-through stores (vmcnt(0): acknowledged = left the GPU caches) BEFORE
+// the barrier / agent-scope ticket that orders it ahead of the publishing wave.
 __device__ __forceinline__ void host_store(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -244,14 +247,6 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {  // splitmix64 finalizer
   k ^= k >> 31;
   return k;
 }
-
-// Hash slot: {key, first record, record count}; 16 B, one probe = one 16-B load.
-// (FMX_MAP_SLOTS build: one slot per voxel.)
-struct alignas(16) Slot {
-  unsigned long long key;
-  uint32_t first;
-  uint32_t count;
-};
 
 // Brick: the 2 x 2 x 2 cells (x, y, z) >> 1 of one 64-B bucket — the 27-cell
 // neighbourhood of any cell lies in at most 8 bricks, and neighbouring queries share

@@ -101,8 +101,6 @@ enum ProfId {
   PROF_MATCH,
   PROF_PAIR_SORT,
   PROF_LINEARIZE,
-  PROF_LIN_FINAL,
-  PROF_ERROR,
   PROF_INSERT,
   PROF_WINDOW,
   PROF_COUNT
@@ -143,7 +141,7 @@ struct Pool {
 // range-error word; records (build order and voxel-sorted) planar [0, n[0]) then
 // point [n[0], n[0] + n[1]); normals for planar records only.
 struct VoxMap {
-  DBuf<uint4> table;            // fmx::Brick (fmx::Slot in the FMX_MAP_SLOTS build)
+  DBuf<uint4> table;            // fmx::Brick
   DBuf<uint32_t> bcnt, bcur;    // per brick cell: record count, scatter cursor (build only)
   uint64_t cap[2] = {0, 0};     // powers of two
   uint32_t n[2] = {0, 0};
@@ -158,23 +156,6 @@ struct Seg {
   uint32_t n;         // records
   uint32_t pool_off;  // offset in the pool
   uint32_t pad;
-};
-
-// Device-resident ICP + LM state (single-pose mode), one per context (icp.hip).
-struct IcpDev {
-  double Tcur[12];     // X(j) estimate (ConstraintManager::update_current_pose)
-  double Tbefore[12];  // pose this ICP iteration matched at
-  double T[12];        // LM: current values
-  double Tn[12];       // LM: trial values
-  double H[36], g[6], c, err, lambda, cur, linchg;
-  int32_t phase;       // LM: 0 linearize at T, 1 trial pending (linearize at Tn), 2 done
-  int32_t lm_iters;    // iterations of the running LM
-  int32_t lm_total;    // LM iterations this scan
-  int32_t lins;        // linearizations this scan
-  int32_t icp_iters;
-  int32_t icp_done;    // ICP converged (form.cpp:86-88 break)
-  int32_t ended;       // icp_iters value the end kernel last processed
-  int32_t K;
 };
 
 struct Chunk {
@@ -314,7 +295,7 @@ struct fmx_ctx {
   bool lds_attr_set = false;
 
   // ---- linearize
-  fmx::DBuf<double> poses_ij, partials, G, bpart;  // bpart: k_linearize_total block partials
+  fmx::DBuf<double> bpart;                        // k_linearize_total block partials
   fmx::DBuf<uint32_t> ticket;                     // its last-block ticket
   fmx::DBuf<uint32_t> mcnt, mticket;              // query-order match: per-pair counters + ticket
   fmx::DBuf<uint32_t> ins_blk, ins_off;           // per match block insert counts / offsets
@@ -326,10 +307,6 @@ struct fmx_ctx {
   bool have_qo = false;
   fmx::HBuf<double> h_poses, h_G;
   fmx::HBuf<int32_t> h_i32;
-
-  // ---- device ICP/LM state
-  fmx::DBuf<fmx::IcpDev> icp;
-  fmx::HBuf<fmx::IcpDev> h_icp;
 
   // ---- smoothing-mode window store
   fmx::WinStore win;
@@ -379,21 +356,10 @@ struct HostScope {
   }
 };
 
-// Wait for the context stream: hipStreamQuery spin (default) or, FMX_SYNC=sync,
-// hipStreamSynchronize.  An isolated empty-kernel round trip favours the latter
-// (11.5 vs 52 us, tools/apibench), but register_scan measures 4-5 % faster with the
-// spin (best of 3, C4), so the spin stays the default.
+// Wait for the context stream with a hipStreamQuery spin (hipStreamSynchronize's
+// blocking wake-up measured 4-5 % slower on register_scan, C4).
 inline void stream_wait(fmx_ctx* c) {
   HostScope hs(1);
-  static const bool query = [] {
-    const char* s = std::getenv("FMX_SYNC");
-    return !(s && std::string(s) == "sync");
-  }();
-  if (!query) {
-    const hipError_t e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) throw HipError(std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
-    return;
-  }
   for (;;) {
     const hipError_t e = hipStreamQuery(c->stream);
     if (e == hipSuccess) return;
@@ -434,7 +400,7 @@ inline uint32_t next_flag(fmx_ctx* c) {
   void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, \
                      hipStream_t st = nullptr);                                                      \
   void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,            \
-                 const IcpDev* icp = nullptr, bool sorted = true);                                   \
+                 bool sorted = true);                                                                \
   void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);                                  \
   void match_counts_fetch(fmx_ctx* c, bool wait = true);
 namespace g8 { FMX_VM_DECLS }
@@ -447,23 +413,14 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
 // stream so the build overlaps extraction)
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w,
                    hipStream_t st = nullptr);
-// icp != null: pose from the device ICP state.  sorted: bucket the accepted matches
-// pair-major into SoA correspondences (fmx_match / fmx_linearize); otherwise only the
-// per-pair counts are produced and register_scan linearizes in query order.
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,
-               const IcpDev* icp = nullptr, bool sorted = true);
+// sorted: bucket the accepted matches pair-major into SoA correspondences (fmx_match /
+// fmx_linearize, the smoothing mode); otherwise only the per-pair counts are produced
+// and the single-pose mode linearizes in query order.
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted = true);
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
 // wait = false: the caller knows the match kernel has completed (a later kernel in
 // stream order published a flag)
 void match_counts_fetch(fmx_ctx* c, bool wait = true);
-// 0 begin ICP iteration, 1 end ICP iteration + state to host (waits), 2 begin final LM,
-// 3 state to host (waits)
-void icp_launch(fmx_ctx* c, int what);
-void lm_rounds(fmx_ctx* c, int rounds);
-void run_linearize(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
-                   double* G_out, double* err_out);
-// single-pose fast path: Ti = the built map's poses (device), Tj by value (no upload)
-void run_linearize_mapj(fmx_ctx* c, const double* pose_j34, double sigma, int mode, double* G_out, double* err_out);
 // out[0..27]: summed single-pose system over all pairs at pose_j; out[28]: error
 void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, double* out);
 void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
@@ -477,4 +434,7 @@ void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vecto
 void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out);
 void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
 void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* called with G_out = null
+// fmx_linearize / fmx_error on k_win_linearize: mode 0 13 x 13 (91), 1 single-pose 7 x 7 (28), 2 errors only
+void win_linearize_pairs(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
+                         double* G_out, double* err_out);
 }  // namespace fmx

@@ -357,12 +357,11 @@ __attribute__((target("avx512f,fma"))) double dot_512(const double* p, const dou
   return _mm512_reduce_add_pd(acc);
 }
 
-// 0 plain, 1 AVX2+FMA, 2 AVX-512 (FMX_CHOL_PLAIN / FMX_CHOL_AVX2 force the lower ones)
+// 0 plain, 1 AVX2+FMA, 2 AVX-512: the host CPU's widest
 int simd_level() {
   static const int lv = [] {
-    if (std::getenv("FMX_CHOL_PLAIN")) return 0;
     const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
-    if (avx2 && __builtin_cpu_supports("avx512f") && !std::getenv("FMX_CHOL_AVX2")) return 2;
+    if (avx2 && __builtin_cpu_supports("avx512f")) return 2;
     return avx2 ? 1 : 0;
   }();
   return lv;

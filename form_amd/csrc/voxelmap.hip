@@ -62,8 +62,7 @@ struct BuildArgs {
   const double* poses;
   uint32_t n0, n;  // planar records, all records
   double w;
-  Slot* table;      // FMX_MAP_SLOTS
-  Brick* bricks;    // brick layout (default)
+  Brick* bricks;
   uint32_t* bcnt;   // [brick][8] record counts
   uint64_t mask[2];
   uint64_t off1;  // first point slot / brick
@@ -100,19 +99,6 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
     a.rslot[rec] = 0xFFFFFFFFu;
     return;
   }
-#ifdef FMX_MAP_SLOTS
-  const unsigned long long key = pack_key(cx, cy, cz);
-  Slot* table = a.table + (t == 0 ? 0 : a.off1);
-  const uint64_t mask = a.mask[t];
-  uint64_t h = mix64(key) & mask;
-  for (;;) {
-    const unsigned long long prev = atomicCAS(&table[h].key, 0ull, key);
-    if (prev == 0ull || prev == key) break;
-    h = (h + 1) & mask;
-  }
-  atomicAdd(&table[h].count, 1u);
-  a.rslot[rec] = (uint32_t)((t == 0 ? 0 : a.off1) + h);
-#else
   const unsigned long long key = brick_key(cx, cy, cz);
   Brick* bricks = a.bricks + (t == 0 ? 0 : a.off1);
   const uint64_t mask = a.mask[t];
@@ -125,17 +111,8 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   const uint32_t cell = (uint32_t)(((t == 0 ? 0 : a.off1) + h) * 8 + brick_cell(cx, cy, cz));
   atomicAdd(a.bcnt + cell, 1u);
   a.rslot[rec] = cell;
-#endif
 }
 
-struct CountIn {
-  const Slot* t;
-  __device__ uint32_t operator()(size_t i) const { return t[i].count; }
-};
-struct FirstOut {
-  Slot* t;
-  __device__ void operator()(size_t i, uint32_t v) const { t[i].first = v; }
-};
 // Brick layout: scanned over [brick][cell] (+ one zero entry past the end), the
 // prefix is cell (i / 8, i % 8)'s first record, the scatter cursor, and the previous
 // brick's end marker beg[8] at every brick boundary.
@@ -159,7 +136,7 @@ struct BrickFirstOut {
 __global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec, const uint32_t* __restrict__ rslot,
                                                      const uint32_t* __restrict__ rseg,
                                                      const double4* __restrict__ tpos,
-                                                     const double4* __restrict__ tnrm, Slot* __restrict__ table,
+                                                     const double4* __restrict__ tnrm,
                                                      uint32_t* __restrict__ cursor,
                                                      double4* __restrict__ pos, double4* __restrict__ nrm,
                                                      uint32_t* __restrict__ seg, uint32_t* __restrict__ rid) {
@@ -167,11 +144,7 @@ __global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec,
   if (rec >= nrec) return;
   const uint32_t s = rslot[rec];
   if (s == 0xFFFFFFFFu) return;
-#ifdef FMX_MAP_SLOTS
-  const uint32_t o = atomicAdd(&table[s].first, 1u);
-#else
   const uint32_t o = atomicAdd(cursor + s, 1u);  // brick cell cursor
-#endif
   const double4 tp = tpos[rec];
   const uint32_t sg = rseg[rec];
   // .w: build order (k_match tie-break) in the low 32 bits, the segment above them
@@ -183,8 +156,7 @@ __global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec,
 }
 
 struct MapView {
-  const Slot* table;    // FMX_MAP_SLOTS
-  const Brick* bricks;  // brick layout
+  const Brick* bricks;
   uint64_t mask;
   const double4* pos;
   const double4* nrm;
@@ -244,16 +216,6 @@ constexpr int kMatchThreads = kQPB * kGroup;  // 256
 #ifndef FMX_SMALL_CELL
 #define FMX_SMALL_CELL 2
 #endif
-#ifndef FMX_MATCH_SPEC_FACES
-#define FMX_MATCH_SPEC_FACES 0
-#endif
-// face probes issued with the own-voxel probe (needs >= 7 lanes per query); measured
-// no faster, off by default
-constexpr bool kSpecFaces = FMX_MATCH_SPEC_FACES && kGroup >= 8;
-#ifndef FMX_MATCH_SPEC_FRAC
-#define FMX_MATCH_SPEC_FRAC 0.15
-#endif
-constexpr double kSpecFrac = FMX_MATCH_SPEC_FRAC;  // only faces nearer than this fraction of a cell
 constexpr int kSmallCell = FMX_SMALL_CELL;  // neighbour cells with at most this many records: one lane folds them
 // Tiled pair sort: a tile = kTileBlocks match blocks of one type = 1024 queries, one
 // k_pair_scatter_t block; the match counts matches per (type, pair, tile).
@@ -371,18 +333,13 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
                                                          int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
                                                          double4* __restrict__ m_pi, double4* __restrict__ m_ni,
                                                          uint8_t* __restrict__ m_ins, uint32_t* __restrict__ hist,
-                                                         uint32_t* __restrict__ work, const IcpDev* __restrict__ icp,
+                                                         uint32_t* __restrict__ work,
                                                          uint32_t* __restrict__ mcnt, uint32_t* __restrict__ mticket,
                                                          uint32_t* __restrict__ host_counts,
                                                          uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off,
                                                          uint32_t* __restrict__ thist, SortOut so) {
   extern __shared__ uint32_t s_hist[];  // [K]
-#ifdef FMX_MATCH_TIMING
-  uint64_t mtime[6];
-  mtime[0] = wall_clock64();
-#endif
-  if (icp && icp->icp_done) return;  // device ICP loop already converged
-  const double* Tj = icp ? icp->Tbefore : a.Tj;
+  const double* Tj = a.Tj;
   const bool planar = blockIdx.x < a.nb_pl;
   const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kQPB + threadIdx.x / kGroup;
   const int g = threadIdx.x % kGroup;
@@ -403,25 +360,6 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     const double hi[3] = {(bx + 1) * a.w - wq[0], (by + 1) * a.w - wq[1], (bz + 1) * a.w - wq[2]};
     double best = a.bound;
     uint32_t best_rid = 0xFFFFFFFFu, best_i = 0xFFFFFFFFu;
-#ifdef FMX_MAP_SLOTS
-    auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count) {
-      const unsigned long long key = pack_key(bx + sx, by + sy, bz + sz);
-      uint64_t h = mix64(key) & M.mask;
-      first = 0;
-      count = 0;
-      for (;;) {
-        ++n_probe;
-        const Slot sl = M.table[h];
-        if (sl.key == key) {
-          first = sl.first - sl.count;
-          count = sl.count;
-          return;
-        }
-        if (sl.key == 0ull) return;
-        h = (h + 1) & M.mask;
-      }
-    };
-#else
     // one bucket read per probe: key and the cell's two boundaries in flight together
     auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count) {
       const int X = bx + sx, Y = by + sy, Z = bz + sz;
@@ -444,7 +382,6 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         h = (h + 1) & M.mask;
       }
     };
-#endif
     // a record is one double4: world position + its build order in .w (exact in a
     // double), so a candidate test is one 32-B load
     auto fold = [&](const double4& p, uint32_t i) {
@@ -508,69 +445,35 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       }
       return lb;
     };
-    // face cells probed speculatively by lanes 1..6 alongside lane 0's own-voxel
-    // probe (one bucket-load latency instead of two); the face pass below still
-    // applies the same bound test, so the cells walked and the result are unchanged
-    uint32_t sf = 0, sc = 0;
-    double slb = INFINITY;
     // phase 1: the query's own voxel (shift 0, visited first by the reference too),
     // its records split over the group's lanes
     if (inr) {
       uint32_t first = 0, count = 0;
-      if constexpr (kSpecFaces) {
-        const bool face = g >= 1 && g <= 6;
-        const double lb = face ? shift_lb(g) : 0.0;
-        if (g == 0 || (face && lb <= best && lb <= kSpecFrac * kSpecFrac * a.w * a.w)) {
-          probe(c_shift[g][0], c_shift[g][1], c_shift[g][2], first, count);
-          if (face) {
-            sf = first;
-            sc = count;
-            slb = lb;
-          }
-        }
-      } else {
-        if (g == 0) probe(0, 0, 0, first, count);
-      }
+      if (g == 0) probe(0, 0, 0, first, count);
       first = __shfl(first, 0, kGroup);
       count = __shfl(count, 0, kGroup);
       n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
       scan_range(first, count);
     }
     group_min();  // every lane now holds the own-voxel best: the bound for phase 2
-#ifdef FMX_MATCH_TIMING
-    mtime[1] = wall_clock64();
-#endif
     // phase 2: the neighbour cells in passes of increasing lower bound — ring-1 faces
     // (shifts 1..6), ring-1 edges + corners (7..26), then ring 2 (27..124) when the
     // map uses half-width cells — each pass pruned against the best found so far.  In
     // a pass a lane bounds and probes its shifts in parallel, then the group walks
     // every surviving cell together (records split over the lanes), re-checking each
     // bound against the shared best.
-    auto pass = [&](int s_begin, int s_end, bool spec) {
+    auto pass = [&](int s_begin, int s_end) {
       for (int s0 = s_begin; s0 < s_end; s0 += kGroup) {  // one shift per lane per chunk
         uint32_t vf = 0, vc = 0;
         double vlb = INFINITY;
         const int s = s0 + g;
-        if (spec) {  // lane g holds face g: probed in phase 1 if it was near, else now
-          if (slb <= best) {
-            vf = sf;
-            vc = sc;
-            vlb = slb;
-          } else if (inr && g >= 1 && g <= 6 && slb == INFINITY) {
-            const double lb = shift_lb(g);
-            if (lb <= best) {
-              probe(c_shift[g][0], c_shift[g][1], c_shift[g][2], vf, vc);
-              vlb = lb;
-            }
-          }
-        } else if (inr && s < s_end) {
+        if (inr && s < s_end) {
           const double lb = shift_lb(s);
           if (lb <= best) {  // else conservative: no point inside can win
             probe(c_shift[s][0], c_shift[s][1], c_shift[s][2], vf, vc);
             vlb = lb;
           }
         }
-#ifndef FMX_MATCH_SERIAL_CELLS
         // small cells (<= kSmallCell records): the lane that probed one folds its
         // records itself, every lane's loads in flight together, one group min after;
         // the argmin on (d^2, build order) does not depend on the folding order
@@ -588,9 +491,6 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         const int gsh = (lane_id() / kGroup) * kGroup;
         if ((__ballot(small) >> gsh) & ((1ull << kGroup) - 1)) group_min();
         uint64_t live = __ballot(vc > (uint32_t)kSmallCell);  // larger cells: walked by the group
-#else
-        uint64_t live = __ballot(vc != 0);  // wave-wide mask; this group's lanes
-#endif
         live = (live >> ((lane_id() / kGroup) * kGroup)) & ((1ull << kGroup) - 1);
         while (live) {
           const int l = __ffsll((unsigned long long)live) - 1;
@@ -605,15 +505,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         }
       }
     };
-    pass(1, 7, kSpecFaces);
-#ifdef FMX_MATCH_TIMING
-    mtime[2] = wall_clock64();
-#endif
-    pass(7, 27, false);
-    if (a.rings >= 2) pass(27, 125, false);
-#ifdef FMX_MATCH_TIMING
-    mtime[3] = wall_clock64();
-#endif
+    pass(1, 7);
+    pass(7, 27);
+    if (a.rings >= 2) pass(27, 125);
     if (g == 0) {
       const bool found = best_i != 0xFFFFFFFFu;
       int32_t pair = -1;
@@ -643,26 +537,10 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
     }
   }
-#ifdef FMX_MATCH_TIMING
-  __syncthreads();
-  mtime[4] = wall_clock64();
-  if (threadIdx.x == 0 && (blockIdx.x % 50) == 0)
-    printf("MB %d %llu %llu %d %d %d\n", (int)blockIdx.x, (unsigned long long)mtime[0], (unsigned long long)mtime[4],
-           (int)(mtime[1] - mtime[0]), (int)(mtime[2] - mtime[1]), (int)(mtime[3] - mtime[2]));
-#endif
   // work counters (probes, candidate records) for the algorithmic-byte model: one
   // plain store per block (no same-address atomics), summed on the host
   __shared__ uint32_t s_work[2][kMatchThreads / kWave];
-#ifdef FMX_MATCH_MAXLANE  // debug: per-block maximum per lane instead of sums
-  uint32_t wp = n_probe, wc = n_cand;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    wp = max(wp, (uint32_t)__shfl_xor((int)wp, o, 64));
-    wc = max(wc, (uint32_t)__shfl_xor((int)wc, o, 64));
-  }
-#else
   const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
-#endif
   if (lane_id() == 0) {
     s_work[0][threadIdx.x / kWave] = wp;
     s_work[1][threadIdx.x / kWave] = wc;
@@ -671,13 +549,8 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   if (threadIdx.x == 0) {
     uint32_t tp = 0, tc = 0;
     for (int i = 0; i < kMatchThreads / kWave; ++i) {
-#ifdef FMX_MATCH_MAXLANE
-      tp = max(tp, s_work[0][i]);
-      tc = max(tc, s_work[1][i]);
-#else
       tp += s_work[0][i];
       tc += s_work[1][i];
-#endif
     }
     work[2 * blockIdx.x] = tp;
     work[2 * blockIdx.x + 1] = tc;
@@ -748,9 +621,6 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   }
   if (a.sorted && a.tiles) pair_sort_tail(a, thist, so, host_counts);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef FMX_MATCH_TIMING
-  if (threadIdx.x == 0) printf("MLAST %d %llu\n", (int)blockIdx.x, (unsigned long long)wall_clock64());
-#endif
 }
 
 struct HistIn {
@@ -769,11 +639,10 @@ __global__ __launch_bounds__(1024) void k_pair_base(int K, uint32_t nb_pl, uint3
                                                     const uint32_t* __restrict__ hoff, const uint32_t* __restrict__ total,
                                                     uint32_t* __restrict__ pair_counts, uint32_t* __restrict__ pair_base,
                                                     uint32_t* __restrict__ chunk_range, Chunk* __restrict__ chunks,
-                                                    uint32_t* __restrict__ n_chunks, const IcpDev* __restrict__ icp,
+                                                    uint32_t* __restrict__ n_chunks,
                                                     uint32_t* __restrict__ host_counts) {
   __shared__ uint32_t ws[16];
   __shared__ uint32_t carry;
-  if (icp && icp->icp_done) return;
   const size_t npl_all = (size_t)K * nb_pl, n_all = npl_all + (size_t)K * nb_pt;
   // start offset of section (t, k) in the scanned array; sections of empty types
   // (nb = 0) start where the next section starts
@@ -854,9 +723,7 @@ __global__ __launch_bounds__(kQPB) void k_pair_scatter(uint32_t nq_pl, uint32_t 
                                                      const uint32_t* __restrict__ hist_off,
                                                      uint32_t nb_pt, const uint32_t* __restrict__ pair_base,
                                                      double* __restrict__ c_pl, size_t ld_pl,
-                                                     double* __restrict__ c_pt, size_t ld_pt,
-                                                     const IcpDev* __restrict__ icp) {
-  if (icp && icp->icp_done) return;
+                                                     double* __restrict__ c_pt, size_t ld_pt) {
   const bool planar = blockIdx.x < nb_pl;
   const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - nb_pl) * kQPB + threadIdx.x;
   const uint32_t nq = planar ? nq_pl : nq_pt;
@@ -1064,17 +931,6 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   // for zeroing, insert, count scan and scatter
   VoxMap& M = c->map;
   const uint32_t n = nrec[0] + nrec[1];
-#ifdef FMX_MAP_SLOTS
-  for (int t = 0; t < 2; ++t) {
-    M.n[t] = nrec[t];
-    M.cap[t] = next_pow2(std::max<uint64_t>(2ull * nrec[t], 1024));  // load factor <= 0.5
-  }
-  const uint64_t slots = M.cap[0] + M.cap[1];
-  M.table.ensure(slots + 1);
-  c->map_err_p = reinterpret_cast<uint32_t*>(M.table.p + slots);
-  FMX_HIP(hipMemsetAsync(M.table.p, 0, (slots + 1) * sizeof(Slot), st));
-  const double table_bytes = 16.0 * (double)slots;
-#else
   // bricks: more buckets than records, so an empty bucket always ends a probe (a
   // brick holds >= 1 record; real scans fill a few percent of the buckets)
   for (int t = 0; t < 2; ++t) {
@@ -1090,7 +946,6 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   M.bcur.ensure(8 * slots + 1);
   FMX_HIP(hipMemsetAsync(M.bcnt.p, 0, (8 * slots + 1) * sizeof(uint32_t), st));
   const double table_bytes = 64.0 * (double)slots;
-#endif
   M.tpos.ensure(n + 1);
   M.tnrm.ensure(nrec[0] + 1);
   M.rslot.ensure(n + 1);
@@ -1114,7 +969,6 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     ba.n0 = nrec[0];
     ba.n = n;
     ba.w = c->cell_w;
-    ba.table = reinterpret_cast<Slot*>(M.table.p);
     ba.bricks = reinterpret_cast<Brick*>(M.table.p);
     ba.bcnt = M.bcnt.p;
     ba.mask[0] = M.cap[0] - 1;
@@ -1128,17 +982,11 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, ba);
     FMX_HIP(hipGetLastError());
     c->dev_u32.ensure(8);
-#ifdef FMX_MAP_SLOTS
-    c->scan_scratch.ensure(scan_scratch_size(slots) + 4);
-    exclusive_scan(CountIn{reinterpret_cast<const Slot*>(M.table.p)}, FirstOut{reinterpret_cast<Slot*>(M.table.p)},
-                   slots, c->scan_scratch.p, c->dev_u32.p + 4, st);
-#else
     c->scan_scratch.ensure(scan_scratch_size(8 * slots + 1) + 4);
     exclusive_scan(BrickCountIn{M.bcnt.p}, BrickFirstOut{reinterpret_cast<Brick*>(M.table.p), M.bcur.p}, 8 * slots + 1,
                    c->scan_scratch.p, c->dev_u32.p + 4, st);
-#endif
     hipLaunchKernelGGL(k_map_scatter, dim3((n + 255) / 256), dim3(256), 0, st, nrec[0], n, M.rslot.p, M.rseg.p,
-                       M.tpos.p, M.tnrm.p, reinterpret_cast<Slot*>(M.table.p), M.bcur.p, M.pos.p, M.nrm.p, M.seg.p,
+                       M.tpos.p, M.tnrm.p, M.bcur.p, M.pos.p, M.nrm.p, M.seg.p,
                        M.rid.p);
     FMX_HIP(hipGetLastError());
   }
@@ -1148,8 +996,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   c->have_qo = false;
 }
 
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, const IcpDev* icp,
-               bool sorted) {
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted) {
   hipStream_t st = c->stream;
   const int K = std::max<int>((int)c->K, 1);
   MatchArgs a;
@@ -1171,8 +1018,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   a.nb_pt = nb_pt;
   a.K = (int)c->K;
   a.sorted = sorted ? 1 : 0;
-  static const bool old_sort = std::getenv("FMX_PAIR_SORT_BLOCKS") != nullptr;  // A/B: per-block histogram path
-  a.tiles = sorted && !old_sort && c->K <= (uint32_t)kTileMaxPairs ? 1 : 0;
+  a.tiles = sorted && c->K <= (uint32_t)kTileMaxPairs ? 1 : 0;  // wider windows: per-block histograms
   a.ntl_pl = (a.nb_pl + kTileBlocks - 1) / kTileBlocks;
   a.ntl_pt = (nb_pt + kTileBlocks - 1) / kTileBlocks;
   const uint32_t nq = c->n_qpl + c->n_qpt;
@@ -1208,8 +1054,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->h_counts.ensure(2 * (size_t)K + 4);
   auto view = [&](int t) {  // type t's table section over the shared record arrays
     VoxMap& M = c->map;
-    return MapView{reinterpret_cast<const Slot*>(M.table.p) + (t == 0 ? 0 : M.cap[0]),
-                   reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
+    return MapView{reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
                    M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
   };
   // Algorithmic bytes of a match launch: query read (16 B) +
@@ -1221,7 +1066,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
     hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
                        c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
-                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, icp, c->mcnt.p, c->mticket.p, c->h_counts.d,
+                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d,
                        c->ins_blk.p, c->ins_off.p, c->thist.p, so);
     FMX_HIP(hipGetLastError());
   }
@@ -1229,8 +1074,8 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   if (nb == 0) FMX_HIP(hipMemsetAsync(c->h_counts.d, 0, (2 * (size_t)c->K + 2) * sizeof(uint32_t), st));
   c->match_nb_pl = a.nb_pl;
   c->match_nb = nb;
+  c->n_qo = nq;  // query-order rows (k_linearize_total) in both modes
   if (!sorted) {  // counts come from the match kernel's last block
-    c->n_qo = nq;
   } else if (a.tiles) {  // offsets, counts and chunk table from the match kernel's last block
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
     if (nb == 0) {  // no launch: an empty chunk table
@@ -1250,13 +1095,13 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     if (nh > 0) exclusive_scan(HistIn{c->hist.p}, HistOut{c->hist_off.p}, nh, c->scan_scratch.p, c->dev_u32.p + 5, st);
     else FMX_HIP(hipMemsetAsync(c->dev_u32.p + 5, 0, 4, st));
     hipLaunchKernelGGL(k_pair_base, dim3(1), dim3(1024), 0, st, a.K, a.nb_pl, nb_pt, c->hist_off.p, c->dev_u32.p + 5,
-                       c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p, icp,
+                       c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p,
                        c->h_counts.d);
     FMX_HIP(hipGetLastError());
     if (nb > 0 && c->K > 0) {
       hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(kQPB), 0, st, c->n_qpl, c->n_qpt, a.nb_pl, a.K, c->m_pair.p,
                          c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, nb_pt, c->pair_base.p,
-                         c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt, icp);
+                         c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
       FMX_HIP(hipGetLastError());
     }
   }
@@ -1294,16 +1139,6 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
     }
     c->last_probes = tp;
     c->last_cands = tc;
-    static const bool dbg = std::getenv("FMX_MATCH_DEBUG") != nullptr;  // per-block work spread
-    if (dbg && c->work_blocks) {
-      uint32_t mp = 0, mc = 0;
-      for (uint32_t b = 0; b < c->work_blocks; ++b) {
-        mp = std::max(mp, c->h_work.p[2 * b]);
-        mc = std::max(mc, c->h_work.p[2 * b + 1]);
-      }
-      fprintf(stderr, "match blocks %u: probes mean %.1f max %u, candidate-lane-tests mean %.1f max %u\n",
-              c->work_blocks, tp / c->work_blocks, mp, tc / c->work_blocks, mc);
-    }
   }
   c->counts_pending = false;
 }

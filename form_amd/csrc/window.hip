@@ -43,6 +43,7 @@ constexpr int kFinBatch = 16;   // chunk partials in flight per thread in the pa
 constexpr int kWinLd = 96;      // doubles per chunk partial (91 used)
 constexpr int kWinG = 92;       // per pair: 91 G entries + error
 constexpr int kLdsStride = 13;  // doubles per staged row (13 entries; the pad lanes read 0)
+constexpr int kPairedPoses = -2;  // WinArgs::implicit_j: fmx_linearize's per-pair (T_i, T_j) table
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -66,7 +67,9 @@ struct WinArgs {
   const double* c_pt;
   size_t ld_pt;
   const double* dposes;  // pose table in device memory, or null: by value (WinPoses)
-  int implicit_j;        // >= 0: chunk.pair indexes pose i, pose j = implicit_j
+  int implicit_j;        // >= 0: chunk.pair indexes pose i, pose j = implicit_j;
+                         // kPairedPoses: pair k's poses are table entries 2k (i) and 2k + 1 (j);
+                         // else the slots packed in chunk.type
   double inv;            // 1 / sigma (FastIsotropic invsigma_, gtsam.hpp:96)
   double* partials;      // [chunk][kWinLd]
   uint32_t* pair_ticket; // [pair], self-resetting
@@ -138,6 +141,9 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
   if (a.implicit_j >= 0) {
     pi = slot;
     pj = a.implicit_j;
+  } else if (a.implicit_j == kPairedPoses) {
+    pi = 2 * slot;
+    pj = 2 * slot + 1;
   } else {
     pi = (int)((d.type >> 8) & 0xFFFu);
     pj = (int)(d.type >> 20);
@@ -273,7 +279,12 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
   t = __shfl(t, 0, 64);
   WSTAMP(5);
   if (t != n_ne - 1) return;
-  // every pair finisher drained its host stores before taking its ticket: publish
+  // Cross-wave / cross-block ordering (fmx_device.hpp, "several finishers"): every
+  // wave of every pair finisher issued its G stores as system-scope write-through
+  // stores and waited for their acknowledgement (vmcnt(0)) before the block barrier
+  // that precedes its ticket; an acknowledged write-through store has left the GPU
+  // caches, so all G stores are host-visible before the last ticket is taken and
+  // this word is stored.  publish
   if (lane == 0) {
     __hip_atomic_store(a.done_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     publish_flag(a.flag, a.seq);
@@ -617,6 +628,59 @@ void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double
   // exact row counts arrive with the match counts; the byte model uses the last known
   win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K);
   if (G_out) win_finish(c, G_out);
+}
+
+// fmx_linearize / fmx_error — the GTSAM seam, DenseFactor::linearize of every pair's
+// FeatureFactor (gtsam.hpp:67-86) — on the SAME kernel as register_scan's window
+// linearizations: the correspondences of the last sorted match (or fmx_corr_set),
+// pair k between poses_i[k] and poses_j[k] (a 2K-entry pose table).  mode 0: G = the
+// 13 x 13 augmented information (91); mode 1: the single-pose 7 x 7 (28) =
+// [H_j b]^T [H_j b], the trailing 7 x 7 block of the 13 x 13 (BinaryFactorWrapper,
+// gtsam.hpp:144-170); mode 2: errors only.  err[k] = 0.5 ||r/sigma||^2.  Pairs
+// without rows linearize to zero.
+void win_linearize_pairs(fmx_ctx* c, const double* poses_i, const double* poses_j, double sigma, int mode,
+                         double* G_out, double* err_out) {
+  if (!c->have_corr) throw StatusError(FMX_E_STATE, "no correspondences (call fmx_match or fmx_corr_set)");
+  const int K = (int)c->K;
+  if (K == 0) return;
+  if (2 * (size_t)K > 0xFFFFFFu) throw StatusError(FMX_E_INVAL, "too many pairs");
+  WinStore& W = c->win;
+  if (W.pending) win_finish(c, nullptr);
+  std::vector<double> table(24 * (size_t)K);
+  for (int k = 0; k < K; ++k) {
+    std::memcpy(&table[24 * (size_t)k], poses_i + 12 * (size_t)k, 12 * sizeof(double));
+    std::memcpy(&table[24 * (size_t)k + 12], poses_j + 12 * (size_t)k, 12 * sizeof(double));
+  }
+  if (c->counts_pending) match_counts_fetch(c);  // exact byte model (rows per type)
+  W.hG.ensure((size_t)K * kWinG);
+  std::memset(W.hG.p, 0, (size_t)K * kWinG * sizeof(double));  // pairs without rows are never written
+  WinArgs a{};
+  a.chunks = c->chunks.p;
+  a.n_chunks = c->n_chunks.p;
+  a.chunk_range = c->chunk_range.p;
+  a.npairs = K;
+  a.c_pl = c->c_pl.p;
+  a.ld_pl = c->ld_pl;
+  a.c_pt = c->c_pt.p;
+  a.ld_pt = c->ld_pt;
+  a.implicit_j = kPairedPoses;
+  a.inv = 1.0 / sigma;  // FastIsotropic invsigma_ (gtsam.hpp:96)
+  win_start(c, a, c->max_chunks, table.data(), 2 * K, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * K);
+  win_finish(c, nullptr);
+  const double* hg = W.hG.p;
+  for (int k = 0; k < K; ++k) {
+    const double* g = hg + (size_t)k * kWinG;
+    if (err_out) err_out[k] = g[91];
+    if (!G_out || mode == 2) continue;
+    if (mode == 0) {
+      std::memcpy(G_out + (size_t)k * 91, g, 91 * sizeof(double));
+    } else {  // rows / columns 6..12 of the packed upper 13 x 13
+      double* o = G_out + (size_t)k * 28;
+      int q = 0;
+      for (int r = 6; r < 13; ++r)
+        for (int cc = r; cc < 13; ++cc) o[q++] = g[r * 13 - r * (r - 1) / 2 + (cc - r)];
+    }
+  }
 }
 
 }  // namespace fmx

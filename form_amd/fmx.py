@@ -78,7 +78,7 @@ EXPORTED = [
     "fmx_extract", "fmx_extract_download", "fmx_set_queries", "fmx_set_queries_device", "fmx_keypoints_add",
     "fmx_keypoints_add_device",
     "fmx_keypoints_remove", "fmx_map_build", "fmx_match", "fmx_match_download", "fmx_map_insert",
-    "fmx_corr_set", "fmx_linearize", "fmx_error", "fmx_register_scan", "fmx_current_pose",
+    "fmx_corr_set", "fmx_linearize", "fmx_error", "fmx_linearize_matched", "fmx_register_scan", "fmx_current_pose",
     "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
     "fmx_profile_name", "fmx_profile_read", "fmx_sync",
 ]
@@ -285,6 +285,14 @@ class Context:
         err = np.zeros(max(self.K, 1))
         self._chk(self._L.fmx_error(self.h, _p(pi_), _p(pj_), C.c_double(sigma), _p(err)))
         return err[:self.K]
+
+    def linearize_matched(self, pose_j34, sigma: float = 0.1):
+        """Single-pose 7x7 system (28 packed) summed over every accepted match of the
+        last match at pose_j, and its error."""
+        pose = np.ascontiguousarray(pose_j34, np.float64).reshape(12)
+        out = np.zeros(29)
+        self._chk(self._L.fmx_linearize_matched(self.h, _p(pose), C.c_double(sigma), _p(out)))
+        return out[:28].copy(), float(out[28])
 
     # ---------------------------------------------------------------- estimator
     def register_scan(self, scan):

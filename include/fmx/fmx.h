@@ -140,7 +140,10 @@ fmx_status fmx_match(fmx_ctx* ctx, const double pose_j34[12], double max_dist,
                      uint32_t* counts_planar, uint32_t* counts_point);
 /* Per-query match results of the last fmx_match, planar queries then point
  * queries (any pointer may be NULL): pair[q] (-1 if not accepted), d2[q]
- * (DBL_MAX when no map point lies within max_dist), pi[3q], ni[3q] (planar only). */
+ * (DBL_MAX when no record lies within
+ * max(max_dist, min_dist_map) of the query inside its 27 voxels; with both <= the
+ * voxel width the search is bounded by them, otherwise it covers all 27 voxels, so a
+ * finite d2 may exceed max_dist^2 — accept/insert decisions equal the reference's), pi[3q], ni[3q] (planar only). */
 fmx_status fmx_match_download(fmx_ctx* ctx, int32_t* pair, double* d2, double* pi, double* ni);
 /* KeypointMap::insert_matches (map.tpp:148-165): append every query of the last
  * match whose NN distance^2 > min_dist_map^2 to the store under the query scan. */
@@ -162,6 +165,13 @@ fmx_status fmx_linearize(fmx_ctx* ctx, const double* poses_i34, const double* po
  * Jacobians), err: K x 1. */
 fmx_status fmx_error(fmx_ctx* ctx, const double* poses_i34, const double* poses_j34,
                      double sigma, double* err);
+/* The single-pose ablation's whole linear system at X(j) = pose_j34 (X(i) fixed at
+ * the built map's poses): sum over every accepted match of the last fmx_match of the
+ * 7 x 7 [H_j b]^T [H_j b] — what GTSAM's LM eliminates from get_single_graph's
+ * BinaryFactorWrapper<FeatureFactor>s (constraints.cpp:235-250, gtsam.hpp:40-54,
+ * 144-170) — in one launch over the match outputs in query order.  out[0..27]: the
+ * packed upper 7 x 7, out[28]: the error 0.5 ||r/sigma||^2. */
+fmx_status fmx_linearize_matched(fmx_ctx* ctx, const double pose_j34[12], double sigma, double out[29]);
 
 /* ---------------- host adapter: Estimator::register_scan -------------------
  * form::Estimator::register_scan (form/form.hpp:82-83, form.cpp:40-114): predict,
