@@ -1,18 +1,23 @@
 """bench.py — scan-to-submap registration throughput on MI355X (driver contract).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|c5]
   (N > 1: launched by torch.distributed.run, one rank per GPU)
 
 A step = Estimator::register_scan of one synthetic organized scan (form/form.cpp:40-114):
 feature extraction, voxel-map build of the window keyscans, the ICP loop (match + LM
 whose linearizations and error evaluations run on the GPU) and map insertion.  Scans
-are ray-cast on the GPU before the timed region (inputs resident in HBM).  Multi-GPU:
-real scans do not shard, so every rank registers its own independent
-stream ("replicas only", weak scaling); value = all ranks' scans / max-over-ranks time.
+are ray-cast on the GPU before the timed region (inputs resident in HBM); --prefill
+untimed scans run first so the timed steps see the window in steady state.
+Multi-GPU: a 128-beam scan does not shard, so every rank registers
+its own independent stream ("replicas", weak scaling); value = all ranks' scans /
+max-over-ranks time.  Beside it, `sharded_c5` times the north star's scaling config
+on the same ranks: one 2M-point scan registered against a replicated 50M-voxel
+submap, its points sharded over the ranks, the normal equations all-reduced over
+RCCL each ICP iteration (strong scaling).
 
 Prints ONE JSON line (rank 0) with the contract fields plus `roofline` (dominant
-kernel, HIP-event timed inside the timed region) and `cpu_baseline` (the C++ oracle
-on the host cores, bounded sample of the same stream).
+kernel, HIP-event timed), `cpu_baseline` (the C++ oracle on the host cores, bounded
+sample of the same stream) and `sharded_c5`.
 """
 from __future__ import annotations
 
@@ -42,6 +47,12 @@ def parse():
     ap.add_argument("--workload", default="c4", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--c5-side", type=int, default=7071, help="C5 terrain grid side (7071^2 = 50M voxels)")
     ap.add_argument("--c5-queries", type=int, default=2097152, help="C5 query points (2M)")
+    ap.add_argument("--prefill", type=int, default=90,
+                    help="untimed scans registered before the warmup so the timed region runs with the "
+                         "window in steady state (10 recent scans + keyscans), not while it fills")
+    ap.add_argument("--c5-steps", type=int, default=5, help="sharded C5 registrations timed beside the C4 line")
+    ap.add_argument("--c5-warmup", type=int, default=1)
+    ap.add_argument("--no-c5", action="store_true", help="skip the sharded C5 measurement beside the C4 line")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--profile-steps", type=int, default=None,
                     help="extra steps, after the timed ones, with per-kernel HIP-event timing (roofline); "
@@ -96,15 +107,16 @@ def sum_over_ranks(x, world, local):
     return float(t.item())
 
 
-def pmc_traffic(a, name):
+def pmc_traffic(a, name, workload=None):
     """HBM bytes per launch of kernel class `name` from the committed PMC summary of this
     workload (tools/gpu_pmc.sh, tools/gpu_c5pmc.sh), or None."""
-    path = a.traffic_json or os.path.join(
-        ROOT, "profiles", "traffic_latest.json" if a.workload == "c4" else f"traffic_{a.workload}.json")
+    workload = workload or a.workload
+    path = (a.traffic_json if workload == a.workload else None) or os.path.join(
+        ROOT, "profiles", "traffic_latest.json" if workload == "c4" else f"traffic_{workload}.json")
     try:
         with open(path) as f:
             tj = json.load(f)
-        if tj.get("workload") == a.workload and name in tj.get("kernels", {}):
+        if tj.get("workload") == workload and name in tj.get("kernels", {}):
             return tj["kernels"][name]["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         pass
@@ -140,11 +152,28 @@ def pin_thread(world, local):
     return old
 
 
+def host_info():
+    """The host the CPU baseline runs on: logical CPUs, this job's affinity, CPU model."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": model}
+
+
 def cpu_baseline(scans_host, params, budget_s, single):
-    """Oracle register_scan on the host cores over the first scans of the same stream."""
+    """Oracle register_scan on the host cores over the first scans of the same stream.
+    Threads: the job's CPU share — OMP_NUM_THREADS when the launcher sets it (the GPU
+    box allots 16 CPUs per GPU and exports 16), else every CPU in this process's
+    affinity mask (the reference's TBB default: all host cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O  # CPU baseline only (test infrastructure)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    hi = host_info()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or hi["affinity_cpus"]
     prm = O.default_params(params)
     prm.disable_smoothing = int(single)
     est = O.Estimator(prm, threads)
@@ -163,10 +192,11 @@ def cpu_baseline(scans_host, params, budget_s, single):
     per = float(np.median(steady))
     return dict(value=1.0 / per, unit="scans/s", cores=threads, kind="port",
                 sample=f"oracle register_scan ({'single-pose' if single else 'smoothing'} mode; C++ restatement, "
-                       f"std::thread at the reference's TBB sites: normals, match queries, factor linearization) "
-                       f"over the first {len(times)} scans of the same synthetic stream; median of "
-                       f"{len(steady)} steady-state scans = {per * 1e3:.1f} ms/scan",
-                ms_per_scan=per * 1e3), poses
+                       f"std::thread at the reference's TBB sites (normals, match queries) and over the factors "
+                       f"of a linearization (GTSAM's TBB-parallel NonlinearFactorGraph::linearize)) over the first "
+                       f"{len(times)} scans of the same synthetic stream; median of {len(steady)} steady-state "
+                       f"scans = {per * 1e3:.1f} ms/scan",
+                ms_per_scan=per * 1e3, **hi), poses
 
 
 def ate_block(scans_host, oracle_poses, params, k0, device, single):
@@ -188,82 +218,115 @@ def ate_block(scans_host, oracle_poses, params, k0, device, single):
             "scans": n, "truth": "synthetic trajectory (synth.trajectory_pose)"}
 
 
-def run_c5(a, rank, world, local):
-    """C5: 2M query points vs a 50M-voxel terrain submap, queries
-    sharded over ranks, map replicated.  A step = one ICP iteration of the full 2M
-    point set: match the shard, reduce it to the 7x7 normal equations (single pose),
-    all_reduce (RCCL over xGMI when N > 1), identical Gauss-Newton update on every
-    rank.  Strong scaling: the total work per step is fixed."""
+def c5_setup(a, rank, world, local):
+    """The sharded C5 problem on this rank: the replicated 50M-voxel terrain map, this
+    rank's shard of the 2M-point scan, an RCCL communicator over all ranks."""
     from form_amd import shard
     dev = f"cuda:{local}"
     w = 0.8
     pos4, nrm4 = shard.terrain_map(a.c5_side, w, synth.SEED, dev)
-    Ttrue = shard.compose(np.hstack([np.eye(3), np.array([[0.03], [-0.04], [0.0]])]),
-                          shard.expmap(np.array([0.0, 0.0, np.radians(0.5), 0.0, 0.0, 0.0])))
-    q4, n4 = shard.make_queries(pos4, nrm4, a.c5_queries, Ttrue, 0.05, synth.SEED + 1)
+    Ttrue = shard.c5_offset()
+    q4, n4 = shard.make_queries(pos4, nrm4, a.c5_queries, Ttrue, 0.03, synth.SEED + 1)
     b, e = shard.shard_bounds(a.c5_queries, rank, world)
     n_map = pos4.shape[0]
-    prm = fmx.EstimatorParams(keypoint_pool_capacity=n_map + 1024, voxel_subdivision=a.subdiv or 1)  # one record per voxel
+    prm = fmx.EstimatorParams(keypoint_pool_capacity=n_map + 1024, voxel_subdivision=a.subdiv or 1)
     ctx = fmx.Context(prm, device=local)
+    if world > 1:  # RCCL communicator of the exchange step (fmx_comm_init)
+        import torch.distributed as dist
+        uid = [fmx.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(uid[0], world, rank)
     ctx.keypoints_add_device(0, pos4, nrm4)
     I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
     ctx.map_build([0], I34[None], w)
-    qs, ns = q4[b:e].contiguous(), n4[b:e].contiguous()
-    ctx.set_queries_device(qs, ns)
-    del pos4, nrm4
+    ctx.set_queries_device(q4[b:e].contiguous(), n4[b:e].contiguous())
+    del pos4, nrm4, q4, n4
     torch.cuda.synchronize()
-    T = I34.copy()
+    return ctx, Ttrue, n_map, w
 
-    def step(T):
+
+def c5_register(ctx, w, max_iters=30, thr=1e-4):
+    """One registration of the 2M-point scan: ICP iterations of match
+    (this rank's shard) -> the shard's single-pose 7x7 normal equations, all-reduced
+    over the ranks on the device (RCCL) -> the identical Gauss-Newton step on every
+    rank, from the identity to convergence (form.cpp:83-88's 1e-4 threshold on the
+    increment).  Returns (pose, ICP iterations)."""
+    from form_amd import shard
+    T = np.hstack([np.eye(3), np.zeros((3, 1))])
+    for it in range(max_iters):
         ctx.match(T, w)
-        G, _ = ctx.linearize(I34[None], T[None], 0.1, True)
-        Gs = shard.allreduce_sum(G[0], device=dev)
-        return shard.compose(T, shard.expmap(shard.gauss_newton_step(Gs)))
+        S, _ = ctx.linearize_matched(T, 0.1)
+        dx = shard.gauss_newton_step(S)
+        T = shard.compose(T, shard.expmap(dx))
+        if np.linalg.norm(dx) < thr:
+            return T, it + 1
+    return T, max_iters
 
-    for _ in range(a.warmup):
-        T = step(T)
+
+def run_c5(a, rank, world, local, steps, warmup, profile=True):
+    """C5: a 2M-point scan vs a 50M-voxel terrain submap, the scan's
+    points sharded over the ranks, the map replicated.  A step = one registration
+    (c5_register); strong scaling: the total work per step is fixed."""
+    from form_amd import shard
+    ctx, Ttrue, n_map, w = c5_setup(a, rank, world, local)
+    for _ in range(warmup):
+        T, iters = c5_register(ctx, w)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        T = step(T)
+    it_total = 0
+    for _ in range(steps):
+        T, iters = c5_register(ctx, w)
+        it_total += iters
     torch.cuda.synchronize()
     barrier(world)
     t_local = time.perf_counter() - t0
-    ctx.profile(True)
-    ctx.profile_reset()
-    psteps = a.steps if a.profile_steps is None else a.profile_steps
-    for _ in range(psteps):
-        T = step(T)
-    ctx.sync()
-    prof = ctx.profile_read()
-    work = ctx.match_work()
+    prof, work = {}, {"queries": 1.0}
+    if profile:
+        ctx.profile(True)
+        ctx.profile_reset()
+        for _ in range(max(steps // 2, 1)):
+            c5_register(ctx, w)
+        ctx.sync()
+        prof = ctx.profile_read()
+        work = ctx.match_work()
+        ctx.profile(False)
     t_max = max_over_ranks(t_local, world, local)
+    ctx.close()
     if rank != 0:
         return None
-    value = a.steps / t_max
-    name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
-    avg_ms = d["ms"] / max(d["launches"], 1)
-    bytes_per = d["bytes"] / max(d["launches"], 1)
-    achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    err = float(np.abs(T - Ttrue).max())
-    return {
-        "metric": METRIC, "value": round(value, 3), "unit": "scans/s (2M-point scans)", "n_gpus": world,
-        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t_max / a.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-        "dtype": "fp32 points / fp64 map, residuals and normal equations",
-        "data": "synthetic (jittered terrain grid, seed 0x464F524D)",
-        "config": {"workload": f"c5: {a.c5_queries} queries vs {n_map}-voxel submap, queries sharded, "
-                               "7x7 normal equations all-reduced", "points_per_scan": a.c5_queries,
-                   "parallelism": f"query shards x{world} + all_reduce"},
+    value = steps / t_max
+    et, er = shard.pose_error(T, Ttrue)
+    e0t, e0r = shard.pose_error(np.hstack([np.eye(3), np.zeros((3, 1))]), Ttrue)
+    out = {
+        "metric": "C5 registrations/s + Mpts/s (2M-point scan vs 50M-voxel submap, points sharded, RCCL all-reduce)",
+        "value": round(value, 3), "unit": "registrations/s (2M-point scans)", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(t_max / steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong",
+        "icp_iters_per_registration": round(it_total / steps, 3),
+        "icp_iters_per_s": round(it_total / t_max, 3),
         "mpts_per_s": round(value * a.c5_queries / 1e6, 3),
-        "roofline": dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                         frac=round(achieved / HBM_PEAK_GBS, 6), traffic=pmc_traffic(a, name),
-                         avg_launch_us=round(avg_ms * 1e3, 3), alg_bytes_per_launch=bytes_per),
-        "kernels_ms_per_step": {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()},
-        "pose_error_vs_truth": err,
-        "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
+        "config": {"workload": f"c5: {a.c5_queries} points within {shard.C5_RANGE_M:.0f} m vs a {n_map}-voxel "
+                               "terrain submap; points sharded contiguously, map replicated; single-pose 7x7 "
+                               "normal equations all-reduced (RCCL, device buffers, context stream) per ICP "
+                               "iteration", "points_per_scan": a.c5_queries,
+                   "parallelism": f"point shards x{world} + all_reduce"},
+        "pose_error": {"initial_m": round(e0t, 6), "initial_rad": round(e0r, 8), "final_m": round(et, 6),
+                       "final_rad": round(er, 8)},
     }
+    if prof:
+        name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
+        avg_ms = d["ms"] / max(d["launches"], 1)
+        bytes_per = d["bytes"] / max(d["launches"], 1)
+        achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        nprof = max(steps // 2, 1)
+        out["roofline"] = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+                               frac=round(achieved / HBM_PEAK_GBS, 6), traffic=pmc_traffic(a, name, "c5"),
+                               avg_launch_us=round(avg_ms * 1e3, 3), alg_bytes_per_launch=bytes_per)
+        out["kernels_ms_per_step"] = {k: round(v["ms"] / nprof, 4) for k, v in prof.items() if v["ms"] > 0}
+        out["match_work_per_query"] = {k: round(v / max(work["queries"], 1), 3) for k, v in work.items()
+                                       if k != "queries"}
+    return out
 
 
 def main():
@@ -271,7 +334,7 @@ def main():
     rank, world, local = dist_setup(a.gpus)
     if a.workload == "c5":
         torch.cuda.set_device(local)
-        out = run_c5(a, rank, world, local)
+        out = run_c5(a, rank, world, local, a.steps, a.warmup)
         if out is not None:
             print(json.dumps(out))
         if world > 1:
@@ -287,7 +350,8 @@ def main():
     world_obj = synth.World()
     k0 = 1000 * rank
     psteps = a.steps if a.profile_steps is None else a.profile_steps
-    total = a.warmup + a.steps + psteps
+    pre = a.prefill
+    total = pre + a.warmup + a.steps + psteps
     scans = [synth.raycast(world_obj, synth.trajectory_pose(k0 + k), geo, synth.SEED + 7919 * (k0 + k + 1), dev)
              for k in range(total)]
     torch.cuda.synchronize()
@@ -302,11 +366,11 @@ def main():
     ablation = None
     if not a.no_ablation:  # the other mode over the same scans (secondary, untimed by the driver)
         actx = new_ctx(not single)
-        for k in range(a.warmup):
+        for k in range(pre + a.warmup):
             actx.register_scan(scans[k])
         actx.sync()
         ta = time.perf_counter()
-        for k in range(a.warmup, a.warmup + a.steps):
+        for k in range(pre + a.warmup, pre + a.warmup + a.steps):
             actx.register_scan(scans[k])
         actx.sync()
         ta = time.perf_counter() - ta
@@ -315,14 +379,14 @@ def main():
         actx.close()
         del actx
     ctx = new_ctx(single)
-    for k in range(a.warmup):
+    for k in range(pre + a.warmup):
         ctx.register_scan(scans[k])
     ctx.sync()
     stats = []
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.warmup, a.warmup + a.steps):
+    for k in range(pre + a.warmup, pre + a.warmup + a.steps):
         ctx.register_scan(scans[k])
         stats.append(ctx.last_stats())
     ctx.sync()
@@ -332,14 +396,19 @@ def main():
     # roofline pass: same stream continued, per-kernel HIP events on the context stream
     ctx.profile(True)
     ctx.profile_reset()
-    for k in range(a.warmup + a.steps, total):
+    for k in range(pre + a.warmup + a.steps, total):
         ctx.register_scan(scans[k])
     ctx.sync()
     prof = ctx.profile_read()
     work = ctx.match_work()
     ctx.profile(False)
+    ctx.close()
     t_max = max_over_ranks(t_local, world, local)
     scans_total = sum_over_ranks(float(a.steps), world, local)
+    # the sharded C5 registration beside the replica line: every rank takes part
+    c5 = None
+    if not a.no_c5:
+        c5 = run_c5(a, rank, world, local, a.c5_steps, a.c5_warmup, profile=False)
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
@@ -358,6 +427,8 @@ def main():
                 frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, avg_launch_us=round(avg_ms * 1e3, 3),
                 alg_bytes_per_launch=bytes_per)
     st_mean = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
+    kern_ms = {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()}
+    kern_sum = sum(kern_ms.values())
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -373,20 +444,29 @@ def main():
         "data": "synthetic (ray-cast organized scans, seed 0x464F524D; no datasets offline)",
         "config": {"workload": f"{a.workload}: {geo.rows}x{geo.cols} organized scan stream ({n_pts} pts/scan), "
                                f"register_scan, {'single-pose ablation (disable_smoothing)' if single else 'smoothing mode (ConstraintManager default)'}",
-                   "points_per_scan": n_pts, "parallelism": f"replicas x{world}"},
+                   "points_per_scan": n_pts, "parallelism": f"replicas x{world}",
+                   "timed_scans": [pre + a.warmup, pre + a.warmup + a.steps],
+                   "prefill": pre},
         "mpts_per_s": round(value * n_pts / 1e6, 3),
         "roofline": roof,
-        "kernels_ms_per_step": {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()},
+        "kernels_ms_per_step": kern_ms,
         "profile_steps": psteps,
+        # device time per scan (profile pass, HIP events; the side-stream map build
+        # overlaps extraction and is counted in full) over the timed wall time per scan
+        "gpu_busy_frac": round(min(kern_sum / ms_per_step, 1.0), 4) if ms_per_step > 0 else None,
+        "host_round_trips_per_scan": round(st_mean.get("host_waits", 0.0), 2),
         "counters": st_mean,
         "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
     }
     if ablation is not None:
         out["ablation"] = ablation
+    if c5 is not None:
+        out["sharded_c5"] = c5
     if prev_aff is not None:
         os.sched_setaffinity(0, prev_aff)  # the CPU baseline's threads use every host core
     if not a.no_cpu_baseline and world == 1:
         host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
+        del scans
         out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s, single)
         out["ate"] = ate_block(host, opos, params, k0, local, single)
     print(json.dumps(out))

@@ -32,10 +32,15 @@ int match_group_for(uint64_t nq) {
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, hipStream_t st) {
   g8::run_map_build(c, scans, poses34, w, st);  // the same build in both variants
 }
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted) {
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
+               bool defer_scatter) {
   c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt);
-  if (c->match_group == 4) g4::run_match(c, pose_j34, max_dist, min_dist_map, sorted);
-  else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted);
+  if (c->match_group == 4) g4::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
+  else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
+}
+void run_pair_scatter(fmx_ctx* c) {
+  if (c->match_group == 4) g4::run_pair_scatter(c);
+  else g8::run_pair_scatter(c);
 }
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
   if (c->match_group == 4) g4::run_insert(c, scan, n_inserted);
@@ -736,6 +741,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " + std::to_string(RC) +
                                       " != " + std::to_string(n));
   const uint64_t j = e.init ? e.scan + 1 : 0;
+  const uint64_t waits0 = c->host_waits;
   // Host work that only needs the estimator state runs while this scan's extraction
   // kernels execute: the previous scan's deferred tail (keyscan step +
   // marginalization), then step(prediction) (constraints.cpp:206-223) and the map
@@ -846,6 +852,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[5] = c->map.n[1];
   c->stats[6] = lins;
   c->stats[7] = scans.size();
+  c->stats[8] = c->host_waits - waits0;
   if (out) *out = fc;
 }
 
@@ -927,6 +934,8 @@ void fmx_destroy(fmx_ctx* c) {
     (void)hipEventDestroy(pe.second.second);
   }
   delete c->est;
+  comm_destroy(c);
+  c->d_sum.release();
   // DBuf/HBuf members do not free in their destructors: release explicitly.
   c->scan.release(); c->planar_mask.release(); c->sel_slots.release(); c->pt_slots.release();
   c->row_counts.release(); c->row_ok.release(); c->row_off.release(); c->closest.release();
@@ -954,7 +963,7 @@ void fmx_destroy(fmx_ctx* c) {
     auto& W = c->win;
     for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }
     W.meta.release(); if (W.meta_ev) (void)hipEventDestroy(W.meta_ev); W.partials.release(); W.dposes.release();
-    W.pticket.release(); W.dticket.release(); W.dbg.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
+    W.pticket.release(); W.dticket.release(); W.dflag.release(); W.dbg.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -1055,7 +1064,7 @@ fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint3
     if (!c->have_map) throw StatusError(FMX_E_STATE, "fmx_map_build first");
     if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
     if (!(max_dist > 0)) throw StatusError(FMX_E_INVAL, "max_dist must be > 0");
-    run_match(c, pose_j, max_dist, c->P.min_dist_map);
+    run_match(c, pose_j, max_dist, c->P.min_dist_map, true, true);  // rows scattered when read
     match_counts_fetch(c);
     c->h_u32.ensure(8);
     FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->map_err_p, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1140,6 +1149,26 @@ fmx_status fmx_linearize_matched(fmx_ctx* c, const double pose_j[12], double sig
   });
 }
 
+fmx_status fmx_comm_unique_id(uint8_t id[128]) {
+  if (!id) return FMX_E_INVAL;
+  try {
+    comm_unique_id(id);
+    return FMX_OK;
+  } catch (const StatusError& e) {
+    return e.st;
+  } catch (const std::exception&) {
+    return FMX_E_RCCL;
+  }
+}
+
+fmx_status fmx_comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank) {
+  return guard(c, [&] {
+    if (!id) throw StatusError(FMX_E_INVAL, "null id");
+    FMX_HIP(hipStreamSynchronize(c->stream));
+    comm_init(c, id, nranks, rank);
+  });
+}
+
 fmx_status fmx_register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
   return guard(c, [&] { register_scan(c, xyzw, n, on_dev, out); });
 }
@@ -1155,8 +1184,11 @@ fmx_status fmx_current_pose(fmx_ctx* c, double pose[12]) {
   });
 }
 
-fmx_status fmx_last_stats(fmx_ctx* c, uint64_t stats[8]) {
-  return guard(c, [&] { std::memcpy(stats, c->stats, sizeof(c->stats)); });
+fmx_status fmx_last_stats(fmx_ctx* c, uint64_t* stats, int n) {
+  return guard(c, [&] {
+    if (!stats || n < 0) throw StatusError(FMX_E_INVAL, "null stats");
+    for (int k = 0; k < n; ++k) stats[k] = k < kStatsN ? c->stats[k] : 0;
+  });
 }
 
 fmx_status fmx_match_work(fmx_ctx* c, double work[3]) {

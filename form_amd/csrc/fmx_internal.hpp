@@ -158,6 +158,13 @@ struct Seg {
   uint32_t pad;
 };
 
+// Launch geometry of a sorted match's pending row scatter (run_pair_scatter).
+struct PairScatter {
+  uint32_t nb_pl = 0, nb_pt = 0, ntl_pl = 0, ntl_pt = 0;
+  int K = 0;
+  int tiles = 0;
+};
+
 struct Chunk {
   uint32_t type;  // bits 0-7: 0 plane rows, 1 point pairs; window chunks: pose slot i
                   // in bits 8-19, pose slot j in bits 20-31
@@ -208,7 +215,7 @@ struct WinStore {
   // launch scratch
   DBuf<double> partials, dposes;
   DBuf<uint64_t> dbg;  // FMX_WIN_TIMING stamps
-  DBuf<uint32_t> pticket, dticket;
+  DBuf<uint32_t> pticket, dticket, dflag;  // dflag: the completion word of a sharded launch
   bool pending = false;  // a k_win_linearize launched by win_start, not yet finished
   uint32_t pending_seq = 0, pending_grid = 0;
   int pending_np = 0;
@@ -217,6 +224,8 @@ struct WinStore {
 };
 
 }  // namespace fmx
+
+constexpr int kStatsN = 9;  // fmx_last_stats entries
 
 struct fmx_ctx {
   fmx_params P{};
@@ -281,6 +290,8 @@ struct fmx_ctx {
   uint32_t max_chunks = 0;
   int match_group = 8;  // lanes per query of the last run_match (voxelmap.hip g8 / g4)
   bool have_corr = false;
+  fmx::PairScatter ps;          // the last sorted match's scatter (voxelmap.hip)
+  bool scatter_pending = false; // ... not yet launched (deferred by fmx_match)
   uint64_t rows_pl = 0, rows_pt = 0;           // correspondences (plane rows, point pairs)
   std::vector<uint32_t> cnt_pl, cnt_pt;         // per pair, host copy after match
   fmx::HBuf<double> h_corr;
@@ -311,10 +322,16 @@ struct fmx_ctx {
   // ---- smoothing-mode window store
   fmx::WinStore win;
 
+  // ---- multi-GPU exchange (comm.cpp): RCCL communicator, or null
+  void* comm = nullptr;
+  int comm_size = 1, comm_rank = 0;
+  fmx::DBuf<double> d_sum;  // device-side linearization sums all-reduced in place
+
   // ---- host estimator state (register_scan)
   struct Est;
   Est* est = nullptr;
-  uint64_t stats[8] = {};
+  uint64_t stats[kStatsN] = {};
+  uint64_t host_waits = 0;  // host waits on device results (stream / completion word) so far
 };
 
 namespace fmx {
@@ -360,6 +377,7 @@ struct HostScope {
 // blocking wake-up measured 4-5 % slower on register_scan, C4).
 inline void stream_wait(fmx_ctx* c) {
   HostScope hs(1);
+  ++c->host_waits;
   for (;;) {
     const hipError_t e = hipStreamQuery(c->stream);
     if (e == hipSuccess) return;
@@ -373,6 +391,7 @@ inline void stream_wait(fmx_ctx* c) {
 // stream error, throws (no silent hang).
 inline void wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq) {
   HostScope hs(1);
+  ++c->host_waits;
   for (uint32_t spins = 1;; ++spins) {
     if (*f == seq) break;
     if ((spins & 0x3FFF) == 0) {
@@ -400,7 +419,8 @@ inline uint32_t next_flag(fmx_ctx* c) {
   void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, \
                      hipStream_t st = nullptr);                                                      \
   void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map,            \
-                 bool sorted = true);                                                                \
+                 bool sorted = true, bool defer_scatter = false);                                    \
+  void run_pair_scatter(fmx_ctx* c);                                                                 \
   void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);                                  \
   void match_counts_fetch(fmx_ctx* c, bool wait = true);
 namespace g8 { FMX_VM_DECLS }
@@ -416,7 +436,11 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
 // sorted: bucket the accepted matches pair-major into SoA correspondences (fmx_match /
 // fmx_linearize, the smoothing mode); otherwise only the per-pair counts are produced
 // and the single-pose mode linearizes in query order.
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted = true);
+// defer_scatter: the pair-major row scatter waits for run_pair_scatter (fmx_match: the
+// caller may read only the query-order outputs, e.g. fmx_linearize_matched).
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted = true,
+               bool defer_scatter = false);
+void run_pair_scatter(fmx_ctx* c);  // no-op unless a sorted match's scatter is pending
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
 // wait = false: the caller knows the match kernel has completed (a later kernel in
 // stream order published a flag)
@@ -434,6 +458,11 @@ void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vecto
 void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out);
 void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
 void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* called with G_out = null
+// comm.cpp: RCCL communicator of the sharded path, all-reduce on the context stream
+void comm_unique_id(uint8_t id[128]);
+void comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank);
+void comm_destroy(fmx_ctx* c);
+void comm_allreduce_sum(fmx_ctx* c, double* dev, size_t n);  // no-op without a communicator
 // fmx_linearize / fmx_error on k_win_linearize: mode 0 13 x 13 (91), 1 single-pose 7 x 7 (28), 2 errors only
 void win_linearize_pairs(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
                          double* G_out, double* err_out);

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kTotWaves * kWave) void k_linearize_total(
   }
   if (threadIdx.x == 0) {
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    publish_flag(flag, seq);  // out[] was stored by this wave (threads 0..28 of wave 0)
+    if (flag) publish_flag(flag, seq);  // out[] was stored by this wave (threads 0..28 of wave 0)
   }
 }
 
@@ -224,6 +224,7 @@ void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, 
   c->rows_pt = Nt;
   c->counts_pending = false;
   c->have_corr = true;
+  c->scatter_pending = false;
   c->have_match = false;
 }
 
@@ -253,22 +254,34 @@ void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, doubl
   if (!c->have_qo) throw StatusError(FMX_E_STATE, "no query-order match");
   hipStream_t st = c->stream;
   for (int i = 0; i < 29; ++i) out[i] = 0.0;
-  if (c->K == 0 || c->n_qo == 0) return;
+  if ((c->K == 0 || c->n_qo == 0) && !c->comm) return;  // sharded: every rank joins the collective
   const uint32_t nblk = tot_blocks(c);
   Pose34 tjv;
   std::memcpy(tjv.m, pose_j34, sizeof(tjv.m));
   c->h_G.ensure(32);
-  const uint32_t seq = next_flag(c);
+  // sharded (fmx_comm_init): the sums go to a device buffer, are all-reduced there on
+  // this stream and copied out; else straight to mapped host memory behind the word
+  const bool comm = c->comm != nullptr;
+  if (comm) c->d_sum.ensure(32);
+  const uint32_t seq = next_flag(c);  // allocates the word on first use
+  double* dst = comm ? c->d_sum.p : c->h_G.d;
+  uint32_t* flag = comm ? nullptr : c->h_flag.d;
   if (c->counts_pending && c->prof.on) match_counts_fetch(c);  // exact byte model for the profile
   {
     // bytes: pair id per query + (p_i, n_i 32 B each, p_j 16 B) per accepted plane row,
     // (p_i 32 B, p_j 16 B) per accepted point pair
     ProfScope ps(c->prof, PROF_LINEARIZE, 4.0 * c->n_qo + 80.0 * c->rows_pl + 48.0 * c->rows_pt, st);
     hipLaunchKernelGGL(k_linearize_total, dim3(nblk), dim3(kTotWaves * kWave), 0, st, qo_rows(c), c->map_poses_p,
-                       1.0 / sigma, c->bpart.p, c->ticket.p, c->h_G.d, tjv, c->h_flag.d, seq);
+                       1.0 / sigma, c->bpart.p, c->ticket.p, dst, tjv, flag, seq);
     FMX_HIP(hipGetLastError());
   }
-  wait_flag(c, c->h_flag.p, seq);
+  if (comm) {
+    comm_allreduce_sum(c, c->d_sum.p, 29);
+    FMX_HIP(hipMemcpyAsync(c->h_G.p, c->d_sum.p, 29 * sizeof(double), hipMemcpyDeviceToHost, st));
+    stream_wait(c);
+  } else {
+    wait_flag(c, c->h_flag.p, seq);
+  }
   match_counts_fetch(c, false);  // the match kernel finished before this one started
   std::memcpy(out, c->h_G.p, 29 * sizeof(double));
 }

@@ -996,7 +996,29 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   c->have_qo = false;
 }
 
-void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted) {
+// The pair-major row scatter of the last sorted match (k_pair_scatter_t over the
+// tiles, or k_pair_scatter per match block for windows wider than kTileMaxPairs).
+void run_pair_scatter(fmx_ctx* c) {
+  if (!c->scatter_pending) return;
+  c->scatter_pending = false;
+  const PairScatter& s = c->ps;
+  const uint32_t nb = s.nb_pl + s.nb_pt;
+  if (nb == 0 || c->K == 0) return;
+  hipStream_t st = c->stream;
+  ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
+  if (s.tiles)
+    hipLaunchKernelGGL(k_pair_scatter_t, dim3(s.ntl_pl + s.ntl_pt), dim3(kTileQ), 0, st, c->n_qpl, c->n_qpt, s.ntl_pl,
+                       s.ntl_pt, s.K, c->m_pair.p, c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p,
+                       c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
+  else
+    hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(kQPB), 0, st, c->n_qpl, c->n_qpt, s.nb_pl, s.K, c->m_pair.p,
+                       c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, s.nb_pt, c->pair_base.p,
+                       c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
+  FMX_HIP(hipGetLastError());
+}
+
+void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
+               bool defer_scatter) {
   hipStream_t st = c->stream;
   const int K = std::max<int>((int)c->K, 1);
   MatchArgs a;
@@ -1075,19 +1097,13 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->match_nb_pl = a.nb_pl;
   c->match_nb = nb;
   c->n_qo = nq;  // query-order rows (k_linearize_total) in both modes
-  if (!sorted) {  // counts come from the match kernel's last block
-  } else if (a.tiles) {  // offsets, counts and chunk table from the match kernel's last block
-    ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
-    if (nb == 0) {  // no launch: an empty chunk table
-      FMX_HIP(hipMemsetAsync(c->n_chunks.p, 0, sizeof(uint32_t), st));
-      FMX_HIP(hipMemsetAsync(c->chunk_range.p, 0, (size_t)(a.K + 1) * sizeof(uint32_t), st));
-    } else if (c->K > 0) {
-      hipLaunchKernelGGL(k_pair_scatter_t, dim3(a.ntl_pl + a.ntl_pt), dim3(kTileQ), 0, st, c->n_qpl, c->n_qpt,
-                         a.ntl_pl, a.ntl_pt, a.K, c->m_pair.p, c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p,
-                         c->hist_off.p, c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
-      FMX_HIP(hipGetLastError());
-    }
-  } else {
+  // Pair-major correspondences: the counts, offsets and chunk table come from the match
+  // kernel's last block (tiled) or from the scan + k_pair_base (wider windows) right
+  // away; the row scatter itself may be deferred (defer_scatter: fmx_match, whose
+  // caller may only read the query-order outputs) until run_pair_scatter.
+  c->ps = PairScatter{a.nb_pl, nb_pt, a.ntl_pl, a.ntl_pt, a.K, a.tiles};
+  c->scatter_pending = false;
+  if (sorted && !a.tiles) {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
     const size_t nh = (size_t)a.K * nb;
     c->scan_scratch.ensure(scan_scratch_size(nh) + 4);
@@ -1098,12 +1114,13 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
                        c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p,
                        c->h_counts.d);
     FMX_HIP(hipGetLastError());
-    if (nb > 0 && c->K > 0) {
-      hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(kQPB), 0, st, c->n_qpl, c->n_qpt, a.nb_pl, a.K, c->m_pair.p,
-                         c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, nb_pt, c->pair_base.p,
-                         c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
-      FMX_HIP(hipGetLastError());
-    }
+  } else if (sorted && nb == 0) {  // no launch: an empty chunk table
+    FMX_HIP(hipMemsetAsync(c->n_chunks.p, 0, sizeof(uint32_t), st));
+    FMX_HIP(hipMemsetAsync(c->chunk_range.p, 0, (size_t)(a.K + 1) * sizeof(uint32_t), st));
+  }
+  if (sorted) {
+    c->scatter_pending = true;
+    if (!defer_scatter) run_pair_scatter(c);
   }
   // per-pair counts reach pinned host memory from k_pair_base; consumed at the next sync
   if (c->prof.on) {  // per-block work counters, only needed for the profile's byte model

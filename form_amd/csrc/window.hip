@@ -361,7 +361,10 @@ void win_timing_collect(fmx_ctx* c, uint32_t grid_chunks) {
 
 // Launch k_win_linearize (win_start); wait for its word and copy npairs x 92 doubles
 // out (win_finish).  The host assembles the x-dependent non-pair terms in between.
-void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double bytes) {
+// out_dev (sharded fmx_linearize): G to this device buffer instead, the completion word
+// to a device scratch word; the caller all-reduces and copies (no win_finish).
+void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double bytes,
+               double* out_dev = nullptr) {
   WinStore& W = c->win;
   if (W.pending) win_finish(c, nullptr);  // an abandoned one (error path): drain it first
   hipStream_t st = c->stream;
@@ -391,6 +394,11 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
   a.hostG = W.hG.d;
   a.seq = next_flag(c);
   a.flag = c->h_flag.d;
+  if (out_dev) {
+    W.dflag.ensure(1);
+    a.hostG = out_dev;
+    a.flag = W.dflag.p;
+  }
   a.dbg = nullptr;
   if (win_timing_on()) {
     if (W.dbg.cap < (size_t)grid_chunks * 8) {
@@ -409,7 +417,7 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
       hipLaunchKernelGGL(k_win_linearize<kWinMaxArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
     FMX_HIP(hipGetLastError());
   }
-  W.pending = true;
+  W.pending = out_dev == nullptr;
   W.pending_seq = a.seq;
   W.pending_np = a.npairs;
   W.pending_grid = grid_chunks;
@@ -439,6 +447,7 @@ void win_persist(fmx_ctx* c, uint64_t j) {
   WinStore& W = c->win;
   hipStream_t st = c->stream;
   if (!c->have_corr) throw StatusError(FMX_E_STATE, "win_persist: no sorted match");
+  run_pair_scatter(c);
   uint64_t npl = 0, npt = 0;
   for (uint32_t k = 0; k < c->K; ++k) {
     npl += c->cnt_pl[k];
@@ -614,6 +623,7 @@ void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double si
 // chunk table): poses[k] = pose of map_scans[k], poses[K] = the current pose.
 void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out) {
   if (!c->have_corr) throw StatusError(FMX_E_STATE, "win_linearize_current: no sorted match");
+  run_pair_scatter(c);
   WinArgs a{};
   a.chunks = c->chunks.p;
   a.n_chunks = c->n_chunks.p;
@@ -641,6 +651,7 @@ void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double
 void win_linearize_pairs(fmx_ctx* c, const double* poses_i, const double* poses_j, double sigma, int mode,
                          double* G_out, double* err_out) {
   if (!c->have_corr) throw StatusError(FMX_E_STATE, "no correspondences (call fmx_match or fmx_corr_set)");
+  run_pair_scatter(c);  // fmx_match deferred it
   const int K = (int)c->K;
   if (K == 0) return;
   if (2 * (size_t)K > 0xFFFFFFu) throw StatusError(FMX_E_INVAL, "too many pairs");
@@ -653,7 +664,15 @@ void win_linearize_pairs(fmx_ctx* c, const double* poses_i, const double* poses_
   }
   if (c->counts_pending) match_counts_fetch(c);  // exact byte model (rows per type)
   W.hG.ensure((size_t)K * kWinG);
-  std::memset(W.hG.p, 0, (size_t)K * kWinG * sizeof(double));  // pairs without rows are never written
+  // pairs without rows are never written: zero them first (sharded: in the device
+  // buffer the ranks all-reduce, on the stream ahead of the kernel)
+  const bool comm = c->comm != nullptr;
+  if (comm) {
+    c->d_sum.ensure((size_t)K * kWinG);
+    FMX_HIP(hipMemsetAsync(c->d_sum.p, 0, (size_t)K * kWinG * sizeof(double), c->stream));
+  } else {
+    std::memset(W.hG.p, 0, (size_t)K * kWinG * sizeof(double));
+  }
   WinArgs a{};
   a.chunks = c->chunks.p;
   a.n_chunks = c->n_chunks.p;
@@ -665,8 +684,15 @@ void win_linearize_pairs(fmx_ctx* c, const double* poses_i, const double* poses_
   a.ld_pt = c->ld_pt;
   a.implicit_j = kPairedPoses;
   a.inv = 1.0 / sigma;  // FastIsotropic invsigma_ (gtsam.hpp:96)
-  win_start(c, a, c->max_chunks, table.data(), 2 * K, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * K);
-  win_finish(c, nullptr);
+  win_start(c, a, c->max_chunks, table.data(), 2 * K, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * K,
+            comm ? c->d_sum.p : nullptr);
+  if (comm) {  // every pair's G (and error) summed over the ranks on this stream
+    comm_allreduce_sum(c, c->d_sum.p, (size_t)K * kWinG);
+    FMX_HIP(hipMemcpyAsync(W.hG.p, c->d_sum.p, (size_t)K * kWinG * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    stream_wait(c);
+  } else {
+    win_finish(c, nullptr);
+  }
   const double* hg = W.hG.p;
   for (int k = 0; k < K; ++k) {
     const double* g = hg + (size_t)k * kWinG;

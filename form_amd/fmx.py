@@ -25,7 +25,7 @@ _LIB = None
 
 FMX_OK = 0
 _STATUS = {1: "FMX_E_INVAL", 2: "FMX_E_SIZE", 3: "FMX_E_OOM", 4: "FMX_E_HIP", 5: "FMX_E_STATE",
-           6: "FMX_E_RANGE"}
+           6: "FMX_E_RANGE", 7: "FMX_E_RCCL"}
 
 
 class FmxError(RuntimeError):
@@ -80,7 +80,7 @@ EXPORTED = [
     "fmx_keypoints_remove", "fmx_map_build", "fmx_match", "fmx_match_download", "fmx_map_insert",
     "fmx_corr_set", "fmx_linearize", "fmx_error", "fmx_linearize_matched", "fmx_register_scan", "fmx_current_pose",
     "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
-    "fmx_profile_name", "fmx_profile_read", "fmx_sync",
+    "fmx_profile_name", "fmx_profile_read", "fmx_sync", "fmx_comm_unique_id", "fmx_comm_init",
 ]
 
 
@@ -294,6 +294,13 @@ class Context:
         self._chk(self._L.fmx_linearize_matched(self.h, _p(pose), C.c_double(sigma), _p(out)))
         return out[:28].copy(), float(out[28])
 
+    # ---------------------------------------------------------------- multi-GPU
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int):
+        """Attach an RCCL communicator (see comm_unique_id): linearization sums are then
+        all-reduced over the ranks on the device, on this context's stream."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._chk(self._L.fmx_comm_init(self.h, buf, C.c_int(nranks), C.c_int(rank)))
+
     # ---------------------------------------------------------------- estimator
     def register_scan(self, scan):
         on_dev, ptr, n, keep = _scan_ptr(scan)
@@ -309,10 +316,10 @@ class Context:
         return T.reshape(3, 4)
 
     def last_stats(self) -> dict:
-        s = np.zeros(8, np.uint64)
-        self._chk(self._L.fmx_last_stats(self.h, _p(s)))
         keys = ["icp_iters", "lm_iters", "matched_planar", "matched_point", "map_planar", "map_point",
-                "linearizations", "map_scans"]
+                "linearizations", "map_scans", "host_waits"]
+        s = np.zeros(len(keys), np.uint64)
+        self._chk(self._L.fmx_last_stats(self.h, _p(s), C.c_int(len(keys))))
         return {k: int(v) for k, v in zip(keys, s)}
 
     def match_work(self) -> dict:
@@ -355,6 +362,15 @@ def _scan_ptr(scan):
     if a.ndim != 2 or a.shape[1] != 4:
         raise ValueError("scan must be (N, 4) float32 (PointXYZf layout)")
     return 0, _p(a), a.shape[0], a
+
+
+def comm_unique_id() -> bytes:
+    """fmx_comm_unique_id: the 128-byte RCCL id one rank creates and shares."""
+    buf = (C.c_uint8 * 128)()
+    st = lib().fmx_comm_unique_id(buf)
+    if st != FMX_OK:
+        raise FmxError(st, "fmx_comm_unique_id failed (RCCL missing?)")
+    return bytes(buf)
 
 
 class Estimator:

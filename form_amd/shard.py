@@ -77,10 +77,29 @@ def compose(A: np.ndarray, B: np.ndarray) -> np.ndarray:
 
 
 # ----------------------------------------------------------------- C5 synthetic data
+# Terrain: z = A (sin(2 pi x / LX) + cos(2 pi y / LY)).  The wavelengths are a few
+# voxels and incommensurate, so the surface normals vary in x AND y (slopes up to
+# ~0.4 per term): point-to-plane residuals then constrain x, y and yaw as well as
+# z / roll / pitch (a flat or nearly flat field leaves them unobservable).
+TERRAIN_A, TERRAIN_LX, TERRAIN_LY = 0.6, 9.7, 13.3
+# Sensor range of the 2M-point "scan" (OS2-128 class, ~240 m): queries are map
+# surface samples within this radius of the sensor.  With the injected rotation
+# (C5_OFFSET) the farthest points start <= ~0.45 m from their surface, inside the
+# 0.8 m match radius, so ICP converges from the offset pose.
+C5_RANGE_M = 240.0
+
+
+def c5_offset() -> np.ndarray:
+    """The injected sensor-pose error (truth): 5 cm translation, 0.1 deg yaw, 0.05 deg
+    roll and pitch (GTSAM tangent [w; v])."""
+    d = np.radians
+    return expmap(np.array([d(0.05), d(-0.05), d(0.1), 0.03, -0.04, 0.0]))
+
+
 def terrain_map(n_side: int, w: float, seed: int, device="cpu"):
-    """Jittered terrain grid: one planar feature per w-voxel over n_side x n_side
-    voxels, heights within +-0.2 m, normals of the height field.  Returns (pos4,
-    nrm4) float32 tensors (N, 4) in the map scan's frame."""
+    """Jittered terrain grid: one planar feature per w-column over n_side x n_side
+    columns (centred on the origin), on the height field above with its normals.
+    Returns (pos4, nrm4) float32 tensors (N, 4) in the map scan's frame."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     n = n_side * n_side
     ij = torch.arange(n, device=device)
@@ -89,27 +108,31 @@ def terrain_map(n_side: int, w: float, seed: int, device="cpu"):
     jit = torch.rand((n, 2), generator=g, dtype=torch.float64).to(device)
     x = (i + 0.1 + 0.8 * jit[:, 0]) * w - 0.5 * n_side * w
     y = (j + 0.1 + 0.8 * jit[:, 1]) * w - 0.5 * n_side * w
-    a, b = 0.7, 0.9
-    z = 0.1 * torch.sin(a * x) + 0.1 * torch.cos(b * y)  # |z| <= 0.2
-    nx = -0.1 * a * torch.cos(a * x)
-    ny = 0.1 * b * torch.sin(b * y)
-    nrm = torch.stack([-nx, -ny, torch.ones_like(x)], 1)
+    kx, ky = 2 * math.pi / TERRAIN_LX, 2 * math.pi / TERRAIN_LY
+    z = TERRAIN_A * (torch.sin(kx * x) + torch.cos(ky * y))
+    dzdx = TERRAIN_A * kx * torch.cos(kx * x)
+    dzdy = -TERRAIN_A * ky * torch.sin(ky * y)
+    nrm = torch.stack([-dzdx, -dzdy, torch.ones_like(x)], 1)
     nrm = nrm / nrm.norm(dim=1, keepdim=True)
     pos4 = torch.zeros((n, 4), dtype=torch.float32, device=device)
-    pos4[:, 0], pos4[:, 1], pos4[:, 2] = x.float(), y.float(), (z + 0.2).float()
+    pos4[:, 0], pos4[:, 1], pos4[:, 2] = x.float(), y.float(), z.float()
     nrm4 = torch.zeros((n, 4), dtype=torch.float32, device=device)
     nrm4[:, :3] = nrm.float()
     return pos4, nrm4
 
 
-def make_queries(pos4, nrm4, n_query: int, offset: np.ndarray, noise: float, seed: int):
-    """n_query map features perturbed by N(0, noise) and expressed in the frame of a
-    sensor offset by `offset` (3x4): q_local = offset^-1 * (p + e)."""
+def make_queries(pos4, nrm4, n_query: int, offset: np.ndarray, noise: float, seed: int,
+                 radius: float = C5_RANGE_M):
+    """An n_query-point scan taken from a sensor at pose `offset` (3x4, world <- sensor):
+    map surface samples within `radius` of the origin (drawn with replacement, each
+    with N(0, noise) range noise), in the sensor frame: q = offset^-1 (p + e).  Returned
+    in map (grid) order: a LiDAR scan's points arrive spatially coherent."""
     dev = pos4.device
     g = torch.Generator(device="cpu").manual_seed(seed)
-    # a random subset of the map features, kept in map (grid) order: a LiDAR scan's
-    # points arrive spatially coherent, not shuffled
-    sel = torch.randperm(pos4.shape[0], generator=g)[:n_query].sort().values.to(dev)
+    r2 = (pos4[:, 0].double() ** 2 + pos4[:, 1].double() ** 2)
+    inside = torch.nonzero(r2 <= radius * radius).squeeze(1)
+    pick = torch.randint(0, inside.shape[0], (n_query,), generator=g).to(dev)
+    sel = inside[pick].sort().values
     p = pos4[sel, :3].double() + noise * torch.randn((n_query, 3), generator=g, dtype=torch.float64).to(dev)
     R = torch.as_tensor(offset[:, :3], dtype=torch.float64, device=dev)
     t = torch.as_tensor(offset[:, 3], dtype=torch.float64, device=dev)
@@ -120,3 +143,10 @@ def make_queries(pos4, nrm4, n_query: int, offset: np.ndarray, noise: float, see
     q4[:, :3] = ql.float()
     n4[:, :3] = nl.float()
     return q4, n4
+
+
+def pose_error(T: np.ndarray, Ttrue: np.ndarray) -> tuple[float, float]:
+    """(translation error m, rotation error rad) of T against Ttrue."""
+    D = compose(np.hstack([Ttrue[:, :3].T, -(Ttrue[:, :3].T @ Ttrue[:, 3])[:, None]]), T)
+    ang = math.acos(max(-1.0, min(1.0, (np.trace(D[:, :3]) - 1) / 2)))
+    return float(np.linalg.norm(D[:, 3])), ang

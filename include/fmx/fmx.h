@@ -38,7 +38,8 @@ typedef enum fmx_status {
   FMX_E_OOM = 3,   /* device allocation failed or a capacity was exceeded */
   FMX_E_HIP = 4,   /* HIP runtime error */
   FMX_E_STATE = 5, /* call out of order (e.g. match before map_build) */
-  FMX_E_RANGE = 6  /* voxel coordinate outside the +-2^20 packed-key range */
+  FMX_E_RANGE = 6, /* voxel coordinate outside the +-2^20 packed-key range */
+  FMX_E_RCCL = 7   /* RCCL missing or a collective failed (multi-GPU only) */
 } fmx_status;
 
 /* form::FeatureExtractor::Params (form/feature/extraction.hpp:59-88). */
@@ -173,6 +174,19 @@ fmx_status fmx_error(fmx_ctx* ctx, const double* poses_i34, const double* poses_
  * packed upper 7 x 7, out[28]: the error 0.5 ||r/sigma||^2. */
 fmx_status fmx_linearize_matched(fmx_ctx* ctx, const double pose_j34[12], double sigma, double out[29]);
 
+/* ---------------- multi-GPU: the sharded C5 path -----------
+ * One rank per GPU, each with the same voxel map and a contiguous shard of the
+ * queries.  fmx_comm_unique_id on one rank; the caller shares the 128 bytes (e.g. a
+ * torch.distributed broadcast); fmx_comm_init on every rank (collective).  From then
+ * on the context's linearization sums — fmx_linearize_matched's 7 x 7 system and
+ * fmx_linearize / fmx_error's per-pair G — are all-reduced (fp64 sum) over the ranks
+ * with RCCL on the context's HIP stream, device buffer to device buffer, before they
+ * reach the host, so every rank returns the identical global system.  The reference
+ * has no multi-device path; this is the north star's "RCCL all-reduce of the normal
+ * equations over xGMI".  RCCL is loaded on first use (FMX_E_RCCL if absent). */
+fmx_status fmx_comm_unique_id(uint8_t id[128]);
+fmx_status fmx_comm_init(fmx_ctx* ctx, const uint8_t id[128], int nranks, int rank);
+
 /* ---------------- host adapter: Estimator::register_scan -------------------
  * form::Estimator::register_scan (form/form.hpp:82-83, form.cpp:40-114): predict,
  * extract, map build, ICP loop (match + LM), final LM, insert_matches, keyscan
@@ -186,9 +200,11 @@ fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, i
 /* Estimator::current_lidar_estimate (form/form.hpp:79). */
 fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
 
-/* Statistics of the last register_scan: {icp_iters, lm_iters, matched_planar,
- * matched_point, map_planar, map_point, linearizations, map_scans}. */
-fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t stats[8]);
+/* Statistics of the last register_scan, the first n of: {icp_iters, lm_iters,
+ * matched_planar, matched_point, map_planar, map_point, linearizations, map_scans,
+ * host_waits (host<->device round trips: waits on a completion word or the stream)};
+ * entries past the known ones read 0. */
+fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t* stats, int n);
 /* Work of the last fmx_match (counted by the kernel, available while profiling is
  * enabled): queries, hash probes, candidate records distance-tested. */
 fmx_status fmx_match_work(fmx_ctx* ctx, double work[3]);

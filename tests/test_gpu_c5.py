@@ -1,0 +1,193 @@
+"""C5 scale: the full 50M-voxel terrain submap on the
+device, a sampled 64k-point scan, bit-exact against the CPU oracle's VoxelMap; the
+registration converges from the injected offset; the sharded exchange step (RCCL
+communicator on the context stream; two ranks each running the HIP path on its shard)
+reproduces the unsharded normal equations.
+
+The oracle cannot hold 50M voxels cheaply, and does not need to: a query's nearest
+neighbour lies in its 27 voxels (map.tpp:54-91), so the oracle map is built from every
+terrain feature within +-3 grid columns of a sampled query — a superset of those 27
+voxels' contents — while the device matches against the whole map.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from form_amd import shard, synth
+
+pytestmark = pytest.mark.gpu
+
+SIDE, W = 7071, 0.8  # 50M voxels, the bench's C5 map
+I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
+
+
+@pytest.fixture(scope="module")
+def c5_map():
+    import torch
+    pos4, nrm4 = shard.terrain_map(SIDE, W, synth.SEED, "cuda:0")
+    torch.cuda.synchronize()
+    return pos4, nrm4
+
+
+def _ctx(fmx, n_map):
+    return fmx.Context(fmx.EstimatorParams(keypoint_pool_capacity=n_map + 1024, voxel_subdivision=1))
+
+
+def _near_features(pos4, nrm4, qw):
+    """Every terrain feature within +-3 grid columns of the world points qw (numpy)."""
+    import torch
+    ic = np.rint(qw[:, 0] / W + 0.5 * SIDE - 0.5).astype(np.int64)
+    jc = np.rint(qw[:, 1] / W + 0.5 * SIDE - 0.5).astype(np.int64)
+    d = np.arange(-3, 4)
+    ii = np.clip(ic[:, None, None] + d[None, :, None], 0, SIDE - 1)
+    jj = np.clip(jc[:, None, None] + d[None, None, :], 0, SIDE - 1)
+    idx = np.unique((ii * SIDE + jj).ravel())
+    t = torch.as_tensor(idx, device=pos4.device)
+    feats = torch.cat([pos4[t, :3], nrm4[t, :3]], 1).cpu().numpy()
+    return np.ascontiguousarray(feats)
+
+
+def test_c5_match_full_map_matches_oracle(fmx_mod, oracle, c5_map):
+    pos4, nrm4 = c5_map
+    n_map = pos4.shape[0]
+    assert n_map == SIDE * SIDE > 50_000_000 - 100_000
+    Tt = shard.c5_offset()
+    q4, n4 = shard.make_queries(pos4, nrm4, 65536, Tt, 0.03, 77)
+    ctx = _ctx(fmx_mod, n_map)
+    ctx.keypoints_add_device(0, pos4, nrm4)
+    ctx.map_build([0], I34[None], W)
+    ctx.set_queries_device(q4, n4)
+    Tj = shard.expmap(np.array([0.0005, -0.0003, 0.0008, 0.02, 0.01, -0.01]))  # an ICP iterate
+    cpl, _ = ctx.match(Tj, W)
+    got = ctx.match_download()
+    Q = np.concatenate([q4[:, :3].cpu().numpy(), n4[:, :3].cpu().numpy()], 1)
+    qw = Q[:, :3].astype(np.float64) @ Tj[:, :3].T + Tj[:, 3]
+    om = oracle.VoxelMap(W, 0)
+    om.add_scan(0, I34, _near_features(pos4, nrm4, qw))
+    ref = om.match(Q, Tj)
+    acc = ref["found"] & (ref["d2"] < W * W)
+    assert acc.sum() > 60000
+    assert np.array_equal(got["pair"] >= 0, acc)
+    assert np.array_equal(got["d2"][acc], ref["d2"][acc])
+    assert np.array_equal(got["pi"][acc], ref["pi"][acc])
+    assert np.array_equal(got["ni"][acc], ref["ni"][acc])
+    assert cpl[0] == acc.sum()
+    # the summed single-pose system over those matches
+    S, e = ctx.linearize_matched(Tj, 0.1)
+    G, er = oracle.linearize(np.array([acc.sum()], np.uint32), ref["pi"][acc], ref["ni"][acc],
+                             Q[acc, :3].astype(np.float64), np.array([0], np.uint32), np.zeros((0, 3)),
+                             np.zeros((0, 3)), I34[None], Tj[None], 0.1, True)
+    assert np.all(np.abs(S - G[0]) <= 1e-10 * np.abs(G[0]).max())
+    assert abs(e - er[0]) <= 1e-10 * er[0]
+
+
+def test_c5_registration_converges(fmx_mod, c5_map):
+    """ICP from the identity against the full map recovers the injected 5 cm / 0.1 deg
+    offset to well below it (the terrain constrains x, y and yaw too)."""
+    pos4, nrm4 = c5_map
+    Tt = shard.c5_offset()
+    q4, n4 = shard.make_queries(pos4, nrm4, 262144, Tt, 0.03, 78)
+    ctx = _ctx(fmx_mod, pos4.shape[0])
+    ctx.keypoints_add_device(0, pos4, nrm4)
+    ctx.map_build([0], I34[None], W)
+    ctx.set_queries_device(q4, n4)
+    T = I34.copy()
+    for it in range(30):
+        ctx.match(T, W)
+        S, _ = ctx.linearize_matched(T, 0.1)
+        dx = shard.gauss_newton_step(S)
+        T = shard.compose(T, shard.expmap(dx))
+        if np.linalg.norm(dx) < 1e-4:
+            break
+    et, er = shard.pose_error(T, Tt)
+    e0t, e0r = shard.pose_error(I34, Tt)
+    assert it < 10
+    assert et < 0.02 * e0t and er < 0.02 * e0r, (et, er, e0t, e0r)
+
+
+def test_comm_single_rank_is_identity(fmx_mod, c5_map):
+    """A one-rank RCCL communicator (the device all-reduce path on a 1-GPU box): the
+    all-reduced systems equal the plain ones bit for bit."""
+    pos4, nrm4 = c5_map
+    q4, n4 = shard.make_queries(pos4, nrm4, 100000, shard.c5_offset(), 0.03, 79)
+    out = []
+    for use_comm in (False, True):
+        ctx = _ctx(fmx_mod, pos4.shape[0])
+        if use_comm:
+            ctx.comm_init(fmx_mod.comm_unique_id(), 1, 0)
+        ctx.keypoints_add_device(0, pos4, nrm4)
+        ctx.map_build([0], I34[None], W)
+        ctx.set_queries_device(q4, n4)
+        ctx.match(I34, W)
+        S, e = ctx.linearize_matched(I34, 0.1)
+        G, err = ctx.linearize(I34[None], I34[None], 0.1, False)
+        out.append((S, e, G, err))
+        ctx.close()
+    (S0, e0, G0, r0), (S1, e1, G1, r1) = out
+    assert np.array_equal(S0, S1) and e0 == e1
+    assert np.array_equal(G0, G1) and np.array_equal(r0, r1)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+
+    from form_amd import fmx
+    from form_amd import shard as sh
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    side = 1501  # 2.25M voxels: the sharding logic, not the map size, is under test
+    pos4, nrm4 = sh.terrain_map(side, W, synth.SEED, "cuda:0")
+    q4, n4 = sh.make_queries(pos4, nrm4, 200000, sh.c5_offset(), 0.03, 80)
+    b, e = sh.shard_bounds(q4.shape[0], rank, world)
+    ctx = fmx.Context(fmx.EstimatorParams(keypoint_pool_capacity=pos4.shape[0] + 1024))
+    ctx.keypoints_add_device(0, pos4, nrm4)
+    ctx.map_build([0], I34[None], W)
+    ctx.set_queries_device(q4[b:e].contiguous(), n4[b:e].contiguous())
+    Tj = sh.expmap(np.array([0.0005, -0.0003, 0.0008, 0.02, 0.01, -0.01]))
+    ctx.match(Tj, W)
+    S, err = ctx.linearize_matched(Tj, 0.1)
+    Ssum = sh.allreduce_sum(np.append(S, err))  # the host exchange (gloo) over the HIP results
+    np.save(os.path.join(out_dir, f"S_{rank}.npy"), Ssum)
+    torch.cuda.synchronize()
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_match_unsharded(fmx_mod, tmp_path):
+    """World size 2 (gloo for the exchange, both ranks on this box's GPU): each rank
+    runs the HIP match + linearization on its half of the points; the all-reduced
+    system equals one process's unsharded system to 1e-10 and is identical on both
+    ranks."""
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    S = [np.load(tmp_path / f"S_{r}.npy") for r in range(world)]
+    assert np.array_equal(S[0], S[1])
+    pos4, nrm4 = shard.terrain_map(1501, W, synth.SEED, "cuda:0")
+    q4, n4 = shard.make_queries(pos4, nrm4, 200000, shard.c5_offset(), 0.03, 80)
+    ctx = _ctx(fmx_mod, pos4.shape[0])
+    ctx.keypoints_add_device(0, pos4, nrm4)
+    ctx.map_build([0], I34[None], W)
+    ctx.set_queries_device(q4, n4)
+    Tj = shard.expmap(np.array([0.0005, -0.0003, 0.0008, 0.02, 0.01, -0.01]))
+    ctx.match(Tj, W)
+    S1, e1 = ctx.linearize_matched(Tj, 0.1)
+    ref = np.append(S1, e1)
+    assert np.all(np.abs(S[0] - ref) <= 1e-10 * np.abs(ref).max())
