@@ -947,8 +947,8 @@ void fmx_destroy(fmx_ctx* c) {
   }
   {
     auto& M = c->map;
-    M.table.release(); M.bcnt.release(); M.bcur.release(); M.tpos.release(); M.tnrm.release(); M.rslot.release();
-    M.rseg.release(); M.pos.release(); M.nrm.release(); M.seg.release(); M.rid.release();
+    M.table.release(); M.bcnt.release(); M.state.release(); M.rinfo.release(); M.claim.release(); M.dense.release();
+    M.pos.release(); M.nrm.release();
   }
   c->h_mapposes.release(); c->map_blob.release();
   c->blk_lo.release(); c->blk_hi.release(); c->h_work.release();

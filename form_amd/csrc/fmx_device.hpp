@@ -227,18 +227,23 @@ inline void exclusive_scan(In in, Out out, size_t n, uint32_t* scratch /* >= nb 
 inline size_t scan_scratch_size(size_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
 
 // ---------------------------------------------------------------- voxel keys
-// Packed voxel key: 21 bits per signed coordinate (offset 2^20), +1 so that 0 is
-// the empty slot marker.  Valid coordinates: |c| < 2^20 - 1.
-constexpr int kKeyBias = 1 << 20;
+// Brick key: the brick coordinates (cell >> 1), 19 bits each with an offset of 2^18,
+// under a 6-bit build epoch in bits 57-62.  A bucket whose key carries another epoch
+// (0 included: never written) is empty for the current build, so a rebuild needs no
+// table clear: the epoch advances instead (the host clears the table once every 63
+// builds, when the epoch wraps).  Valid cell coordinates: |c| < 2^19 - 2.
+constexpr int kKeyBias = 1 << 18;
+constexpr int kEpochShift = 57;
+constexpr uint32_t kEpochMax = 63;
 __device__ __forceinline__ uint64_t pack_key(int x, int y, int z) {
-  return (((uint64_t)(uint32_t)(x + kKeyBias) << 42) | ((uint64_t)(uint32_t)(y + kKeyBias) << 21) |
-          (uint64_t)(uint32_t)(z + kKeyBias)) +
-         1ull;
+  return ((uint64_t)(uint32_t)(x + kKeyBias) << 38) | ((uint64_t)(uint32_t)(y + kKeyBias) << 19) |
+         (uint64_t)(uint32_t)(z + kKeyBias);
 }
 __device__ __forceinline__ bool key_in_range(int x, int y, int z) {
-  const int L = kKeyBias - 2;
+  const int L = 2 * kKeyBias - 2;
   return x > -L && x < L && y > -L && y < L && z > -L && z < L;
 }
+__device__ __forceinline__ uint32_t key_epoch(uint64_t k) { return (uint32_t)(k >> kEpochShift); }
 __device__ __forceinline__ uint64_t mix64(uint64_t k) {  // splitmix64 finalizer
   k ^= k >> 30;
   k *= 0xbf58476d1ce4e5b9ull;
@@ -251,15 +256,18 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {  // splitmix64 finalizer
 // Brick: the 2 x 2 x 2 cells (x, y, z) >> 1 of one 64-B bucket — the 27-cell
 // neighbourhood of any cell lies in at most 8 bricks, and neighbouring queries share
 // them.  Records of cell c (c = (x & 1) | (y & 1) << 1 | (z & 1) << 2) are
-// [beg[c], beg[c + 1]); empty buckets have key 0.  pad[0] of the extra bucket after
-// the table is the map's range-error word.
+// [beg[c], beg[c + 1]); bit c of `dense` marks a cell stored with a sub-cell header
+// (voxelmap.hip, dense cells).
 struct alignas(64) Brick {
-  unsigned long long key;  // pack_key of the brick coordinates
+  unsigned long long key;  // epoch | pack_key of the brick coordinates
   uint32_t beg[9];
-  uint32_t pad[5];
+  uint32_t dense;
+  uint32_t pad[4];
 };
 static_assert(sizeof(Brick) == 64, "brick = 64 B");
-__device__ __forceinline__ uint64_t brick_key(int x, int y, int z) { return pack_key(x >> 1, y >> 1, z >> 1); }
+__device__ __forceinline__ uint64_t brick_key(int x, int y, int z, uint32_t epoch) {
+  return ((uint64_t)epoch << kEpochShift) | pack_key(x >> 1, y >> 1, z >> 1);
+}
 __device__ __forceinline__ uint32_t brick_cell(int x, int y, int z) {
   return (uint32_t)((x & 1) | ((y & 1) << 1) | ((z & 1) << 2));
 }

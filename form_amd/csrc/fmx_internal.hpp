@@ -135,20 +135,20 @@ struct Pool {
   std::map<uint64_t, std::pair<uint64_t, uint32_t>> ranges;  // scan -> (offset, count)
 };
 
-// One built voxel map (VoxelMap<P>, map.hpp:66-94) in HBM.
-// Device voxel map of both feature types (one build): table = planar slots
-// [0, cap[0]), point slots [cap[0], cap[0] + cap[1]), then one slot holding the
-// range-error word; records (build order and voxel-sorted) planar [0, n[0]) then
-// point [n[0], n[0] + n[1]); normals for planar records only.
+// One built voxel map (VoxelMap<P>, map.hpp:66-94) in HBM, both feature types
+// (voxelmap.hip): table = planar bricks [0, cap[0]), point bricks [cap[0], cap[0] +
+// cap[1]); records planar [0, n[0]) then point [n[0], n[0] + n[1]) (+ the sub-cell
+// headers of dense cells), grouped by cell; normals for planar records only.
 struct VoxMap {
-  DBuf<uint4> table;            // fmx::Brick
-  DBuf<uint32_t> bcnt, bcur;    // per brick cell: record count, scatter cursor (build only)
+  DBuf<uint4> table;            // fmx::Brick (epoch-tagged keys: no clear between builds)
+  DBuf<uint32_t> bcnt;          // per brick cell: record count (zero between builds)
+  DBuf<uint4> state;            // two alternating BuildState (voxelmap.hip)
+  uint32_t epoch = 0;           // build epoch of the current map (1..63)
   uint64_t cap[2] = {0, 0};     // powers of two
   uint32_t n[2] = {0, 0};
-  DBuf<double4> tpos, tnrm;     // transformed records, build order
-  DBuf<uint32_t> rslot, rseg;   // per build-order record
-  DBuf<double4> pos, nrm;       // voxel-sorted
-  DBuf<uint32_t> seg, rid;      // voxel-sorted segment (pair) and build-order id
+  DBuf<uint2> rinfo;            // per build-order record: cell, rank in the cell
+  DBuf<uint32_t> claim, dense;  // claimed bricks, dense cells of the last build
+  DBuf<double4> pos, nrm;       // grouped by cell
 };
 
 struct Seg {
@@ -268,7 +268,7 @@ struct fmx_ctx {
   double cell_w = 0;    // internal cell width of the built map
   int cell_m = 1;       // subdivision: rings searched
   bool have_map = false;
-  uint32_t* map_err_p = nullptr;  // range-error word (in map.table)
+  uint32_t* map_err_p = nullptr;  // range-error word of the last build (in map.state)
 
   // ---- match results (query-indexed; planar then point)
   fmx::DBuf<int32_t> m_pair;
@@ -357,6 +357,70 @@ struct HostTiming {
 inline HostTiming& host_timing() {
   static HostTiming h;
   return h;
+}
+// Match-kernel diagnostics (env FMX_MATCH_DIAG; needs the profiled path, which
+// downloads the per-block work words): per launch the kernel span, block-duration
+// percentiles, when 50/90/99 % of the blocks had finished, and the largest per-query
+// candidate counts of the slowest blocks.  Printed to stderr at exit.
+struct MatchDiag {
+  bool on = std::getenv("FMX_MATCH_DIAG") != nullptr;
+  uint64_t launches = 0;
+  double span = 0, p50 = 0, p90 = 0, p99 = 0, pmax = 0, f50 = 0, f90 = 0, f99 = 0, mq_all = 0, mq_slow = 0;
+  uint64_t mq_hist[8] = {0};
+  ~MatchDiag() {
+    if (!on || !launches) return;
+    const double n = (double)launches;
+    fprintf(stderr,
+            "match diag: %llu launches; span %.1f us; block dur p50 %.1f p90 %.1f p99 %.1f max %.1f us; "
+            "blocks done at 50/90/99%%: %.1f %.1f %.1f us; max query cands per block: mean %.1f, slowest 1%% %.1f\n",
+            (unsigned long long)launches, span / n, p50 / n, p90 / n, p99 / n, pmax / n, f50 / n, f90 / n, f99 / n,
+            mq_all / n, mq_slow / n);
+    fprintf(stderr, "match diag: block max-query-cands histogram <16 <32 <64 <128 <256 <512 <1024 >=1024:");
+    for (uint64_t h : mq_hist) fprintf(stderr, " %llu", (unsigned long long)h);
+    fprintf(stderr, "\n");
+  }
+};
+inline MatchDiag& match_diag() {
+  static MatchDiag d;
+  return d;
+}
+// w: kWorkWords (8) words per block: probes, cands, max query cands, 0, t_begin, t_end, 0, 0
+inline void match_diag_add(const uint32_t* w, uint32_t nb) {
+  MatchDiag& d = match_diag();
+  if (!d.on || nb == 0) return;
+  uint32_t t0 = w[4];
+  for (uint32_t b = 1; b < nb; ++b)
+    if ((int32_t)(w[8 * b + 4] - t0) < 0) t0 = w[8 * b + 4];
+  std::vector<double> dur(nb), fin(nb);
+  std::vector<std::pair<double, uint32_t>> by;
+  double mq = 0;
+  for (uint32_t b = 0; b < nb; ++b) {
+    dur[b] = (double)(int32_t)(w[8 * b + 5] - w[8 * b + 4]) * 0.01;  // 100 MHz -> us
+    fin[b] = (double)(int32_t)(w[8 * b + 5] - t0) * 0.01;
+    by.push_back({dur[b], w[8 * b + 2]});
+    mq += w[8 * b + 2];
+    int h = 0;
+    for (uint32_t v = w[8 * b + 2]; v >= 16 && h < 7; v >>= 1) ++h;
+    d.mq_hist[h]++;
+  }
+  std::sort(dur.begin(), dur.end());
+  std::sort(fin.begin(), fin.end());
+  std::sort(by.begin(), by.end());
+  auto pct = [&](const std::vector<double>& v, double q) { return v[std::min<size_t>(v.size() - 1, (size_t)(q * v.size()))]; };
+  d.launches++;
+  d.span += fin.back();
+  d.p50 += pct(dur, 0.5);
+  d.p90 += pct(dur, 0.9);
+  d.p99 += pct(dur, 0.99);
+  d.pmax += dur.back();
+  d.f50 += pct(fin, 0.5);
+  d.f90 += pct(fin, 0.9);
+  d.f99 += pct(fin, 0.99);
+  d.mq_all += mq / nb;
+  const size_t ns = std::max<size_t>(1, nb / 100);
+  double ms = 0;
+  for (size_t i = nb - ns; i < nb; ++i) ms += by[i].second;
+  d.mq_slow += ms / ns;
 }
 inline double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();

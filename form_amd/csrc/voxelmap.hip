@@ -34,6 +34,9 @@
 #ifndef FMX_VM_NS
 #define FMX_VM_NS g8
 #endif
+#ifndef FMX_DENSE_MIN
+#define FMX_DENSE_MIN 64
+#endif
 
 namespace fmx {
 // This file is compiled twice (Makefile): FMX_MATCH_GROUP 8 -> fmx::g8 and 4 -> fmx::g4;
@@ -53,7 +56,38 @@ __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
 
 // Both feature types in one launch (the fused VoxMap layout, fmx_internal.hpp):
 // record rec < n0 is planar record rec, else point record rec - n0; each type has its
-// own table section (point slots at off1) and segment list.
+// own table section (point bricks at off1) and segment list.
+//
+// The build (map.tpp:128-146 + push_back :41-52), four launches, no table clear:
+//   k_map_insert  one lane per record: world transform, voxel key, claim or find the
+//                 brick (epoch-tagged CAS, linear probing; a claim appends the brick to
+//                 the claim list), count the record into its cell (the returned count
+//                 is the record's rank in the cell)
+//   k_map_alloc   one lane per claimed brick: the cells' record ranges (wave scan +
+//                 one atomic per wave and type), dense cells get a sub-cell header;
+//                 the counts are reset for the next build
+//   k_map_scatter one lane per record: the record at its cell's first slot + rank
+//   k_map_dense   one block per dense cell (> kDenseMin records): counting sort of
+//                 its records into 4 x 4 x 4 sub-cells, header = the sub-cell ends
+// The order of records inside a cell (and of the cells' ranges) follows the atomics,
+// so it varies from build to build; nothing observable depends on it: k_match's
+// argmin is over the total order (d^2, reference shift rank, build order).
+struct BuildState {  // per build, two alternating copies (the other is cleared)
+  uint32_t nclaim;   // claimed bricks
+  uint32_t cur[2];   // record slot cursors (planar from 0, point from BuildArgs::pt_base)
+  uint32_t err;      // range error: a record outside the packable key range
+  uint32_t ndense;   // dense cells
+  uint32_t pad[3];
+};
+constexpr int kDenseMin = FMX_DENSE_MIN;  // records that make a cell dense
+constexpr int kSubPerAxis = 4;            // dense cells: 4 x 4 x 4 sub-cells of w / 4
+constexpr int kSubCells = kSubPerAxis * kSubPerAxis * kSubPerAxis;
+constexpr int kHdr = kSubCells * 4 / 32;  // header slots (double4) holding the 64 u32 sub-cell ends
+constexpr int kDenseThreads = 1024;
+constexpr int kDenseRecs = 8;             // records per thread: dense cells up to 8192 records are sorted
+constexpr uint32_t kUnsorted = 0xFFFFFFFFu;  // header[0] of a dense cell too large to sort
+constexpr uint32_t kDenseGrid = 1024;     // k_map_dense blocks (each loops over the dense list)
+
 struct BuildArgs {
   const float4* pool_pos[2];
   const float4* pool_nrm;  // planar only
@@ -61,98 +95,222 @@ struct BuildArgs {
   int K;
   const double* poses;
   uint32_t n0, n;  // planar records, all records
+  uint32_t pt_base;  // first point slot: planar records + the most header slots they can need
   double w;
   Brick* bricks;
-  uint32_t* bcnt;   // [brick][8] record counts
+  uint32_t* bcnt;   // [brick][8] record counts, zero between builds
   uint64_t mask[2];
-  uint64_t off1;  // first point slot / brick
-  double4* tpos;
-  double4* tnrm;  // [n0]
-  uint32_t* rslot;
-  uint32_t* rseg;
-  uint32_t* err;
+  uint64_t off1;  // first point brick
+  uint32_t epoch;
+  uint2* rinfo;     // per record: cell (brick * 8 + c) or ~0, rank in the cell
+  uint32_t* claim;  // claimed bricks
+  uint32_t* dense;  // dense cells
+  BuildState* st;
+  BuildState* st_next;
+  double4* pos;
+  double4* nrm;
 };
 
-__global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
-  const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
-  if (rec >= a.n) return;
-  const int t = rec < a.n0 ? 0 : 1;
-  const uint32_t r = t == 0 ? rec : rec - a.n0;
-  const Seg* segs = a.segs[t];
+// world position (and normal) of build-order record rec
+struct RecW {
+  double p[3], n[3];
+  uint32_t seg;
+  int t;
+};
+__device__ __forceinline__ RecW rec_world(const BuildArgs& a, uint32_t rec, bool with_nrm) {
+  RecW o;
+  o.t = rec < a.n0 ? 0 : 1;
+  const uint32_t r = o.t == 0 ? rec : rec - a.n0;
+  const Seg* segs = a.segs[o.t];
   const int s = find_seg(segs, a.K, r);
   const Seg sg = segs[s];
   const double* T = a.poses + 12 * s;
-  const float4 lp = a.pool_pos[t][sg.pool_off + (r - sg.off)];
-  double wp[3];
-  d_xform(T, (double)lp.x, (double)lp.y, (double)lp.z, wp);  // PlanarFeat::transform (features.hpp:137-140)
-  a.tpos[rec] = make_double4(wp[0], wp[1], wp[2], 0.0);
-  if (t == 0) {
+  const float4 lp = a.pool_pos[o.t][sg.pool_off + (r - sg.off)];
+  d_xform(T, (double)lp.x, (double)lp.y, (double)lp.z, o.p);  // PlanarFeat::transform (features.hpp:137-140)
+  if (with_nrm && o.t == 0) {
     const float4 ln = a.pool_nrm[sg.pool_off + (r - sg.off)];
-    double wn[3];
-    d_rot(T, (double)ln.x, (double)ln.y, (double)ln.z, wn);
-    a.tnrm[rec] = make_double4(wn[0], wn[1], wn[2], 0.0);
+    d_rot(T, (double)ln.x, (double)ln.y, (double)ln.z, o.n);
   }
-  a.rseg[rec] = (uint32_t)s;
-  const int cx = (int)floor(wp[0] / a.w), cy = (int)floor(wp[1] / a.w), cz = (int)floor(wp[2] / a.w);
-  if (!key_in_range(cx, cy, cz)) {
-    atomicOr(a.err, 1u);
-    a.rslot[rec] = 0xFFFFFFFFu;
-    return;
-  }
-  const unsigned long long key = brick_key(cx, cy, cz);
-  Brick* bricks = a.bricks + (t == 0 ? 0 : a.off1);
-  const uint64_t mask = a.mask[t];
-  uint64_t h = mix64(key) & mask;
-  for (;;) {  // the table has more buckets than records: an empty one always exists
-    const unsigned long long prev = atomicCAS(&bricks[h].key, 0ull, key);
-    if (prev == 0ull || prev == key) break;
-    h = (h + 1) & mask;
-  }
-  const uint32_t cell = (uint32_t)(((t == 0 ? 0 : a.off1) + h) * 8 + brick_cell(cx, cy, cz));
-  atomicAdd(a.bcnt + cell, 1u);
-  a.rslot[rec] = cell;
+  o.seg = (uint32_t)s;
+  return o;
 }
 
-// Brick layout: scanned over [brick][cell] (+ one zero entry past the end), the
-// prefix is cell (i / 8, i % 8)'s first record, the scatter cursor, and the previous
-// brick's end marker beg[8] at every brick boundary.
-struct BrickCountIn {
-  const uint32_t* c;
-  __device__ uint32_t operator()(size_t i) const { return c[i]; }
-};
-struct BrickFirstOut {
-  Brick* b;
-  uint32_t* cur;
-  __device__ void operator()(size_t i, uint32_t v) const {
-    cur[i] = v;
-    b[i >> 3].beg[i & 7] = v;
-    if ((i & 7) == 0 && i > 0) b[(i >> 3) - 1].beg[8] = v;
-  }
-};
-
-// After the scatter each slot's `first` has advanced by `count`: records of a voxel
-// are [first - count, first).  Planar slots precede point slots in the scan, so
-// planar records land in [0, n0) and nrm is written for them only.
-__global__ __launch_bounds__(256) void k_map_scatter(uint32_t n0, uint32_t nrec, const uint32_t* __restrict__ rslot,
-                                                     const uint32_t* __restrict__ rseg,
-                                                     const double4* __restrict__ tpos,
-                                                     const double4* __restrict__ tnrm,
-                                                     uint32_t* __restrict__ cursor,
-                                                     double4* __restrict__ pos, double4* __restrict__ nrm,
-                                                     uint32_t* __restrict__ seg, uint32_t* __restrict__ rid) {
+__global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
-  if (rec >= nrec) return;
-  const uint32_t s = rslot[rec];
-  if (s == 0xFFFFFFFFu) return;
-  const uint32_t o = atomicAdd(cursor + s, 1u);  // brick cell cursor
-  const double4 tp = tpos[rec];
-  const uint32_t sg = rseg[rec];
-  // .w: build order (k_match tie-break) in the low 32 bits, the segment above them
-  // (exact in a double: < 2^53), so the match epilogue needs no seg[] lookup
-  pos[o] = make_double4(tp.x, tp.y, tp.z, (double)rec + 4294967296.0 * (double)sg);
-  if (rec < n0) nrm[o] = tnrm[rec];
-  seg[o] = sg;
-  rid[o] = rec;
+  if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildState) / 4)  // the next build's state
+    reinterpret_cast<uint32_t*>(a.st_next)[threadIdx.x] = 0u;
+  if (rec >= a.n) return;
+  const RecW R = rec_world(a, rec, false);
+  const int cx = (int)floor(R.p[0] / a.w), cy = (int)floor(R.p[1] / a.w), cz = (int)floor(R.p[2] / a.w);
+  if (!key_in_range(cx, cy, cz)) {
+    atomicOr(&a.st->err, 1u);
+    a.rinfo[rec] = make_uint2(0xFFFFFFFFu, 0u);
+    return;
+  }
+  const unsigned long long key = brick_key(cx, cy, cz, a.epoch);
+  const uint64_t boff = R.t == 0 ? 0 : a.off1;
+  Brick* bricks = a.bricks + boff;
+  const uint64_t mask = a.mask[R.t];
+  uint64_t h = mix64(key) & mask;
+  for (;;) {  // more buckets than records: a bucket of another epoch always exists
+    const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) break;
+    if (key_epoch(cur) != a.epoch) {  // empty for this build: claim it
+      const unsigned long long prev = atomicCAS(&bricks[h].key, cur, key);
+      if (prev == cur) {
+        a.claim[atomicAdd(&a.st->nclaim, 1u)] = (uint32_t)(boff + h);
+        break;
+      }
+      if (prev == key) break;
+      if (key_epoch(prev) != a.epoch) continue;  // (not reached: only this epoch's keys are written)
+    }
+    h = (h + 1) & mask;
+  }
+  const uint32_t cell = (uint32_t)((boff + h) * 8 + brick_cell(cx, cy, cz));
+  a.rinfo[rec] = make_uint2(cell, atomicAdd(a.bcnt + cell, 1u));
+}
+
+// One lane per claimed brick: record ranges of its 8 cells, allocated per type from the
+// state's cursors (one atomic per wave); dense cells reserve kHdr header slots and are
+// listed for k_map_dense.  The grid is sized for the worst case (every record claiming a
+// brick); lanes past nclaim only take part in the wave scans.
+__global__ __launch_bounds__(256) void k_map_alloc(BuildArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ncl = __hip_atomic_load(&a.st->nclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x * blockDim.x >= ncl) return;  // whole block past the list
+  const bool valid = i < ncl;
+  const uint32_t gb = valid ? a.claim[i] : 0u;
+  const int t = gb >= a.off1 ? 1 : 0;
+  uint32_t sz[8], tot = 0, dmask = 0;
+  if (valid) {
+    uint4* cp = reinterpret_cast<uint4*>(a.bcnt + (size_t)gb * 8);
+    const uint4 c0 = cp[0], c1 = cp[1];
+    cp[0] = make_uint4(0, 0, 0, 0);  // zero between builds
+    cp[1] = make_uint4(0, 0, 0, 0);
+    const uint32_t c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool d = c[k] > (uint32_t)kDenseMin;
+      dmask |= (d ? 1u : 0u) << k;
+      sz[k] = c[k] + (d ? kHdr : 0);
+      tot += sz[k];
+    }
+  }
+  uint32_t base = 0;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const uint32_t v = valid && t == tt ? tot : 0u;
+    const uint32_t incl = wave_incl_scan(v);
+    uint32_t wb = 0;
+    if (lane_id() == 63 && incl) wb = atomicAdd(&a.st->cur[tt], incl);
+    wb = __shfl(wb, 63, 64);
+    if (t == tt) base = wb + incl - v + (tt == 1 ? a.pt_base : 0u);
+  }
+  if (!valid) return;
+  Brick& B = a.bricks[gb];
+  uint32_t run = base;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    B.beg[k] = run;
+    run += sz[k];
+  }
+  B.beg[8] = run;
+  B.dense = dmask;
+  if (dmask) {
+    const uint32_t o = atomicAdd(&a.st->ndense, (uint32_t)__popc(dmask));
+    uint32_t j = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if ((dmask >> k) & 1) a.dense[o + j++] = gb * 8 + k;
+  }
+}
+
+// .w of a record: build order (k_match tie-break) in the low 32 bits, the segment above
+// them (exact in a double: < 2^53), so the match epilogue needs no seg[] lookup
+__device__ __forceinline__ double rec_tag(uint32_t rec, uint32_t seg) {
+  return (double)rec + 4294967296.0 * (double)seg;
+}
+
+__global__ __launch_bounds__(256) void k_map_scatter(BuildArgs a) {
+  const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rec >= a.n) return;
+  const uint2 ri = a.rinfo[rec];
+  if (ri.x == 0xFFFFFFFFu) return;
+  const Brick& B = a.bricks[ri.x >> 3];
+  const uint32_t c = ri.x & 7;
+  const uint32_t o = B.beg[c] + (((B.dense >> c) & 1) ? kHdr : 0) + ri.y;
+  const RecW R = rec_world(a, rec, true);
+  a.pos[o] = make_double4(R.p[0], R.p[1], R.p[2], rec_tag(rec, R.seg));
+  if (R.t == 0) a.nrm[o] = make_double4(R.n[0], R.n[1], R.n[2], 0.0);
+}
+
+// sub-cell of a position inside cell origin o (per axis), width sw = w / 4
+__device__ __forceinline__ int sub_axis(double p, double o, double sw) {
+  const int i = (int)floor((p - o) / sw);
+  return i < 0 ? 0 : (i > kSubPerAxis - 1 ? kSubPerAxis - 1 : i);
+}
+
+// One block per dense cell: records (in registers) counting-sorted by sub-cell in
+// place; the header's 64 u32 are the sub-cells' end offsets relative to the first
+// record after the header.  Cells over kDenseThreads * kDenseRecs records stay
+// unsorted (header[0] = kUnsorted: k_match scans them whole).
+__device__ void dense_sort_cell(const BuildArgs& a, uint32_t cell, uint32_t* s_cnt, uint32_t* s_off) {
+  const Brick& B = a.bricks[cell >> 3];
+  const uint32_t c = cell & 7;
+  const uint32_t beg = B.beg[c], n = B.beg[c + 1] - beg - kHdr, first = beg + kHdr;
+  const bool planar = (cell >> 3) < a.off1;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(a.pos + beg);
+  const int tid = threadIdx.x;
+  if (n > (uint32_t)(kDenseThreads * kDenseRecs)) {
+    if (tid == 0) hdr[0] = kUnsorted;
+    return;
+  }
+  if (tid < kSubCells) s_cnt[tid] = 0;
+  // the cell's origin from any of its records (all of them map to this cell)
+  const double4 p0 = a.pos[first];
+  const double ox = floor(p0.x / a.w) * a.w, oy = floor(p0.y / a.w) * a.w, oz = floor(p0.z / a.w) * a.w;
+  const double sw = a.w / kSubPerAxis;
+  __syncthreads();
+  double4 rp[kDenseRecs], rn[kDenseRecs];
+  uint32_t rs[kDenseRecs];
+#pragma unroll
+  for (int u = 0; u < kDenseRecs; ++u) {
+    const uint32_t i = (uint32_t)(u * kDenseThreads + tid);
+    if (i < n) {
+      rp[u] = a.pos[first + i];
+      if (planar) rn[u] = a.nrm[first + i];
+      const uint32_t sub = (uint32_t)(sub_axis(rp[u].x, ox, sw) + kSubPerAxis * sub_axis(rp[u].y, oy, sw) +
+                                      kSubPerAxis * kSubPerAxis * sub_axis(rp[u].z, oz, sw));
+      rs[u] = sub | (atomicAdd(&s_cnt[sub], 1u) << 8);
+    }
+  }
+  __syncthreads();
+  if (tid < kWave) {  // exclusive scan of the 64 counts by wave 0
+    const uint32_t v = s_cnt[tid];
+    const uint32_t incl = wave_incl_scan(v);
+    s_off[tid] = incl - v;
+    hdr[tid] = incl;  // sub-cell end
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kDenseRecs; ++u) {
+    const uint32_t i = (uint32_t)(u * kDenseThreads + tid);
+    if (i < n) {
+      const uint32_t o = first + s_off[rs[u] & 0xFF] + (rs[u] >> 8);
+      a.pos[o] = rp[u];
+      if (planar) a.nrm[o] = rn[u];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kDenseThreads) void k_map_dense(BuildArgs a) {
+  const uint32_t nd = __hip_atomic_load(&a.st->ndense, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __shared__ uint32_t s_cnt[kSubCells];
+  __shared__ uint32_t s_off[kSubCells];
+  for (uint32_t di = blockIdx.x; di < nd; di += gridDim.x) {
+    dense_sort_cell(a, a.dense[di], s_cnt, s_off);
+    __syncthreads();
+  }
 }
 
 struct MapView {
@@ -160,8 +318,7 @@ struct MapView {
   uint64_t mask;
   const double4* pos;
   const double4* nrm;
-  const uint32_t* seg;
-  const uint32_t* rid;
+  uint32_t epoch;
 };
 
 // Cell shifts searched around the query's cell: [0] own cell, [1,7) the 6 face
@@ -187,6 +344,12 @@ __device__ __constant__ int c_shift[125][3] = {
     {1, -2, -2}, {1, -2, 2}, {1, 2, -2}, {1, 2, 2}, {2, -2, -1}, {2, -2, 1}, {2, -1, -2},
     {2, -1, 2}, {2, 1, -2}, {2, 1, 2}, {2, 2, -1}, {2, 2, 1}, {-2, -2, -2}, {-2, -2, 2},
     {-2, 2, -2}, {-2, 2, 2}, {2, -2, -2}, {2, -2, 2}, {2, 2, -2}, {2, 2, 2},
+};
+
+// rank of each reference voxel shift (dx, dy, dz) in {-1, 0, 1}^3 in the reference's
+// order (map.tpp:54-68), indexed (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)
+__device__ __constant__ uint8_t c_refrank[27] = {
+    26, 10, 25, 14, 2, 13, 24, 9, 23, 18, 4, 17, 6, 0, 5, 16, 3, 15, 22, 8, 21, 12, 1, 11, 20, 7, 19,
 };
 
 struct MatchArgs {
@@ -222,6 +385,7 @@ constexpr int kSmallCell = FMX_SMALL_CELL;  // neighbour cells with at most this
 constexpr int kTileBlocks = 1024 / kQPB;
 constexpr int kTileQ = kTileBlocks * kQPB;  // 1024
 constexpr int kTileMaxPairs = 256;          // LDS bound of the tiled path (wider windows: per-block path)
+constexpr int kWorkWords = 8;               // per-block match work / diagnostic words
 
 // Outputs of the tiled pair sort's last-block pass (consumed by later launches).
 struct SortOut {
@@ -346,9 +510,11 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
   const MapView& M = planar ? mp : mt;
   __shared__ uint32_t s_ins;
+  __shared__ uint32_t s_hdr[kQPB][kSubCells];  // dense-cell headers, one per query
   for (int k = threadIdx.x; k < a.K; k += kMatchThreads) s_hist[k] = 0;
   if (threadIdx.x == 0) s_ins = 0;
   __syncthreads();
+  const uint32_t t_begin = (uint32_t)wall_clock64();
   uint32_t n_probe = 0, n_cand = 0;
   if (qi < nq) {
     const float4 lq = planar ? q_pl[qi] : q_pt[qi];
@@ -359,56 +525,69 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     const double lo[3] = {wq[0] - bx * a.w, wq[1] - by * a.w, wq[2] - bz * a.w};
     const double hi[3] = {(bx + 1) * a.w - wq[0], (by + 1) * a.w - wq[1], (bz + 1) * a.w - wq[2]};
     double best = a.bound;
+    // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
+    // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
+    // the record's build order (= insertion order inside a voxel, map.tpp:41-52)
     uint32_t best_rid = 0xFFFFFFFFu, best_i = 0xFFFFFFFFu;
-    // one bucket read per probe: key and the cell's two boundaries in flight together
-    auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count) {
+    const int sh = a.rings >= 2 ? 1 : 0;  // cells of w/2: reference voxel = cell >> 1
+    auto srank = [&](int sx, int sy, int sz) -> uint32_t {
+      const int dx = ((bx + sx) >> sh) - (bx >> sh), dy = ((by + sy) >> sh) - (by >> sh),
+                dz = ((bz + sz) >> sh) - (bz >> sh);
+      return (uint32_t)c_refrank[(dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)] << 27;
+    };
+    // one bucket read per probe: key, the cell's two boundaries and its dense bit in
+    // flight together; a bucket of another build epoch ends the chain (empty)
+    auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count, bool& dense) {
       const int X = bx + sx, Y = by + sy, Z = bz + sz;
-      const unsigned long long key = brick_key(X, Y, Z);
+      const unsigned long long key = brick_key(X, Y, Z, M.epoch);
       const uint32_t ci = brick_cell(X, Y, Z);
       uint64_t h = mix64(key) & M.mask;
       first = 0;
       count = 0;
+      dense = false;
       for (;;) {
         ++n_probe;
         const Brick* b = M.bricks + h;
         const unsigned long long k = b->key;
-        const uint32_t b0 = b->beg[ci], b1 = b->beg[ci + 1];
+        const uint32_t b0 = b->beg[ci], b1 = b->beg[ci + 1], dm = b->dense;
         if (k == key) {
           first = b0;
           count = b1 - b0;
+          dense = (dm >> ci) & 1;
           return;
         }
-        if (k == 0ull) return;
+        if (key_epoch(k) != M.epoch) return;
         h = (h + 1) & M.mask;
       }
     };
     // a record is one double4: world position + its build order in .w (exact in a
     // double), so a candidate test is one 32-B load
-    auto fold = [&](const double4& p, uint32_t i) {
+    auto fold = [&](const double4& p, uint32_t i, uint32_t rk) {
       const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
       const double d2 = (dx * dx + dz * dz) + dy * dy;
-      const uint32_t rid = (uint32_t)(unsigned long long)p.w;  // build order: the low 32 bits
-      if (d2 <= best && (d2 < best || rid < best_rid)) {
+      const uint32_t tk = rk | ((uint32_t)(unsigned long long)p.w & 0x07FFFFFFu);  // build order: low bits
+      if (d2 <= best && (d2 < best || tk < best_rid)) {
         best = d2;
-        best_rid = rid;
+        best_rid = tk;
         best_i = i;
       }
     };
     // this lane's share (first + g, step kGroup) of records [first, first + count):
-    // four loads in flight per round, folded in record order (the same argmin)
-    auto scan_range = [&](uint32_t first, uint32_t count) {
+    // four loads in flight per round
+    auto scan_range = [&](uint32_t first, uint32_t count, uint32_t rk) {
       const uint32_t end = first + count;
+      n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
       uint32_t i = first + g;
       for (; i + 3 * kGroup < end; i += 4 * kGroup) {
         const double4 p0 = M.pos[i], p1 = M.pos[i + kGroup], p2 = M.pos[i + 2 * kGroup], p3 = M.pos[i + 3 * kGroup];
-        fold(p0, i);
-        fold(p1, i + kGroup);
-        fold(p2, i + 2 * kGroup);
-        fold(p3, i + 3 * kGroup);
+        fold(p0, i, rk);
+        fold(p1, i + kGroup, rk);
+        fold(p2, i + 2 * kGroup, rk);
+        fold(p3, i + 3 * kGroup, rk);
       }
-      for (; i < end; i += kGroup) fold(M.pos[i], i);
+      for (; i < end; i += kGroup) fold(M.pos[i], i, rk);
     };
-    // argmin over (d^2, build order) across the group's lanes with DPP moves (VALU
+    // argmin over (d^2, tie key) across the group's lanes with DPP moves (VALU
     // latency, no LDS crossbar): [row_mirror l <-> 15-l,] row_half_mirror l <-> 7-l,
     // quad xor 2, quad xor 1 leave every lane with the group minimum
     auto group_min = [&]() {
@@ -432,6 +611,74 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
       step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
     };
+    // Records of one cell, walked by the whole group (group-uniform arguments).  A
+    // dense cell (k_map_dense) starts with a header of its 64 sub-cell ends: the
+    // query's own sub-cell first, then every other sub-cell whose box lower bound does
+    // not exceed the best so far, each group-walked (lane g holds sub-cells 8g..8g+7's
+    // ends; with kGroup < 8 a lane holds several such blocks).
+    const double sw = a.w / kSubPerAxis;
+    uint32_t* hd = s_hdr[threadIdx.x / kGroup];  // this query's copy of a dense cell's header
+    auto scan_cell = [&](uint32_t first, uint32_t count, bool dense, int X, int Y, int Z, uint32_t rk) {
+      constexpr int kPer = kSubCells / kGroup;  // sub-cells per lane
+      const uint32_t* hdr = reinterpret_cast<const uint32_t*>(M.pos + first);
+      const uint32_t base = dense ? first + kHdr : first;
+      const bool sorted = dense && hdr[0] != kUnsorted;
+      // per sub-cell lower bound (1e-9 slack over the fp rounding of the sub-cell index)
+      auto axis_lb = [&](double q, int C, int i) {
+        const double lo = C * a.w + i * sw, hi = lo + sw;
+        const double d = q < lo ? lo - q : (q > hi ? q - hi : 0.0);
+        const double m = fmax(d - 1e-9, 0.0);
+        return m * m;
+      };
+      auto sub_lb = [&](int sub) {
+        return axis_lb(wq[0], X, sub % kSubPerAxis) + axis_lb(wq[1], Y, (sub / kSubPerAxis) % kSubPerAxis) +
+               axis_lb(wq[2], Z, sub / (kSubPerAxis * kSubPerAxis));
+      };
+      auto sub_beg = [&](int sub) { return sub == 0 ? 0u : hd[sub - 1]; };
+      uint32_t live = 0;
+      if (sorted) {  // header -> LDS (the group's lanes, kPer ends each), then live sub-cells
+        // (s_waitcnt + memory clobber: the other lanes' header entries are read below,
+        // and the previous header's reads must not move past these stores)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < kPer; u += 4)
+          *reinterpret_cast<uint4*>(hd + g * kPer + u) = *reinterpret_cast<const uint4*>(hdr + g * kPer + u);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#pragma unroll 1
+        for (int u = 0; u < kPer; ++u) {
+          const int sub = g * kPer + u;
+          if (hd[sub] > sub_beg(sub) && sub_lb(sub) <= best) live |= 1u << u;
+        }
+      }
+      const int gsh = (lane_id() / kGroup) * kGroup;
+      // the ranges walked: the whole cell (not sorted), else the query's own (nearest)
+      // sub-cell first, then every live sub-cell, its bound re-checked against best
+      for (int step = 0;; ++step) {
+        uint32_t rs = base, re = first + count;
+        if (sorted) {
+          int sub;
+          if (step == 0) {
+            sub = sub_axis(wq[0], X * a.w, sw) + kSubPerAxis * sub_axis(wq[1], Y * a.w, sw) +
+                  kSubPerAxis * kSubPerAxis * sub_axis(wq[2], Z * a.w, sw);
+            if (g == sub / kPer) live &= ~(1u << (sub % kPer));
+          } else {
+            const uint64_t any = (__ballot(live != 0) >> gsh) & ((1ull << kGroup) - 1);
+            if (!any) break;
+            const int l = __ffsll((unsigned long long)any) - 1;
+            sub = l * kPer + __shfl(live ? __ffs(live) - 1 : 0, l, kGroup);
+            if (g == l) live &= live - 1;
+          }
+          const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
+          if (e0 == s0 || sub_lb(sub) > best) continue;
+          rs = base + s0;
+          re = base + e0;
+        } else if (step > 0) {
+          break;
+        }
+        scan_range(rs, re - rs, rk);
+        group_min();
+      }
+    };
     const bool inr = key_in_range(bx, by, bz);
     // lower bound on d^2 from the query to any point of the cell at shift s
     auto shift_lb = [&](int s) {
@@ -445,47 +692,42 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       }
       return lb;
     };
-    // phase 1: the query's own voxel (shift 0, visited first by the reference too),
-    // its records split over the group's lanes
-    if (inr) {
-      uint32_t first = 0, count = 0;
-      if (g == 0) probe(0, 0, 0, first, count);
-      first = __shfl(first, 0, kGroup);
-      count = __shfl(count, 0, kGroup);
-      n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
-      scan_range(first, count);
-    }
-    group_min();  // every lane now holds the own-voxel best: the bound for phase 2
-    // phase 2: the neighbour cells in passes of increasing lower bound — ring-1 faces
-    // (shifts 1..6), ring-1 edges + corners (7..26), then ring 2 (27..124) when the
-    // map uses half-width cells — each pass pruned against the best found so far.  In
-    // a pass a lane bounds and probes its shifts in parallel, then the group walks
-    // every surviving cell together (records split over the lanes), re-checking each
-    // bound against the shared best.
-    auto pass = [&](int s_begin, int s_end) {
+    // The cells in passes of increasing lower bound — the query's own cell (shift 0,
+    // visited first by the reference too), ring-1 faces (shifts 1..6), ring-1 edges +
+    // corners (7..26), then ring 2 (27..124) when the map uses half-width cells — each
+    // pass pruned against the best found so far.  In a pass a lane bounds and probes
+    // its shifts in parallel, then the group walks every surviving cell together
+    // (records split over the lanes), re-checking each bound against the shared best.
+    // One loop over the passes, so the cell walk is emitted once.
+    const int npass = a.rings >= 2 ? 4 : 3;
+    for (int ip = 0; ip < npass; ++ip) {
+      const int s_begin = ip == 0 ? 0 : (ip == 1 ? 1 : (ip == 2 ? 7 : 27));
+      const int s_end = ip == 0 ? 1 : (ip == 1 ? 7 : (ip == 2 ? 27 : 125));
       for (int s0 = s_begin; s0 < s_end; s0 += kGroup) {  // one shift per lane per chunk
         uint32_t vf = 0, vc = 0;
+        bool vd = false;
         double vlb = INFINITY;
         const int s = s0 + g;
         if (inr && s < s_end) {
           const double lb = shift_lb(s);
           if (lb <= best) {  // else conservative: no point inside can win
-            probe(c_shift[s][0], c_shift[s][1], c_shift[s][2], vf, vc);
+            probe(c_shift[s][0], c_shift[s][1], c_shift[s][2], vf, vc, vd);
             vlb = lb;
           }
         }
         // small cells (<= kSmallCell records): the lane that probed one folds its
         // records itself, every lane's loads in flight together, one group min after;
-        // the argmin on (d^2, build order) does not depend on the folding order
+        // the argmin on (d^2, tie key) does not depend on the folding order
         const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
         if (small) {
+          const uint32_t rk = srank(c_shift[s][0], c_shift[s][1], c_shift[s][2]);
           double4 pr[kSmallCell];
 #pragma unroll
           for (int u = 0; u < kSmallCell; ++u)
             if (u < (int)vc) pr[u] = M.pos[vf + u];
 #pragma unroll
           for (int u = 0; u < kSmallCell; ++u)
-            if (u < (int)vc) fold(pr[u], vf + u);
+            if (u < (int)vc) fold(pr[u], vf + u, rk);
           n_cand += vc;
         }
         const int gsh = (lane_id() / kGroup) * kGroup;
@@ -499,15 +741,13 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
           if (lb > best) continue;  // best is group-uniform here
           const uint32_t cnt = __shfl(vc, l, kGroup);
           const uint32_t first = __shfl(vf, l, kGroup);
-          n_cand += cnt / kGroup + (g < (int)(cnt % kGroup) ? 1 : 0);
-          scan_range(first, cnt);
-          group_min();
+          const bool dn = __shfl((int)vd, l, kGroup) != 0;
+          const int sl = s0 + l;
+          scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2],
+                    srank(c_shift[sl][0], c_shift[sl][1], c_shift[sl][2]));
         }
       }
-    };
-    pass(1, 7);
-    pass(7, 27);
-    if (a.rings >= 2) pass(27, 125);
+    }
     if (g == 0) {
       const bool found = best_i != 0xFFFFFFFFu;
       int32_t pair = -1;
@@ -537,23 +777,32 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
     }
   }
-  // work counters (probes, candidate records) for the algorithmic-byte model: one
-  // plain store per block (no same-address atomics), summed on the host
-  __shared__ uint32_t s_work[2][kMatchThreads / kWave];
+  // work counters for the algorithmic-byte model and the match diagnostics (one plain
+  // store per block, summed on the host): probes, candidate records, the largest
+  // per-query candidate count of the block, block start / end (100 MHz wall clock)
+  __shared__ uint32_t s_work[3][kMatchThreads / kWave];
+  uint32_t qc = n_cand;  // this query's candidates: sum over its group
+#pragma unroll
+  for (int o = 1; o < kGroup; o <<= 1) qc += __shfl_xor(qc, o, 64);
+#pragma unroll
+  for (int o = kGroup; o < kWave; o <<= 1) qc = max(qc, (uint32_t)__shfl_xor(qc, o, 64));
   const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
   if (lane_id() == 0) {
     s_work[0][threadIdx.x / kWave] = wp;
     s_work[1][threadIdx.x / kWave] = wc;
+    s_work[2][threadIdx.x / kWave] = qc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t tp = 0, tc = 0;
+    uint32_t tp = 0, tc = 0, mq = 0;
     for (int i = 0; i < kMatchThreads / kWave; ++i) {
       tp += s_work[0][i];
       tc += s_work[1][i];
+      mq = max(mq, s_work[2][i]);
     }
-    work[2 * blockIdx.x] = tp;
-    work[2 * blockIdx.x + 1] = tc;
+    uint4* w4 = reinterpret_cast<uint4*>(work) + 2 * blockIdx.x;
+    w4[0] = make_uint4(tp, tc, mq, 0u);
+    w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), 0u, 0u);
   }
   if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
     __hip_atomic_store(ins_blk + blockIdx.x, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -926,68 +1175,81 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   c->map_poses_p = c->map_blob.p;
   c->map_inv_p = c->map_blob.p + 12 * (size_t)Kc;
   const Seg* dseg = reinterpret_cast<const Seg*>(c->map_blob.p + 24 * (size_t)Kc);
-  // fused build of both types: one table allocation (planar slots, point slots, then
-  // the range-error word in one extra slot), one record numbering, one launch each
-  // for zeroing, insert, count scan and scatter
+  // fused build of both types: one brick table (planar bricks, then point bricks),
+  // one record numbering, four launches (k_map_insert / alloc / scatter / dense)
   VoxMap& M = c->map;
   const uint32_t n = nrec[0] + nrec[1];
-  // bricks: more buckets than records, so an empty bucket always ends a probe (a
-  // brick holds >= 1 record; real scans fill a few percent of the buckets)
+  if (n >= (1u << 27)) throw StatusError(FMX_E_SIZE, "voxel map: more than 2^27 records (k_match tie key)");
+  // bricks: more buckets than records, so a bucket of another epoch always ends a probe
+  // (a brick holds >= 1 record; real scans fill a few percent of the buckets)
   for (int t = 0; t < 2; ++t) {
     M.n[t] = nrec[t];
     M.cap[t] = next_pow2(std::max<uint64_t>((uint64_t)nrec[t] + 1, 256));
   }
   const uint64_t slots = M.cap[0] + M.cap[1];  // buckets
-  M.table.ensure(4 * (slots + 1));
-  Brick* bricks = reinterpret_cast<Brick*>(M.table.p);
-  c->map_err_p = &bricks[slots].pad[0];
-  FMX_HIP(hipMemsetAsync(M.table.p, 0, (slots + 1) * sizeof(Brick), st));
-  M.bcnt.ensure(8 * slots + 1);
-  M.bcur.ensure(8 * slots + 1);
-  FMX_HIP(hipMemsetAsync(M.bcnt.p, 0, (8 * slots + 1) * sizeof(uint32_t), st));
-  const double table_bytes = 64.0 * (double)slots;
-  M.tpos.ensure(n + 1);
-  M.tnrm.ensure(nrec[0] + 1);
-  M.rslot.ensure(n + 1);
-  M.rseg.ensure(n + 1);
-  M.pos.ensure(n + 1);
-  M.nrm.ensure(nrec[0] + 1);
-  M.seg.ensure(n + 1);
-  M.rid.ensure(n + 1);
-  const double bytes = 2.0 * 32.0 * nrec[0] + 2.0 * 16.0 * nrec[1] + table_bytes;
+  const bool grown = 4 * slots > M.table.cap || 8 * slots > M.bcnt.cap || M.state.cap < 4;
+  M.table.ensure(4 * slots);
+  M.bcnt.ensure(8 * slots);
+  M.state.ensure(4);  // two BuildState of 32 B
+  if (grown || M.epoch >= kEpochMax) {  // fresh storage or epoch wrap: clear everything once
+    FMX_HIP(hipMemsetAsync(M.table.p, 0, M.table.cap * sizeof(uint4), st));
+    FMX_HIP(hipMemsetAsync(M.bcnt.p, 0, M.bcnt.cap * sizeof(uint32_t), st));
+    FMX_HIP(hipMemsetAsync(M.state.p, 0, M.state.cap * sizeof(uint4), st));
+    M.epoch = 0;
+  }
+  M.epoch += 1;
+  BuildState* bst = reinterpret_cast<BuildState*>(M.state.p);
+  c->map_err_p = &bst[M.epoch & 1].err;
+  M.rinfo.ensure(n + 1);
+  M.claim.ensure(n + 1);
+  M.dense.ensure(n / kDenseMin + 1);
+  // planar slots [0, pt_base): records + the header slots of at most n0 / (kDenseMin + 1)
+  // dense cells; point slots from pt_base
+  const uint32_t pt_base = nrec[0] + nrec[0] / (kDenseMin + 1) * kHdr;
+  M.pos.ensure((size_t)pt_base + nrec[1] + nrec[1] / (kDenseMin + 1) * kHdr + 1);
+  M.nrm.ensure((size_t)pt_base + 1);
+  // algorithmic bytes: read local records (16 B pos + 16 B planar normal, twice: insert
+  // and scatter recompute the transform) + write world records (32 B + 32 B planar) + the
+  // 64-B brick of each record's cell (claim + count, then its range) + rank word
+  const double bytes = 2.0 * (32.0 * nrec[0] + 16.0 * nrec[1]) + 2.0 * 32.0 * nrec[0] + 32.0 * nrec[1] +
+                       2.0 * 64.0 * n / 8.0 + 16.0 * n;
   ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
   HostScope* hs_l = new HostScope(7);
+  BuildArgs ba;
+  ba.pool_pos[0] = c->pool[0].pos.p;
+  ba.pool_pos[1] = c->pool[1].pos.p;
+  ba.pool_nrm = c->pool[0].nrm.p;
+  ba.segs[0] = dseg;
+  ba.segs[1] = dseg + Kc;
+  ba.K = K;
+  ba.poses = c->map_poses_p;
+  ba.n0 = nrec[0];
+  ba.n = n;
+  ba.pt_base = pt_base;
+  ba.w = c->cell_w;
+  ba.bricks = reinterpret_cast<Brick*>(M.table.p);
+  ba.bcnt = M.bcnt.p;
+  ba.mask[0] = M.cap[0] - 1;
+  ba.mask[1] = M.cap[1] - 1;
+  ba.off1 = M.cap[0];
+  ba.epoch = M.epoch;
+  ba.rinfo = M.rinfo.p;
+  ba.claim = M.claim.p;
+  ba.dense = M.dense.p;
+  ba.st = bst + (M.epoch & 1);
+  ba.st_next = bst + ((M.epoch + 1) & 1);
+  ba.pos = M.pos.p;
+  ba.nrm = M.nrm.p;
+  const uint32_t nb = std::max<uint32_t>((n + 255) / 256, 1);  // >= 1: block 0 clears the next state
+  hipLaunchKernelGGL(k_map_insert, dim3(nb), dim3(256), 0, st, ba);
+  FMX_HIP(hipGetLastError());
   if (n > 0) {
-    BuildArgs ba;
-    ba.pool_pos[0] = c->pool[0].pos.p;
-    ba.pool_pos[1] = c->pool[1].pos.p;
-    ba.pool_nrm = c->pool[0].nrm.p;
-    ba.segs[0] = dseg;
-    ba.segs[1] = dseg + Kc;
-    ba.K = K;
-    ba.poses = c->map_poses_p;
-    ba.n0 = nrec[0];
-    ba.n = n;
-    ba.w = c->cell_w;
-    ba.bricks = reinterpret_cast<Brick*>(M.table.p);
-    ba.bcnt = M.bcnt.p;
-    ba.mask[0] = M.cap[0] - 1;
-    ba.mask[1] = M.cap[1] - 1;
-    ba.off1 = M.cap[0];
-    ba.tpos = M.tpos.p;
-    ba.tnrm = M.tnrm.p;
-    ba.rslot = M.rslot.p;
-    ba.rseg = M.rseg.p;
-    ba.err = c->map_err_p;
-    hipLaunchKernelGGL(k_map_insert, dim3((n + 255) / 256), dim3(256), 0, st, ba);
+    hipLaunchKernelGGL(k_map_alloc, dim3(nb), dim3(256), 0, st, ba);
     FMX_HIP(hipGetLastError());
-    c->dev_u32.ensure(8);
-    c->scan_scratch.ensure(scan_scratch_size(8 * slots + 1) + 4);
-    exclusive_scan(BrickCountIn{M.bcnt.p}, BrickFirstOut{reinterpret_cast<Brick*>(M.table.p), M.bcur.p}, 8 * slots + 1,
-                   c->scan_scratch.p, c->dev_u32.p + 4, st);
-    hipLaunchKernelGGL(k_map_scatter, dim3((n + 255) / 256), dim3(256), 0, st, nrec[0], n, M.rslot.p, M.rseg.p,
-                       M.tpos.p, M.tnrm.p, M.bcur.p, M.pos.p, M.nrm.p, M.seg.p,
-                       M.rid.p);
+    hipLaunchKernelGGL(k_map_scatter, dim3(nb), dim3(256), 0, st, ba);
+    FMX_HIP(hipGetLastError());
+    const uint32_t nbd = std::min<uint32_t>(n / (kDenseMin + 1) + 1, kDenseGrid);
+    hipLaunchKernelGGL(k_map_dense, dim3(nbd), dim3(kDenseThreads), 0, st, ba);
     FMX_HIP(hipGetLastError());
   }
   delete hs_l;
@@ -1064,7 +1326,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->ld_pt = c->n_qpt + 1;
   c->c_pl.ensure(9 * c->ld_pl);
   c->c_pt.ensure(6 * c->ld_pt);
-  c->work.ensure(2 * (size_t)nb + 2);
+  c->work.ensure(kWorkWords * (size_t)nb + 8);
   c->work_blocks = nb;
   ensure_zeroed(c->mcnt, 2 * (size_t)K, st);
   ensure_zeroed(c->mticket, 1, st);
@@ -1077,7 +1339,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   auto view = [&](int t) {  // type t's table section over the shared record arrays
     VoxMap& M = c->map;
     return MapView{reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
-                   M.pos.p, M.nrm.p, M.seg.p, M.rid.p};
+                   M.pos.p, M.nrm.p, M.epoch};
   };
   // Algorithmic bytes of a match launch: query read (16 B) +
   // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + 16 B per hash probe +
@@ -1124,8 +1386,9 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   }
   // per-pair counts reach pinned host memory from k_pair_base; consumed at the next sync
   if (c->prof.on) {  // per-block work counters, only needed for the profile's byte model
-    c->h_work.ensure(2 * (size_t)nb + 2);
-    if (nb) FMX_HIP(hipMemcpyAsync(c->h_work.p, c->work.p, 2 * (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    c->h_work.ensure(kWorkWords * (size_t)nb + 8);
+    if (nb)
+      FMX_HIP(hipMemcpyAsync(c->h_work.p, c->work.p, kWorkWords * (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   }
   c->counts_pending = true;
   c->have_match = true;
@@ -1151,9 +1414,10 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
   if (c->prof.on) {
     double tp = 0, tc = 0;
     for (uint32_t b = 0; b < c->work_blocks; ++b) {
-      tp += c->h_work.p[2 * b];
-      tc += c->h_work.p[2 * b + 1];
+      tp += c->h_work.p[kWorkWords * b];
+      tc += c->h_work.p[kWorkWords * b + 1];
     }
+    match_diag_add(c->h_work.p, c->work_blocks);
     c->last_probes = tp;
     c->last_cands = tc;
   }
