@@ -35,7 +35,17 @@
 #define FMX_VM_NS g8
 #endif
 #ifndef FMX_DENSE_MIN
-#define FMX_DENSE_MIN 64
+#define FMX_DENSE_MIN 128
+#endif
+#ifndef FMX_SUB_AXIS
+#define FMX_SUB_AXIS 4
+#endif
+#ifndef FMX_MATCH_WAVES
+#define FMX_MATCH_WAVES 4  // waves per SIMD k_match is compiled for (register budget 128)
+#endif
+#define FMX_MATCH_ATTR __attribute__((amdgpu_waves_per_eu(FMX_MATCH_WAVES, 8)))
+#ifndef FMX_MATCH_DEPTH
+#define FMX_MATCH_DEPTH 4
 #endif
 
 namespace fmx {
@@ -80,9 +90,9 @@ struct BuildState {  // per build, two alternating copies (the other is cleared)
   uint32_t pad[3];
 };
 constexpr int kDenseMin = FMX_DENSE_MIN;  // records that make a cell dense
-constexpr int kSubPerAxis = 4;            // dense cells: 4 x 4 x 4 sub-cells of w / 4
+constexpr int kSubPerAxis = FMX_SUB_AXIS;  // dense cells: 4 x 4 x 4 sub-cells of w / 4
 constexpr int kSubCells = kSubPerAxis * kSubPerAxis * kSubPerAxis;
-constexpr int kHdr = kSubCells * 4 / 32;  // header slots (double4) holding the 64 u32 sub-cell ends
+constexpr int kHdr = (kSubCells * 4 + 31) / 32;  // header slots (double4) holding the u32 sub-cell ends
 constexpr int kDenseThreads = 1024;
 constexpr int kDenseRecs = 8;             // records per thread: dense cells up to 8192 records are sorted
 constexpr uint32_t kUnsorted = 0xFFFFFFFFu;  // header[0] of a dense cell too large to sort
@@ -285,11 +295,14 @@ __device__ void dense_sort_cell(const BuildArgs& a, uint32_t cell, uint32_t* s_c
     }
   }
   __syncthreads();
-  if (tid < kWave) {  // exclusive scan of the 64 counts by wave 0
-    const uint32_t v = s_cnt[tid];
+  static_assert(kSubCells <= kWave, "one wave scans the sub-cell counts");
+  if (tid < kWave) {  // exclusive scan of the sub-cell counts by wave 0
+    const uint32_t v = tid < kSubCells ? s_cnt[tid] : 0u;
     const uint32_t incl = wave_incl_scan(v);
-    s_off[tid] = incl - v;
-    hdr[tid] = incl;  // sub-cell end
+    if (tid < kSubCells) {
+      s_off[tid] = incl - v;
+      hdr[tid] = incl;  // sub-cell end
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -490,7 +503,7 @@ __device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist,
   if (threadIdx.x == 0) *so.n_chunks = carry;
 }
 
-__global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp, MapView mt,
+__global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
                                                          const float4* __restrict__ q_pt,
                                                          const double* __restrict__ inv_poses,
@@ -521,9 +534,6 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
     double wq[3];
     d_xform(Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
     const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
-    // distances from the query to its voxel's faces (per-voxel lower bound)
-    const double lo[3] = {wq[0] - bx * a.w, wq[1] - by * a.w, wq[2] - bz * a.w};
-    const double hi[3] = {(bx + 1) * a.w - wq[0], (by + 1) * a.w - wq[1], (bz + 1) * a.w - wq[2]};
     double best = a.bound;
     // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
     // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
@@ -571,21 +581,6 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
         best_rid = tk;
         best_i = i;
       }
-    };
-    // this lane's share (first + g, step kGroup) of records [first, first + count):
-    // four loads in flight per round
-    auto scan_range = [&](uint32_t first, uint32_t count, uint32_t rk) {
-      const uint32_t end = first + count;
-      n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
-      uint32_t i = first + g;
-      for (; i + 3 * kGroup < end; i += 4 * kGroup) {
-        const double4 p0 = M.pos[i], p1 = M.pos[i + kGroup], p2 = M.pos[i + 2 * kGroup], p3 = M.pos[i + 3 * kGroup];
-        fold(p0, i, rk);
-        fold(p1, i + kGroup, rk);
-        fold(p2, i + 2 * kGroup, rk);
-        fold(p3, i + 3 * kGroup, rk);
-      }
-      for (; i < end; i += kGroup) fold(M.pos[i], i, rk);
     };
     // argmin over (d^2, tie key) across the group's lanes with DPP moves (VALU
     // latency, no LDS crossbar): [row_mirror l <-> 15-l,] row_half_mirror l <-> 7-l,
@@ -635,47 +630,86 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
                axis_lb(wq[2], Z, sub / (kSubPerAxis * kSubPerAxis));
       };
       auto sub_beg = [&](int sub) { return sub == 0 ? 0u : hd[sub - 1]; };
-      uint32_t live = 0;
-      if (sorted) {  // header -> LDS (the group's lanes, kPer ends each), then live sub-cells
-        // (s_waitcnt + memory clobber: the other lanes' header entries are read below,
-        // and the previous header's reads must not move past these stores)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // The ranges in hd[] (LDS): a sorted dense cell's header (coalesced copy: lane g
+      // copies entries [g * kPer, (g + 1) * kPer)); any other cell is one range,
+      // hd[0] = its record count.  The s_waitcnt + memory clobbers order the copy after
+      // the previous cell's reads and before the other lanes' reads.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (sorted) {
+        if constexpr (kPer >= 4) {
 #pragma unroll
-        for (int u = 0; u < kPer; u += 4)
-          *reinterpret_cast<uint4*>(hd + g * kPer + u) = *reinterpret_cast<const uint4*>(hdr + g * kPer + u);
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#pragma unroll 1
-        for (int u = 0; u < kPer; ++u) {
-          const int sub = g * kPer + u;
-          if (hd[sub] > sub_beg(sub) && sub_lb(sub) <= best) live |= 1u << u;
+          for (int u = 0; u < kPer; u += 4)
+            *reinterpret_cast<uint4*>(hd + g * kPer + u) = *reinterpret_cast<const uint4*>(hdr + g * kPer + u);
+        } else {
+#pragma unroll
+          for (int u = 0; u < kPer; ++u) hd[g * kPer + u] = hdr[g * kPer + u];
         }
+      } else if (g == 0) {
+        hd[0] = first + count - base;
       }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const int qs = sub_axis(wq[0], X * a.w, sw) + kSubPerAxis * sub_axis(wq[1], Y * a.w, sw) +
+                     kSubPerAxis * kSubPerAxis * sub_axis(wq[2], Z * a.w, sw);
       const int gsh = (lane_id() / kGroup) * kGroup;
-      // the ranges walked: the whole cell (not sorted), else the query's own (nearest)
-      // sub-cell first, then every live sub-cell, its bound re-checked against best
-      for (int step = 0;; ++step) {
-        uint32_t rs = base, re = first + count;
-        if (sorted) {
-          int sub;
-          if (step == 0) {
-            sub = sub_axis(wq[0], X * a.w, sw) + kSubPerAxis * sub_axis(wq[1], Y * a.w, sw) +
-                  kSubPerAxis * kSubPerAxis * sub_axis(wq[2], Z * a.w, sw);
-            if (g == sub / kPer) live &= ~(1u << (sub % kPer));
-          } else {
-            const uint64_t any = (__ballot(live != 0) >> gsh) & ((1ull << kGroup) - 1);
-            if (!any) break;
-            const int l = __ffsll((unsigned long long)any) - 1;
-            sub = l * kPer + __shfl(live ? __ffs(live) - 1 : 0, l, kGroup);
-            if (g == l) live &= live - 1;
+      // Walk 0: the whole cell, or (sorted) the query's own / nearest sub-cell.  Walk 1
+      // (sorted only): every other sub-cell whose box can still hold a closer record.
+      // A walk is ONE virtual range — the chosen ranges' records concatenated in
+      // sub-cell order, split over the group's lanes, FMX_MATCH_DEPTH loads in flight
+      // per lane across range boundaries — then one group min.
+      for (int wk = 0; wk < (sorted ? 2 : 1); ++wk) {
+        uint64_t mask = 0;
+        uint32_t tot = 0;
+        if (!sorted) {
+          mask = 1;
+          tot = hd[0];
+        } else if (wk == 0) {
+          const uint32_t s0 = sub_beg(qs), e0 = hd[qs];
+          if (e0 > s0 && sub_lb(qs) <= best) {
+            mask = 1ull << qs;
+            tot = e0 - s0;
           }
-          const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
-          if (e0 == s0 || sub_lb(sub) > best) continue;
-          rs = base + s0;
-          re = base + e0;
-        } else if (step > 0) {
-          break;
+        } else {  // lane g bounds sub-cells g, g + kGroup, ...; a ballot per stride
+#pragma unroll 1
+          for (int u = 0; u < kPer; ++u) {
+            const int sub = u * kGroup + g;
+            const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
+            const bool lv = sub != qs && e0 > s0 && sub_lb(sub) <= best;
+            if (lv) tot += e0 - s0;
+            mask |= ((__ballot(lv) >> gsh) & ((1ull << kGroup) - 1)) << (u * kGroup);
+          }
+#pragma unroll
+          for (int o = 1; o < kGroup; o <<= 1) tot += __shfl_xor(tot, o, kGroup);
         }
-        scan_range(rs, re - rs, rk);
+        if (tot == 0) continue;
+        int k = __ffsll((unsigned long long)mask) - 1;
+        uint32_t ks = sub_beg(k), ke = hd[k], vbase = 0;
+        auto locate = [&](uint32_t v) {  // v ascending per lane
+          while (v - vbase >= ke - ks) {
+            vbase += ke - ks;
+            mask &= mask - 1;
+            k = __ffsll((unsigned long long)mask) - 1;
+            ks = sub_beg(k);
+            ke = hd[k];
+          }
+          return base + ks + (v - vbase);
+        };
+        n_cand += tot / kGroup + ((uint32_t)g < tot % kGroup ? 1 : 0);
+        constexpr int D = FMX_MATCH_DEPTH;
+        uint32_t v = g;
+        for (; v + (D - 1) * kGroup < tot; v += D * kGroup) {
+          uint32_t ix[D];
+          double4 pr[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) ix[d] = locate(v + d * kGroup);
+#pragma unroll
+          for (int d = 0; d < D; ++d) pr[d] = M.pos[ix[d]];
+#pragma unroll
+          for (int d = 0; d < D; ++d) fold(pr[d], ix[d], rk);
+        }
+        for (; v < tot; v += kGroup) {
+          const uint32_t i = locate(v);
+          fold(M.pos[i], i, rk);
+        }
         group_min();
       }
     };
@@ -685,8 +719,12 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(MatchArgs a, MapView mp
       double lb = 0.0;
 #pragma unroll
       for (int ax = 0; ax < 3; ++ax) {
+        // distance from the query to its cell's face on the side of the shift (recomputed
+        // here rather than kept live: registers)
         const int sa = c_shift[s][ax];
-        const double e = sa > 0 ? hi[ax] + (sa - 1) * a.w : (sa < 0 ? lo[ax] + (-sa - 1) * a.w : 0.0);
+        const int ba = ax == 0 ? bx : (ax == 1 ? by : bz);
+        const double hi = (ba + 1) * a.w - wq[ax], lo = wq[ax] - ba * a.w;
+        const double e = sa > 0 ? hi + (sa - 1) * a.w : (sa < 0 ? lo + (-sa - 1) * a.w : 0.0);
         const double m = fmax(e - 1e-9, 0.0);
         lb += m * m;
       }
