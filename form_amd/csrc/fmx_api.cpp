@@ -950,7 +950,7 @@ void fmx_destroy(fmx_ctx* c) {
     M.table.release(); M.bcnt.release(); M.state.release(); M.rinfo.release(); M.claim.release(); M.dense.release();
     M.pos.release(); M.nrm.release();
   }
-  c->h_mapposes.release(); c->map_blob.release();
+  c->h_mapposes.release(); c->map_blob.release(); c->h_mapinfo.release();
   c->blk_lo.release(); c->blk_hi.release(); c->h_work.release();
   c->work.release(); c->pair_base.release();
   c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();

@@ -81,6 +81,9 @@ __device__ __forceinline__ T wave_sum(T v) {
 __device__ __forceinline__ void host_store(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void host_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void host_store(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

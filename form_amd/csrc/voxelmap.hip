@@ -43,7 +43,13 @@
 #ifndef FMX_MATCH_WAVES
 #define FMX_MATCH_WAVES 4  // waves per SIMD k_match is compiled for (register budget 128)
 #endif
-#define FMX_MATCH_ATTR __attribute__((amdgpu_waves_per_eu(FMX_MATCH_WAVES, 8)))
+#ifndef FMX_MATCH_WAVES_PLAIN
+#define FMX_MATCH_WAVES_PLAIN 6  // ... and without the dense-cell walk (register budget 80)
+#endif
+#ifndef FMX_MATCH_DEPTH_PLAIN
+#define FMX_MATCH_DEPTH_PLAIN 2  // record loads in flight per lane without the dense-cell walk
+#endif
+#define FMX_MATCH_ATTR __attribute__((amdgpu_waves_per_eu(DENSE ? FMX_MATCH_WAVES : FMX_MATCH_WAVES_PLAIN, 8)))
 #ifndef FMX_MATCH_DEPTH
 #define FMX_MATCH_DEPTH 4
 #endif
@@ -97,6 +103,7 @@ constexpr int kDenseThreads = 1024;
 constexpr int kDenseRecs = 8;             // records per thread: dense cells up to 8192 records are sorted
 constexpr uint32_t kUnsorted = 0xFFFFFFFFu;  // header[0] of a dense cell too large to sort
 constexpr uint32_t kDenseGrid = 1024;     // k_map_dense blocks (each loops over the dense list)
+constexpr int kAllocThreads = 1024;       // k_map_alloc: one cursor atomic per block and type
 
 struct BuildArgs {
   const float4* pool_pos[2];
@@ -117,6 +124,7 @@ struct BuildArgs {
   uint32_t* dense;  // dense cells
   BuildState* st;
   BuildState* st_next;
+  unsigned long long* info;  // pinned host word: epoch << 32 | dense cells (k_match<DENSE> choice)
   double4* pos;
   double4* nrm;
 };
@@ -162,19 +170,30 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   Brick* bricks = a.bricks + boff;
   const uint64_t mask = a.mask[R.t];
   uint64_t h = mix64(key) & mask;
+  bool claimed = false;
   for (;;) {  // more buckets than records: a bucket of another epoch always exists
     const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == key) break;
     if (key_epoch(cur) != a.epoch) {  // empty for this build: claim it
       const unsigned long long prev = atomicCAS(&bricks[h].key, cur, key);
       if (prev == cur) {
-        a.claim[atomicAdd(&a.st->nclaim, 1u)] = (uint32_t)(boff + h);
+        claimed = true;
         break;
       }
       if (prev == key) break;
       if (key_epoch(prev) != a.epoch) continue;  // (not reached: only this epoch's keys are written)
     }
     h = (h + 1) & mask;
+  }
+  // claimed bricks onto the claim list: one atomic per wave (a single counter takes
+  // every claim of the build: ~1.2e7 at C5)
+  const uint64_t cm = __ballot(claimed);
+  if (cm) {
+    const int leader = __ffsll((unsigned long long)cm) - 1;
+    uint32_t cb = 0;
+    if (lane_id() == leader) cb = atomicAdd(&a.st->nclaim, (uint32_t)__popcll(cm));
+    cb = __shfl(cb, leader, 64);
+    if (claimed) a.claim[cb + (uint32_t)__popcll(cm & lanemask_lt())] = (uint32_t)(boff + h);
   }
   const uint32_t cell = (uint32_t)((boff + h) * 8 + brick_cell(cx, cy, cz));
   a.rinfo[rec] = make_uint2(cell, atomicAdd(a.bcnt + cell, 1u));
@@ -184,7 +203,7 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
 // state's cursors (one atomic per wave); dense cells reserve kHdr header slots and are
 // listed for k_map_dense.  The grid is sized for the worst case (every record claiming a
 // brick); lanes past nclaim only take part in the wave scans.
-__global__ __launch_bounds__(256) void k_map_alloc(BuildArgs a) {
+__global__ __launch_bounds__(kAllocThreads) void k_map_alloc(BuildArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ncl = __hip_atomic_load(&a.st->nclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x * blockDim.x >= ncl) return;  // whole block past the list
@@ -206,15 +225,30 @@ __global__ __launch_bounds__(256) void k_map_alloc(BuildArgs a) {
       tot += sz[k];
     }
   }
+  // per type: block-wide exclusive scan of the range sizes, one atomic per block
+  __shared__ uint32_t s_w[2][kAllocThreads / kWave];
+  __shared__ uint32_t s_b[2];
+  const int w = threadIdx.x / kWave;
+  uint32_t incl[2], v[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    v[tt] = valid && t == tt ? tot : 0u;
+    incl[tt] = wave_incl_scan(v[tt]);
+    if (lane_id() == 63) s_w[tt][w] = incl[tt];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint32_t bt = 0;
+    for (int i = 0; i < kAllocThreads / kWave; ++i) bt += s_w[threadIdx.x][i];
+    s_b[threadIdx.x] = bt ? atomicAdd(&a.st->cur[threadIdx.x], bt) : 0u;
+  }
+  __syncthreads();
   uint32_t base = 0;
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    const uint32_t v = valid && t == tt ? tot : 0u;
-    const uint32_t incl = wave_incl_scan(v);
-    uint32_t wb = 0;
-    if (lane_id() == 63 && incl) wb = atomicAdd(&a.st->cur[tt], incl);
-    wb = __shfl(wb, 63, 64);
-    if (t == tt) base = wb + incl - v + (tt == 1 ? a.pt_base : 0u);
+    uint32_t wo = s_b[tt];
+    for (int i = 0; i < w; ++i) wo += s_w[tt][i];
+    if (t == tt) base = wo + incl[tt] - v[tt] + (tt == 1 ? a.pt_base : 0u);
   }
   if (!valid) return;
   Brick& B = a.bricks[gb];
@@ -318,6 +352,7 @@ __device__ void dense_sort_cell(const BuildArgs& a, uint32_t cell, uint32_t* s_c
 
 __global__ __launch_bounds__(kDenseThreads) void k_map_dense(BuildArgs a) {
   const uint32_t nd = __hip_atomic_load(&a.st->ndense, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && threadIdx.x == 0) host_store(a.info, ((unsigned long long)a.epoch << 32) | nd);
   __shared__ uint32_t s_cnt[kSubCells];
   __shared__ uint32_t s_off[kSubCells];
   for (uint32_t di = blockIdx.x; di < nd; di += gridDim.x) {
@@ -503,6 +538,9 @@ __device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist,
   if (threadIdx.x == 0) *so.n_chunks = carry;
 }
 
+// DENSE = false: the map has no dense cell (known from the build's pinned info word),
+// so the sub-cell walk is compiled out (fewer registers, more waves in flight).
+template <bool DENSE>
 __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
                                                          const float4* __restrict__ q_pt,
@@ -523,7 +561,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
   const MapView& M = planar ? mp : mt;
   __shared__ uint32_t s_ins;
-  __shared__ uint32_t s_hdr[kQPB][kSubCells];  // dense-cell headers, one per query
+  __shared__ uint32_t s_hdr[DENSE ? kQPB : 1][kSubCells];  // dense-cell headers, one per query
   for (int k = threadIdx.x; k < a.K; k += kMatchThreads) s_hist[k] = 0;
   if (threadIdx.x == 0) s_ins = 0;
   __syncthreads();
@@ -612,12 +650,28 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     // not exceed the best so far, each group-walked (lane g holds sub-cells 8g..8g+7's
     // ends; with kGroup < 8 a lane holds several such blocks).
     const double sw = a.w / kSubPerAxis;
-    uint32_t* hd = s_hdr[threadIdx.x / kGroup];  // this query's copy of a dense cell's header
+    uint32_t* hd = s_hdr[DENSE ? threadIdx.x / kGroup : 0];  // this query's copy of a dense cell's header
     auto scan_cell = [&](uint32_t first, uint32_t count, bool dense, int X, int Y, int Z, uint32_t rk) {
+      if constexpr (!DENSE) {  // no dense cell in the map: the cell's records, split over the lanes
+        constexpr int D = FMX_MATCH_DEPTH_PLAIN;
+        const uint32_t end = first + count;
+        n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
+        uint32_t i = first + g;
+        for (; i + (D - 1) * kGroup < end; i += D * kGroup) {
+          double4 pr[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) pr[d] = M.pos[i + d * kGroup];
+#pragma unroll
+          for (int d = 0; d < D; ++d) fold(pr[d], i + d * kGroup, rk);
+        }
+        for (; i < end; i += kGroup) fold(M.pos[i], i, rk);
+        group_min();
+        return;
+      }
       constexpr int kPer = kSubCells / kGroup;  // sub-cells per lane
       const uint32_t* hdr = reinterpret_cast<const uint32_t*>(M.pos + first);
       const uint32_t base = dense ? first + kHdr : first;
-      const bool sorted = dense && hdr[0] != kUnsorted;
+      const bool sorted = DENSE && dense && hdr[0] != kUnsorted;
       // per sub-cell lower bound (1e-9 slack over the fp rounding of the sub-cell index)
       auto axis_lb = [&](double q, int C, int i) {
         const double lo = C * a.w + i * sw, hi = lo + sw;
@@ -630,12 +684,13 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
                axis_lb(wq[2], Z, sub / (kSubPerAxis * kSubPerAxis));
       };
       auto sub_beg = [&](int sub) { return sub == 0 ? 0u : hd[sub - 1]; };
-      // The ranges in hd[] (LDS): a sorted dense cell's header (coalesced copy: lane g
-      // copies entries [g * kPer, (g + 1) * kPer)); any other cell is one range,
-      // hd[0] = its record count.  The s_waitcnt + memory clobbers order the copy after
-      // the previous cell's reads and before the other lanes' reads.
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // A sorted dense cell's sub-cell ranges in hd[] (LDS; coalesced copy: lane g
+      // copies entries [g * kPer, (g + 1) * kPer)); any other cell is one range.  The
+      // s_waitcnt + memory clobbers order the copy after the previous cell's reads and
+      // before the other lanes' reads.
       if (sorted) {
+        if (g == 0) n_probe += kHdr * 32 / 64;  // the header's 64-B lines (byte model)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (kPer >= 4) {
 #pragma unroll
           for (int u = 0; u < kPer; u += 4)
@@ -644,10 +699,8 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
 #pragma unroll
           for (int u = 0; u < kPer; ++u) hd[g * kPer + u] = hdr[g * kPer + u];
         }
-      } else if (g == 0) {
-        hd[0] = first + count - base;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       const int qs = sub_axis(wq[0], X * a.w, sw) + kSubPerAxis * sub_axis(wq[1], Y * a.w, sw) +
                      kSubPerAxis * kSubPerAxis * sub_axis(wq[2], Z * a.w, sw);
       const int gsh = (lane_id() / kGroup) * kGroup;
@@ -661,7 +714,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         uint32_t tot = 0;
         if (!sorted) {
           mask = 1;
-          tot = hd[0];
+          tot = first + count - base;
         } else if (wk == 0) {
           const uint32_t s0 = sub_beg(qs), e0 = hd[qs];
           if (e0 > s0 && sub_lb(qs) <= best) {
@@ -682,7 +735,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         }
         if (tot == 0) continue;
         int k = __ffsll((unsigned long long)mask) - 1;
-        uint32_t ks = sub_beg(k), ke = hd[k], vbase = 0;
+        uint32_t ks = sorted ? sub_beg(k) : 0u, ke = sorted ? hd[k] : tot, vbase = 0;  // (not sorted: never advances)
         auto locate = [&](uint32_t v) {  // v ascending per lane
           while (v - vbase >= ke - ks) {
             vbase += ke - ks;
@@ -1278,11 +1331,16 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   ba.st_next = bst + ((M.epoch + 1) & 1);
   ba.pos = M.pos.p;
   ba.nrm = M.nrm.p;
+  if (!c->h_mapinfo.p) {
+    c->h_mapinfo.ensure(1);
+    c->h_mapinfo.p[0] = 0;
+  }
+  ba.info = c->h_mapinfo.d;
   const uint32_t nb = std::max<uint32_t>((n + 255) / 256, 1);  // >= 1: block 0 clears the next state
   hipLaunchKernelGGL(k_map_insert, dim3(nb), dim3(256), 0, st, ba);
   FMX_HIP(hipGetLastError());
   if (n > 0) {
-    hipLaunchKernelGGL(k_map_alloc, dim3(nb), dim3(256), 0, st, ba);
+    hipLaunchKernelGGL(k_map_alloc, dim3((n + kAllocThreads - 1) / kAllocThreads), dim3(kAllocThreads), 0, st, ba);
     FMX_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_map_scatter, dim3(nb), dim3(256), 0, st, ba);
     FMX_HIP(hipGetLastError());
@@ -1380,13 +1438,21 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
                    M.pos.p, M.nrm.p, M.epoch};
   };
   // Algorithmic bytes of a match launch: query read (16 B) +
-  // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + 16 B per hash probe +
-  // 36 B per candidate record tested (double4 position + build-order id), using the
+  // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + one 64-B line per
+  // hash probe (a brick; a dense cell's 256-B header counts as 4 probes) + 32 B per
+  // candidate record tested (double4: position + build order/segment), using the
   // probe/candidate counts of the previous launch (counted by the kernel).
-  const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + 16.0 * c->last_probes + 36.0 * c->last_cands;
+  const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + 64.0 * c->last_probes + 32.0 * c->last_cands;
+  // the sub-cell walk only when the map may hold dense cells: the build's pinned info
+  // word (written by k_map_dense) says "none" for this very build (same epoch)
+  bool dense = c->map.n[0] + c->map.n[1] > 0;
+  if (dense && c->h_mapinfo.p) {
+    const unsigned long long w = __atomic_load_n(c->h_mapinfo.p, __ATOMIC_ACQUIRE);
+    if ((uint32_t)(w >> 32) == c->map.epoch && (uint32_t)w == 0) dense = false;
+  }
   if (nb > 0) {
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
-    hipLaunchKernelGGL(k_match, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
+    hipLaunchKernelGGL(dense ? k_match<true> : k_match<false>, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
                        c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
                        c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d,
                        c->ins_blk.p, c->ins_off.p, c->thist.p, so);

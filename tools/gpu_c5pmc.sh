@@ -4,7 +4,7 @@ mkdir -p gpurun_out/pmc_c5
 export TMPDIR=/tmp
 bash tools/gpu_c5prof.sh || exit 1
 python tools/stats_fmx.py $(find gpurun_out/prof_c5 -name "*kernel_stats.csv" | head -1) > gpurun_out/c5_kernel_stats_fmx.csv
-RX='k_match|k_linearize|k_map_insert|k_map_scatter|k_pair_scatter'
+RX='k_match|k_linearize|k_map_|k_pair_scatter'
 i=0
 for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))

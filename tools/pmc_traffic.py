@@ -4,11 +4,20 @@ Usage: python tools/pmc_traffic.py <workload> <out.json> <pass_dir> [<pass_dir> 
 
 Each pass dir holds a rocprofv3 `*counter_collection.csv` of one counter pass
 (FETCH_SIZE, WRITE_SIZE and TCC hit/miss are collected in separate runs, as
-MI355X_MICROARCH.md §rocprofv3 PMC slots requires).  Per MI355X_MICROARCH.md §HBM:
-FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes
-of wide coalesced reads, so hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
-(the raw sum is kept beside it).  Kernel names are mapped to the fmx profile ids
-bench.py uses for the roofline.
+MI355X_MICROARCH.md §rocprofv3 PMC slots requires).  FETCH_SIZE / WRITE_SIZE are in
+KiB.  Corrections, per access pattern (MI355X_MICROARCH.md §HBM for coalesced streams;
+the rest calibrated on known byte counts with tools/pmc_calib, committed as
+profiles/r2_pmc_calibration.txt):
+  * coalesced reads (16 B per lane, or a group's consecutive 32-B records): FETCH_SIZE
+    reports 1/2 of the bytes -> 2 * FETCH_SIZE;
+  * random 64-B lines (brick probes, one record per line): FETCH_SIZE = the bytes of
+    the 64-B lines fetched (calibrated 1.03 and 2.06 x the 64-B / 32-B useful bytes)
+    -> 1 * FETCH_SIZE;
+  * WRITE_SIZE = bytes for both coalesced and scattered 32-B stores (1.00).
+Per kernel: hbm_bytes_per_launch uses the correction of its dominant read pattern
+(GATHER kernels: 1 x FETCH, the others 2 x FETCH); hbm_bytes_hi / hbm_bytes_lo keep
+both bounds (a gather kernel's coalesced share is undercounted by up to 2x in lo).
+Kernel names are mapped to the fmx profile ids bench.py uses for the roofline.
 """
 from __future__ import annotations
 
@@ -30,11 +39,17 @@ KMAP = {
     "k_linearize<1>": "linearize_pairs",
     "k_linearize<0>": "linearize_full",
     "k_map_insert": "map_build_insert",
+    "k_map_alloc": "map_build_alloc",
     "k_map_scatter": "map_build_scatter",
+    "k_map_dense": "map_build_dense",
     "k_insert": "insert",
     "k_win_linearize": "window",  # smoothing mode: many pairs per launch
     "k_pair_scatter": "pair_sort",
 }
+
+
+# kernels whose HBM reads are dominated by random 64-B lines (1 x FETCH_SIZE)
+GATHER = {"match"}
 
 
 def kernel_id(name: str):
@@ -63,13 +78,19 @@ def main():
         avg = {cn: cs[cn] / max(counts[kid][cn], 1) for cn in cs}
         ent = {"counters_per_launch": avg, "launches": max(counts[kid].values())}
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
-            ent["hbm_bytes_raw_per_launch"] = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
-            ent["hbm_bytes_per_launch"] = (2.0 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
+            lo = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
+            hi = (2.0 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
+            ent["hbm_bytes_lo"] = lo
+            ent["hbm_bytes_hi"] = hi
+            ent["correction"] = "1 x FETCH (random 64-B lines)" if kid in GATHER else "2 x FETCH (coalesced)"
+            ent["hbm_bytes_per_launch"] = lo if kid in GATHER else hi
         hit, miss = avg.get("TCC_HIT_sum"), avg.get("TCC_MISS_sum")
         if hit is not None and miss is not None and hit + miss > 0:
             ent["l2_hit_rate"] = hit / (hit + miss)
         kernels[kid] = ent
-    res = {"workload": workload, "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950, MI355X_MICROARCH.md §HBM)",
+    res = {"workload": workload,
+           "correction": "per kernel (see 'correction'): coalesced 2 x FETCH_SIZE, random 64-B lines 1 x FETCH_SIZE "
+                         "(calibrated, profiles/r2_pmc_calibration.txt), + WRITE_SIZE; KiB -> bytes",
            "kernels": kernels}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
