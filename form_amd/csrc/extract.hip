@@ -167,9 +167,11 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     const int nwd = (C + 63) / 64 + 1;
     uint64_t* accb = reinterpret_cast<uint64_t*>(pts) + C;           // accepted (speculative) bitmap
     int* klist = reinterpret_cast<int*>(accb + nwd);                 // [S][P+1] kept columns in key order
+    int* klist2 = klist + S * P1;                                    // [S][P+1] fix-up re-run results
     int* sel_pt = reinterpret_cast<int*>(curv);                      // point selections, per sector at b (after planar)
     __shared__ int s_cntS[16], s_keepS[16], s_nuS[16], s_nptS[16];
-    if (tid < 16) s_cntS[tid] = s_keepS[tid] = s_nuS[tid] = s_nptS[tid] = 0;
+    __shared__ int s_keep2[16], s_hiA[16], s_fin[16];
+    if (tid < 16) s_cntS[tid] = s_keepS[tid] = s_nuS[tid] = s_nptS[tid] = s_keep2[tid] = s_fin[tid] = 0;
     for (int c = tid; c < C; c += kRowThreads) pos[c] = 0xFFFFFFFFu;
     for (int i = tid; i < nwd; i += kRowThreads) accb[i] = 0;
     __syncthreads();
@@ -226,11 +228,15 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     TSTAMP();
     // planar greedy of sector s by one wave (:343-355), as k_extract_rows; columns
     // [b, blk_hi] are suppressed by the previous sector (blk_hi < b: none)
-    auto planar_greedy = [&](int s, int blk_hi) {
+    // A fix-up re-run resumes at candidate rank `start` with the first `kept0` kept
+    // columns already accepted (their decisions cannot change: they precede every
+    // suppressed column in key order); its chunk stamps start at `chunk0` so they never
+    // equal the stale stamps of the speculative run (chunking may differ).
+    auto planar_greedy = [&](int s, int blk_hi, int start, int kept0, uint32_t chunk0, int* out, int* out_keep) {
       const int b = sec_b(s), e = sec_e(s), n = s_cntS[s];
-      int kept = 0;
-      uint32_t chunk = 0;
-      for (int base = 0; base < n && kept < P1; base += kWave, ++chunk) {
+      int kept = kept0;
+      uint32_t chunk = chunk0;
+      for (int base = start; base < n && kept < P1; base += kWave, ++chunk) {
         const uint32_t stamp = ((uint32_t)s << 14) | chunk;
         const int idx = base + lane;
         const bool in = idx < n;
@@ -267,40 +273,104 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
         }
         if ((A >> lane) & 1) {
           const int rank = kept + __popcll(A & lanemask_lt());
-          if (rank < P1) klist[s * P1 + rank] = c;
+          if (rank < P1) out[s * P1 + rank] = c;
           atomicOr(reinterpret_cast<unsigned long long*>(&accb[c >> 6]), 1ull << (c & 63));
         }
         kept += __popcll(A);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
       }
-      if (lane == 0) s_keepS[s] = kept < P1 ? kept : P1;
+      if (lane == 0) out_keep[s] = kept < P1 ? kept : P1;
     };
-    if (w < S) planar_greedy(w, -1);
+    if (w < S) planar_greedy(w, -1, 0, 0, 0, klist, s_keepS);
     __syncthreads();
     TSTAMP();
-    // P4: fix-up in sector order (wave 0)
-    if (w == 0) {
-      for (int s = 1; s < S; ++s) {
-        const int b = sec_b(s), e = sec_e(s);
-        const int np = s_keepS[s - 1];
-        int mx = -1;
-        for (int i = lane; i < np; i += kWave) mx = max(mx, klist[(s - 1) * P1 + i]);
+    // P4: fix-up.  Sector s's final selection depends on sector s-1's only through the
+    // columns [b, hi] that s-1's last kept point suppresses (hi = its column + k - 1).
+    // (a) every sector s >= 1 in parallel (wave s): assume s-1's speculative selection
+    // is final, and if that suppresses one of s's kept columns, re-run s from there
+    // (resume: the kept columns before the first affected one stand) into klist2.
+    // (b) wave 0, in sector order: with s-1's actual final selection, keep (a)'s
+    // outcome when its assumed hi was right (the usual case: re-runs start at the
+    // sector's left edge and rarely move its last kept column), else redo s.
+    auto hi_of = [&](const int* lst, int np, int s) {  // suppression reach into sector s, or -1
+      int mx = -1;
+      for (int i = lane; i < np; i += kWave) mx = max(mx, lst[(s - 1) * P1 + i]);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-        const int hi = min(mx + (k - 1), e - 1);
-        if (mx < 0 || hi < b) continue;
-        // did the speculative run accept a column in [b, hi]?
-        bool hit = false;
-        for (int c = b + lane; c <= hi; c += kWave)
-          if ((accb[c >> 6] >> (c & 63)) & 1) hit = true;
-        if (!__ballot(hit)) continue;
-        for (int c = b + lane; c < e; c += kWave)  // clear the sector's accepted bits
-          atomicAnd(reinterpret_cast<unsigned long long*>(&accb[c >> 6]), ~(1ull << (c & 63)));
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        planar_greedy(s, hi);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+      const int hi = min(mx + (k - 1), sec_e(s) - 1);
+      return (mx < 0 || hi < sec_b(s)) ? -1 : hi;
+    };
+    // resume sector s from its speculative selection with [b, hi] suppressed; returns
+    // false when none of its kept columns lies in [b, hi] (the speculative one stands)
+    auto rerun = [&](int s, int hi, uint32_t chunk0) {
+      const int b = sec_b(s), e = sec_e(s), nk = s_keepS[s];
+      int r0 = P1;
+      for (int i = lane; i < nk; i += kWave)
+        if (klist[s * P1 + i] <= hi) r0 = min(r0, i);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) r0 = min(r0, __shfl_xor(r0, o, 64));
+      if (r0 >= nk) return false;
+      const int col0 = klist[s * P1 + r0];
+      int start = 0x7FFFFFFF;  // its candidate rank in the sorted sector
+      for (int i = lane; i < s_cntS[s]; i += kWave)
+        if (srt[b + i] == col0) start = i;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) start = min(start, __shfl_xor(start, o, 64));
+      for (int c = b + lane; c < e; c += kWave)  // the sector's accepted bits := kept[0, r0)
+        atomicAnd(reinterpret_cast<unsigned long long*>(&accb[c >> 6]), ~(1ull << (c & 63)));
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < r0; i += kWave) {
+        const int c = klist[s * P1 + i];
+        atomicOr(reinterpret_cast<unsigned long long*>(&accb[c >> 6]), 1ull << (c & 63));
+        klist2[s * P1 + i] = c;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      planar_greedy(s, hi, start, r0, chunk0, klist2, s_keep2);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      return true;
+    };
+    __shared__ int s_mxF[16];  // last kept column of each sector's (a) outcome
+    auto last_kept = [&](const int* lst, int np, int s) {
+      int mx = -1;
+      for (int i = lane; i < np; i += kWave) mx = max(mx, lst[s * P1 + i]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+      return mx;
+    };
+    if (w >= 1 && w < S) {  // (a)
+      const int hi = hi_of(klist, s_keepS[w - 1], w);
+      const bool re = hi >= 0 && rerun(w, hi, 512);
+      if (lane == 0) {
+        s_hiA[w] = hi;
+        s_fin[w] = re ? 1 : 0;
+      }
+    }
+    if (w < S) {  // each sector's last kept column after (a)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int fw = s_fin[w];
+      const int mx = last_kept(fw ? klist2 : klist, fw ? s_keep2[w] : s_keepS[w], w);
+      if (lane == 0) s_mxF[w] = mx;
+    }
+    __syncthreads();
+    TSTAMP();
+    if (w == 0) {  // (b): integer checks; a redo (rare) refreshes the sector's last column
+      for (int s = 1; s < S; ++s) {
+        const int mx = s_mxF[s - 1];
+        const int hi0 = min(mx + (k - 1), sec_e(s) - 1);
+        const int hi = (mx < 0 || hi0 < sec_b(s)) ? -1 : hi0;
+        if (hi == s_hiA[s]) continue;
+        const bool re = hi >= 0 && rerun(s, hi, 1024);
+        const int mxn = last_kept(re ? klist2 : klist, re ? s_keep2[s] : s_keepS[s], s);
+        if (lane == 0) {
+          s_fin[s] = re ? 1 : 0;
+          s_mxF[s] = mxn;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __builtin_amdgcn_wave_barrier();
       }
     }
@@ -309,8 +379,8 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     // P5: suppression used[c +- n], n in [0, k) of every kept point (:347-350)
     for (int t = tid; t < S * P1; t += kRowThreads) {
       const int s = t / P1, i = t % P1;
-      if (i < s_keepS[s]) {
-        const int c = klist[t];
+      if (i < (s_fin[s] ? s_keep2[s] : s_keepS[s])) {
+        const int c = s_fin[s] ? klist2[t] : klist[t];
         for (int n = 0; n < k; ++n) {
           used[c + n] = 0;
           used[c - n] = 0;
@@ -320,9 +390,10 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     __syncthreads();
     int pl_count = 0;
     for (int s = 0; s < S; ++s) {
-      const int nk = s_keepS[s];
+      const int nk = s_fin[s] ? s_keep2[s] : s_keepS[s];
+      const int* lst = s_fin[s] ? klist2 : klist;
       for (int i = tid; i < nk; i += kRowThreads)
-        if (pl_count + i < a.cap_pl) sel_slots[(size_t)r * a.cap_pl + pl_count + i] = (uint32_t)klist[s * P1 + i];
+        if (pl_count + i < a.cap_pl) sel_slots[(size_t)r * a.cap_pl + pl_count + i] = (uint32_t)lst[s * P1 + i];
       pl_count += nk;
     }
     TSTAMP();
@@ -456,8 +527,8 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
     if (tid == 0 && (r == 5 || r == 64 || r == 120)) {
       int d[16] = {0};
       for (int i = 1; i < nts && i < 17; ++i) d[i - 1] = (int)(tstamp[i] - tstamp[i - 1]);
-      printf("PAR row %d: pre %d %d %d %d | cand %d sort %d greedy %d fix %d supp+out %d | elig %d pass %d fix %d\n", r, d[0], d[1],
-             d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11]);
+      printf("PAR row %d: pre %d %d %d %d | cand %d sort %d greedy %d fixA %d fixB %d supp+out %d | elig %d pass %d fix %d\n", r,
+             d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11], d[12]);
     }
 #endif
     return;
@@ -1362,7 +1433,7 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   const int pps = C / a.S;
   const size_t nwd = (size_t)(C + 63) / 64 + 1;
   const bool par = pps <= 512 && a.S <= 16 && pps >= 2 * a.k &&
-                   8 * (size_t)C + 8 * nwd + 4 * (size_t)a.S * (a.P + 1) <= 16 * (size_t)C;
+                   8 * (size_t)C + 8 * nwd + 2 * 4 * (size_t)a.S * (a.P + 1) <= 16 * (size_t)C;
   {
     ProfScope ps(c->prof, PROF_EXTRACT_ROWS, 16.0 * N + N, st);
     if (par) {
