@@ -520,6 +520,55 @@ void set_lin(WinGraph& g, B begin, E end) {
   g.lin_end = end;
 }
 
+// Exchange the context's match results with the speculative set (fmx::MatchSet).
+void swap_match_set(fmx_ctx* c) {
+  MatchSet& S = c->spec;
+  using std::swap;
+  swap(c->m_pair, S.m_pair); swap(c->m_d2, S.m_d2); swap(c->m_pi, S.m_pi); swap(c->m_ni, S.m_ni);
+  swap(c->m_ins, S.m_ins); swap(c->hist, S.hist); swap(c->hist_off, S.hist_off); swap(c->thist, S.thist);
+  swap(c->c_pl, S.c_pl); swap(c->c_pt, S.c_pt); swap(c->pair_counts, S.pair_counts);
+  swap(c->chunk_range, S.chunk_range); swap(c->chunks, S.chunks); swap(c->n_chunks, S.n_chunks);
+  swap(c->pair_base, S.pair_base); swap(c->work, S.work); swap(c->mcnt, S.mcnt); swap(c->mticket, S.mticket);
+  swap(c->ins_blk, S.ins_blk); swap(c->ins_off, S.ins_off); swap(c->h_counts, S.h_counts); swap(c->h_work, S.h_work);
+  swap(c->have_match, S.have_match); swap(c->have_corr, S.have_corr); swap(c->scatter_pending, S.scatter_pending);
+  swap(c->counts_pending, S.counts_pending); swap(c->have_qo, S.have_qo); swap(c->ld_pl, S.ld_pl);
+  swap(c->ld_pt, S.ld_pt); swap(c->max_chunks, S.max_chunks); swap(c->work_blocks, S.work_blocks);
+  swap(c->match_nb_pl, S.match_nb_pl); swap(c->match_nb, S.match_nb); swap(c->n_qo, S.n_qo);
+  swap(c->match_group, S.match_group); swap(c->ps, S.ps); swap(c->rows_pl, S.rows_pl); swap(c->rows_pt, S.rows_pt);
+  swap(c->cnt_pl, S.cnt_pl); swap(c->cnt_pt, S.cnt_pt); swap(c->last_probes, S.last_probes);
+  swap(c->last_cands, S.last_cands); swap(c->ins_tot, S.ins_tot);
+}
+
+// Speculative match (smoothing-mode ICP): when an LM trial is probably the LM's last
+// and the ICP loop will probably continue from it, the sorted match of the trial's X(j)
+// is queued on the context stream right behind the trial's linearization, into the
+// speculative set, so it runs while the host takes the LM decision.  If the next ICP
+// iteration starts from exactly that pose it takes these results (use_spec_match)
+// instead of matching again; results are bit-identical either way.  The speculative
+// set is not read by any queued kernel: it was swapped out at the start of this ICP
+// iteration and every kernel that read it belongs to earlier, completed iterations.
+void spec_match(fmx_ctx* c, const double* pose_j) {
+  const fmx_params& P = c->P;
+  swap_match_set(c);
+  try {
+    run_match(c, pose_j, P.max_dist_matching, P.min_dist_map, true);
+  } catch (...) {
+    swap_match_set(c);
+    throw;
+  }
+  swap_match_set(c);
+  std::memcpy(c->spec_pose, pose_j, sizeof(c->spec_pose));
+  c->spec_valid = true;
+  ++c->spec_launched;
+}
+bool use_spec_match(fmx_ctx* c, const double* pose_j) {
+  if (!c->spec_valid || std::memcmp(c->spec_pose, pose_j, sizeof(c->spec_pose)) != 0) return false;
+  swap_match_set(c);
+  c->spec_valid = false;
+  ++c->spec_hits;
+  return true;
+}
+
 // ICP loop (form.cpp:67-89) + optimize(false) (form.cpp:92-93) in smoothing mode:
 // every LM runs over all window poses; the current scan's FeatureFactors linearize
 // from the sorted match, the stored pairs from the window store (window.hip).
@@ -540,7 +589,8 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
   for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
     ++icp;
     const Pose before = e.values.at(j);
-    run_match(c, before.m, P.max_dist_matching, P.min_dist_map, true);  // pair-major
+    if (!use_spec_match(c, before.m)) run_match(c, before.m, P.max_dist_matching, P.min_dist_map, true);  // pair-major
+    c->spec_valid = false;
     // get_graph(true): the current scan's K pairs (empty ones linearize to zero)
     g.pairs.clear();
     for (uint32_t k = 0; k < c->K; ++k) g.pairs.push_back({slot.at(c->map_scans[k]), slot.at(j)});
@@ -552,6 +602,24 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
       std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
       HostScope hs(10);
       win_linearize_current(c, table.data(), sigma, nullptr);
+      // an LM trial the LM will probably stop after (its predicted decrease within the
+      // LM's convergence tolerances, rel/abs 1e-5; the actual decrease decides and
+      // tracks the prediction closely on this stream, profiles/r2_spec_log.txt): match
+      // its X(j) speculatively — the next ICP iteration starts from the LM's final
+      // X(j).  A trial predicted to decrease more is followed by another.
+      const Pose& xj = x[slot.at(j)];
+      const double lc = g.trial_lin_change, ce = g.trial_err;
+      bool last_likely = lc >= 0.0 && (lc <= 1e-5 * ce || lc <= 1e-5);
+      if (last_likely) {  // ... and the ICP loop continues from it (form.cpp:83-88)
+        double xi[6], dn = 0;
+        logmap(compose(inverse(before), xj), xi);
+        for (double v : xi) dn += v * v;
+        last_likely = std::sqrt(dn) >= P.new_pose_threshold;
+      }
+      static const bool spec_log = std::getenv("FMX_SPEC_LOG") != nullptr;  // diagnostic
+      if (spec_log && lc >= 0.0) fprintf(stderr, "spec it %u lin_change %.3e err %.3e rel %.3e\n", it, lc, ce, lc / ce);
+      if (last_likely && it + 1 < P.max_num_rematches && std::memcmp(xj.m, before.m, sizeof(xj.m)) != 0)
+        spec_match(c, xj.m);
     };
     auto lin_end = [&](double* G) {
       HostScope hs(10);
@@ -571,6 +639,10 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
     logmap(compose(inverse(before), after), xi);
     double dn = 0;
     for (double v : xi) dn += v * v;
+    {
+      static const bool spec_log = std::getenv("FMX_SPEC_LOG") != nullptr;  // diagnostic
+      if (spec_log) fprintf(stderr, "icp it %u lm_iters %d final %s\n", it, R.iters, std::sqrt(dn) < P.new_pose_threshold ? "converged" : "next");
+    }
     if (std::sqrt(dn) < P.new_pose_threshold) break;
     e.values[j] = after;  // update_current_pose
   }
@@ -742,6 +814,8 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
                                       " != " + std::to_string(n));
   const uint64_t j = e.init ? e.scan + 1 : 0;
   const uint64_t waits0 = c->host_waits;
+  const uint64_t spec0 = c->spec_launched, hits0 = c->spec_hits;
+  c->spec_valid = false;  // a new map and query set: no speculation carries over
   // Host work that only needs the estimator state runs while this scan's extraction
   // kernels execute: the previous scan's deferred tail (keyscan step +
   // marginalization), then step(prediction) (constraints.cpp:206-223) and the map
@@ -853,6 +927,8 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[6] = lins;
   c->stats[7] = scans.size();
   c->stats[8] = c->host_waits - waits0;
+  c->stats[9] = c->spec_launched - spec0;
+  c->stats[10] = c->spec_hits - hits0;
   if (out) *out = fc;
 }
 
@@ -904,8 +980,13 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
   c->P = *p;
   c->device = device;
   fmx_status st = guard(c, [&] {
-    FMX_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    FMX_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    // the context stream carries the registration's critical path: highest priority;
+    // the side stream (map build beside the extraction, speculative matches beside the
+    // LM) the lowest, so its blocks yield the CUs to the critical path's
+    int prio_lo = 0, prio_hi = 0;
+    FMX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    FMX_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
+    FMX_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_lo));
     FMX_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FMX_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     const uint64_t cap = p->keypoint_pool_capacity ? p->keypoint_pool_capacity : (4u << 20);
@@ -959,6 +1040,14 @@ void fmx_destroy(fmx_ctx* c) {
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
+  {
+    auto& S = c->spec;
+    S.m_pair.release(); S.m_d2.release(); S.m_pi.release(); S.m_ni.release(); S.m_ins.release();
+    S.hist.release(); S.hist_off.release(); S.thist.release(); S.c_pl.release(); S.c_pt.release();
+    S.pair_counts.release(); S.chunk_range.release(); S.chunks.release(); S.n_chunks.release(); S.pair_base.release();
+    S.work.release(); S.mcnt.release(); S.mticket.release(); S.ins_blk.release(); S.ins_off.release();
+    S.h_counts.release(); S.h_work.release();
+  }
   {
     auto& W = c->win;
     for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }

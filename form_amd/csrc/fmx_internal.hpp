@@ -223,9 +223,34 @@ struct WinStore {
   HBuf<uint32_t> hmeta;
 };
 
+// A second set of match outputs: register_scan launches speculative matches into it
+// (on the side stream) and swaps it in when the speculation was right (fmx_api.cpp,
+// swap_match_set).  The members mirror fmx_ctx's match results one to one.
+struct MatchSet {
+  DBuf<int32_t> m_pair;
+  DBuf<double> m_d2;
+  DBuf<double4> m_pi, m_ni;
+  DBuf<uint8_t> m_ins;
+  DBuf<uint32_t> hist, hist_off, thist;
+  DBuf<double> c_pl, c_pt;
+  DBuf<uint32_t> pair_counts, chunk_range;
+  DBuf<Chunk> chunks;
+  DBuf<uint32_t> n_chunks, pair_base, work, mcnt, mticket, ins_blk, ins_off;
+  HBuf<uint32_t> h_counts, h_work;
+  bool have_match = false, have_corr = false, scatter_pending = false, counts_pending = false, have_qo = false;
+  size_t ld_pl = 0, ld_pt = 0;
+  uint32_t max_chunks = 0, work_blocks = 0, match_nb_pl = 0, match_nb = 0, n_qo = 0;
+  int match_group = 8;
+  PairScatter ps;
+  uint64_t rows_pl = 0, rows_pt = 0;
+  std::vector<uint32_t> cnt_pl, cnt_pt;
+  double last_probes = 0, last_cands = 0;
+  uint32_t ins_tot[2] = {0, 0};
+};
+
 }  // namespace fmx
 
-constexpr int kStatsN = 9;  // fmx_last_stats entries
+constexpr int kStatsN = 11;  // fmx_last_stats entries
 
 struct fmx_ctx {
   fmx_params P{};
@@ -322,6 +347,15 @@ struct fmx_ctx {
 
   // ---- smoothing-mode window store
   fmx::WinStore win;
+
+  // ---- speculative matches (register_scan, smoothing mode): the match of the pose an
+  // LM trial proposes, queued behind the trial's linearization while the host decides;
+  // used by the next ICP iteration if it starts from exactly that pose
+  fmx::MatchSet spec;
+  hipStream_t match_stream = nullptr;  // run_match / run_pair_scatter stream override
+  bool spec_valid = false;
+  double spec_pose[12] = {};
+  uint64_t spec_launched = 0, spec_hits = 0;
 
   // ---- multi-GPU exchange (comm.cpp): RCCL communicator, or null
   void* comm = nullptr;

@@ -566,7 +566,10 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
           xn.resize(R.x.size());
           for (size_t k = 0; k < R.x.size(); ++k) xn[k] = compose(R.x[k], expmap(&dx[6 * k]));
           LMP_BEGIN(1);
+          g.trial_lin_change = linChange;
+          g.trial_err = err;
           nerr = asmb.run(xn, Sn, Gn, R.lins);
+          g.trial_lin_change = -1.0;
           LMP_END(1);
           const double costChange = err - nerr;
           if (linChange > DBL_EPSILON * oldLin) success = (costChange / linChange) > 1e-3;

@@ -45,6 +45,11 @@ struct WinGraph {
   // waits for it and fills G.
   std::function<void(const std::vector<Pose>& x)> lin_begin;
   std::function<void(double* G)> lin_end;
+  // Set by window_lm right before a trial's linearization: the trial's predicted cost
+  // decrease (the linear model's) and the current cost; -1 for the first linearization.
+  // A caller may read them in lin_begin (register_scan: speculate only on a trial the
+  // LM will probably stop after).
+  mutable double trial_lin_change = -1.0, trial_err = 0.0;
 };
 
 struct WinLMResult {

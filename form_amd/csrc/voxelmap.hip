@@ -1362,7 +1362,7 @@ void run_pair_scatter(fmx_ctx* c) {
   const PairScatter& s = c->ps;
   const uint32_t nb = s.nb_pl + s.nb_pt;
   if (nb == 0 || c->K == 0) return;
-  hipStream_t st = c->stream;
+  hipStream_t st = c->match_stream ? c->match_stream : c->stream;
   ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
   if (s.tiles)
     hipLaunchKernelGGL(k_pair_scatter_t, dim3(s.ntl_pl + s.ntl_pt), dim3(kTileQ), 0, st, c->n_qpl, c->n_qpt, s.ntl_pl,
@@ -1377,7 +1377,7 @@ void run_pair_scatter(fmx_ctx* c) {
 
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
-  hipStream_t st = c->stream;
+  hipStream_t st = c->match_stream ? c->match_stream : c->stream;
   const int K = std::max<int>((int)c->K, 1);
   MatchArgs a;
   if (pose_j34) std::memcpy(a.Tj, pose_j34, sizeof(a.Tj));

@@ -202,7 +202,9 @@ fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
 
 /* Statistics of the last register_scan, the first n of: {icp_iters, lm_iters,
  * matched_planar, matched_point, map_planar, map_point, linearizations, map_scans,
- * host_waits (host<->device round trips: waits on a completion word or the stream)};
+ * host_waits (host<->device round trips: waits on a completion word or the stream),
+ * spec_matches (speculative matches launched at LM-trial poses), spec_hits (ICP
+ * iterations that used one instead of matching)};
  * entries past the known ones read 0. */
 fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t* stats, int n);
 /* Work of the last fmx_match (counted by the kernel, available while profiling is
