@@ -26,8 +26,11 @@ namespace fmx {
 // 4 for large sets (>= 128k queries, e.g. C5's 2M): they run in several waves of
 // blocks, so more queries per wave raise the loads in flight (C5 match 1.42 -> 1.04 ms,
 // C4 8 lanes 0.22 vs 4 lanes 0.28 ms per scan).
+#ifndef FMX_MATCH_G4_MIN
+#define FMX_MATCH_G4_MIN (128u << 10)  // queries from which 4 lanes per query are used
+#endif
 int match_group_for(uint64_t nq) {
-  return nq >= (128u << 10) ? 4 : 8;
+  return nq >= (uint64_t)(FMX_MATCH_G4_MIN) ? 4 : 8;
 }
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, hipStream_t st) {
   g8::run_map_build(c, scans, poses34, w, st);  // the same build in both variants
