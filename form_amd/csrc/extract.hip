@@ -200,7 +200,15 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
               const int e = lane * 8 + u;
-              const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)v[u], lj, 64);
+              uint64_t o;  // lane lane ^ lj's element u (DPP / permlane: no LDS traffic)
+              switch (lj) {
+                case 1: o = xor_lane<1>(v[u]); break;
+                case 2: o = xor_lane<2>(v[u]); break;
+                case 4: o = xor_lane<4>(v[u]); break;
+                case 8: o = xor_lane<8>(v[u]); break;
+                case 16: o = xor_lane<16>(v[u]); break;
+                default: o = xor_lane<32>(v[u]); break;
+              }
               const bool up = (e & kk) == 0, lower = (e & j) == 0;
               v[u] = (up == lower) ? (v[u] < o ? v[u] : o) : (v[u] < o ? o : v[u]);
             }

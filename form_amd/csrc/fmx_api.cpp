@@ -330,20 +330,29 @@ struct fmx_ctx::Est {
   // every stored pair's linearization at `values` (the last full LM's final state),
   // keyed (j, i): m_fast_linear and marginalize reuse it
   std::map<std::pair<uint64_t, uint64_t>, std::vector<double>> gcache;
-  // keyscan step + marginalization of the last registered scan, deferred to the next
+  // marginalization of the scans the last keyscan step dropped, deferred to the next
   // register_scan where it runs while that scan's extraction kernels execute
   bool tail_pending = false;
-  uint64_t tail_j = 0;
-  uint32_t tail_nfeat = 0;
+  std::vector<uint64_t> tail_marg;
+  // the last scan's constraint counts and map size (fmx_last_stats)
+  uint64_t last_mpl = 0, last_mpt = 0, last_map_pl = 0, last_map_pt = 0;
+  // speculative map build (smoothing mode): the next scan's map built during this
+  // scan's final LM from a trial it will probably end on; valid iff the next scan's
+  // map inputs (scans, poses) equal these bit for bit
+  bool spec_map = false;
+  std::vector<uint64_t> spec_map_scans;
+  std::vector<double> spec_map_poses;
 };
 
 namespace {
 
 // ConstraintManager::predict_next (constraints.cpp:71-101)
-Pose predict_next(const fmx_ctx::Est& e) {
+// `gone`: keys the pending marginalization is about to erase (treated as absent).
+Pose predict_next(const fmx_ctx::Est& e, const std::vector<uint64_t>& gone = {}) {
   if (!e.init) return identity();
   const uint64_t s = e.scan + 1;
-  const bool pe = s > 0 && e.values.count(s - 1), ppe = s > 1 && e.values.count(s - 2);
+  auto has = [&](uint64_t k) { return e.values.count(k) && std::find(gone.begin(), gone.end(), k) == gone.end(); };
+  const bool pe = s > 0 && has(s - 1), ppe = s > 1 && has(s - 2);
   if (pe && ppe) {
     const Pose& prev = e.values.at(s - 1);
     const Pose& pp = e.values.at(s - 2);
@@ -572,14 +581,18 @@ bool use_spec_match(fmx_ctx* c, const double* pose_j) {
   return true;
 }
 
+void keyscan_step(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat);
+void record_cons(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j);
+
 // ICP loop (form.cpp:67-89) + optimize(false) (form.cpp:92-93) in smoothing mode:
 // every LM runs over all window poses; the current scan's FeatureFactors linearize
 // from the sorted match, the stored pairs from the window store (window.hip).
-void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uint64_t& lm_it, uint64_t& lins,
-                     bool& inserted) {
+// fast: m_fast_linear of the window (fast_linear(e)), computed by the caller while the
+// extraction kernels run
+void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, const LinF& fast, uint64_t& icp,
+                     uint64_t& lm_it, uint64_t& lins, bool& inserted) {
   const fmx_params& P = c->P;
   const double sigma = P.planar_constraint_sigma;
-  const LinF fast = fast_linear(e);
   const std::vector<uint64_t> keys = window_keys(e);
   std::map<uint64_t, int> slot;
   for (size_t k = 0; k < keys.size(); ++k) slot[keys[k]] = (int)k;
@@ -650,7 +663,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
     e.values[j] = after;  // update_current_pose
   }
   // the last match is the scan's constraint set: into the window store
-  match_counts_fetch(c);
+  record_cons(c, e, j);
   win_persist(c, j);
   // insert_matches (form.cpp:98-100) reads only the last match (local keypoints and
   // their NN distances), not the poses optimize(false) moves: its kernel goes ahead of
@@ -659,6 +672,18 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
   ensure_pool_room(c, 1, c->n_qpt);
   run_insert(c, j, nullptr);
   inserted = true;
+  // keyscan step (form.cpp:104-111): it reads only the constraint counts, so it runs
+  // before optimize(false); the next map's scans are known from here on
+  keyscan_step(c, e, j, nfeat);
+  FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the insert: the pool is final
+  std::vector<uint64_t> map_scans;
+  {
+    std::set<uint64_t> sset;
+    for (int t = 0; t < 2; ++t)
+      for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
+    map_scans.assign(sset.begin(), sset.end());
+  }
+  int spec_builds = 0;
   // optimize(false): every stored pair's FeatureFactor (constraints.cpp:294-305)
   const std::vector<WinPair> prs = win_pairs(c);
   g.lins.clear();
@@ -671,6 +696,24 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint64_t& icp, uin
     for (size_t k = 0; k < keys.size(); ++k) std::memcpy(&table[12 * k], x[k].m, 12 * sizeof(double));
     HostScope hs(10);
     win_linearize_stored(c, table.data(), (int)keys.size(), sigma, nullptr);
+    // Speculative map build: a trial the LM will probably stop after (predicted decrease
+    // within its 1e-5 tolerances, as for the speculative match) gives the poses the
+    // next scan's map is built from; build it now on the side stream, behind the insert,
+    // while this LM and the next scan's extraction run.  register_scan(j+1) keeps it
+    // only if its map inputs are exactly these.
+    const double lc = g.trial_lin_change, ce = g.trial_err;
+    if (lc >= 0.0 && (lc <= 1e-5 * ce || lc <= 1e-5) && spec_builds < 2 && !map_scans.empty()) {
+      ++spec_builds;
+      std::vector<double> mp(12 * map_scans.size());
+      for (size_t k = 0; k < map_scans.size(); ++k) std::memcpy(&mp[12 * k], x[slot.at(map_scans[k])].m, 12 * sizeof(double));
+      if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));  // pinned staging reuse (see register_scan)
+      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      run_map_build(c, map_scans, mp.data(), P.max_dist_matching, c->side);
+      FMX_HIP(hipEventRecord(c->ev_join, c->side));
+      e.spec_map = true;
+      e.spec_map_scans = map_scans;
+      e.spec_map_poses = std::move(mp);
+    }
   };
   auto lin_end = [&](double* G) {
     HostScope hs(10);
@@ -782,21 +825,45 @@ void remove_scan(fmx_ctx* c, uint64_t s) {  // KeypointMap::remove (map.tpp:112-
 // and factors remain), never the registered poses, so register_scan defers it to the
 // next call (where it overlaps that scan's extraction); entry points that read the
 // keypoint pool run it first.
+// The tail of register_scan (form.cpp:104-111), in two parts.  The keyscan step runs
+// as soon as the scan's constraint counts are known (it reads only those): the
+// dropped scans leave the keypoint pool, so the next map no longer holds them.  The
+// marginalization proper (host-only factor bookkeeping; it moves no pose, so the map
+// does not depend on it) is deferred to the next register_scan, where it overlaps
+// that scan's extraction; entry points that read the estimator state run it first.
+void keyscan_step(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat) {
+  auto marg = e.ks.step(j, nfeat, [&](uint64_t i) { return num_recent_connections(e, i, e.ks.oldest_rf()); });
+  for (uint64_t m : marg) remove_scan(c, m);
+  e.tail_marg = std::move(marg);
+  e.tail_pending = true;
+}
+// the constraint counts of scan j's last match (ConstraintManager bookkeeping)
+void record_cons(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j) {
+  match_counts_fetch(c);
+  auto& cj = e.cons[j];
+  e.last_mpl = e.last_mpt = 0;
+  for (uint32_t k = 0; k < c->K; ++k) {
+    cj[c->map_scans[k]] = {c->cnt_pl[k], c->cnt_pt[k]};
+    e.last_mpl += c->cnt_pl[k];
+    e.last_mpt += c->cnt_pt[k];
+  }
+  e.last_map_pl = c->map.n[0];
+  e.last_map_pt = c->map.n[1];
+}
 void finish_tail(fmx_ctx* c, fmx_ctx::Est& e) {
   if (!e.tail_pending) return;
   e.tail_pending = false;
+  const std::vector<uint64_t> marg = std::move(e.tail_marg);
+  e.tail_marg.clear();
+  if (marg.empty()) return;
   HostScope hs(5);
   const fmx_params& P = c->P;
-  auto marg = e.ks.step(e.tail_j, e.tail_nfeat, [&](uint64_t i) {
-    return num_recent_connections(e, i, e.ks.oldest_rf());
-  });
   if (!P.disable_smoothing) smooth_marginalize(e, marg);
   for (uint64_t m : marg) {
     if (!P.disable_smoothing) win_remove(c, m);
     e.values.erase(m);
     e.cons.erase(m);
     for (auto& [jj, mm] : e.cons) mm.erase(m);
-    remove_scan(c, m);
   }
 }
 void finish_tail(fmx_ctx* c) {
@@ -827,22 +894,29 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   // depend on this scan's features.
   std::vector<uint64_t> scans;
   std::vector<double> poses;
+  // prepare: the keyscan step, prediction and map inputs (the map build is queued right
+  // after it); finish: the marginalization proper and the new scan's constraint slots.
+  bool map_spec_used = false;
   auto prepare = [&] {
-    finish_tail(c, e);
-    const Pose pred = predict_next(e);
-    e.scan = j;
-    e.init = true;
-    e.values[j] = pred;
-    if (j == 0) e.priors.push_back(PriorF{0, pred, 1e-3});  // addPrior (constraints.cpp:217-220)
-    auto& cj = e.cons[j];
-    for (auto& [i, T] : e.values)
-      if (i != j) cj[i] = {0, 0};
+    const Pose pred = predict_next(e, e.tail_pending ? e.tail_marg : std::vector<uint64_t>{});
     std::set<uint64_t> sset;
     for (int t = 0; t < 2; ++t)
       for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
     scans.assign(sset.begin(), sset.end());
     poses.resize(12 * scans.size());
     for (size_t k = 0; k < scans.size(); ++k) std::memcpy(&poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double));
+    e.scan = j;
+    e.init = true;
+    e.values[j] = pred;
+    if (j == 0) e.priors.push_back(PriorF{0, pred, 1e-3});  // addPrior (constraints.cpp:217-220)
+  };
+  LinF fast;
+  auto finish = [&] {
+    finish_tail(c, e);
+    auto& cj = e.cons[j];
+    for (auto& [i, T] : e.values)
+      if (i != j) cj[i] = {0, 0};
+    if (!P.disable_smoothing) fast = fast_linear(e);  // m_fast_linear (constraints.cpp:257-288)
   };
   // The map build goes to the side stream and is queued while the extraction kernels
   // run (extraction occupies one CU per scan line, so the build's kernels take the
@@ -853,19 +927,29 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     HostScope hs_ex(2);
     do_extract(c, xyzw, n, j, on_dev, &fc, [&] {
       prepare();
-      HostScope hs_map(3);
-      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
-      FMX_HIP(hipEventRecord(c->ev_join, c->side));
+      const bool spec_ok = e.spec_map && e.spec_map_scans == scans && e.spec_map_poses.size() == poses.size() &&
+                           std::memcmp(e.spec_map_poses.data(), poses.data(), poses.size() * sizeof(double)) == 0;
+      if (e.spec_map) ++(spec_ok ? c->spec_map_hits : c->spec_map_misses);
+      map_spec_used = spec_ok;
+      if (!spec_ok) {
+        HostScope hs_map(3);
+        // a discarded speculative build may still be reading the pinned pose staging
+        // buffer this build rewrites: drain it first (misses are rare)
+        if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));
+        FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
+        FMX_HIP(hipEventRecord(c->ev_join, c->side));
+      }
+      e.spec_map = false;
+      finish();
     });
   }
   FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
-  auto& cj = e.cons[j];
   HostScope* hs_icp = new HostScope(4);
   uint64_t icp = 0, lm_it = 0, lins = 0;
   bool inserted = false;
   if (!P.disable_smoothing) {
-    smooth_register(c, e, j, icp, lm_it, lins, inserted);
+    smooth_register(c, e, j, fc.planar + fc.point, fast, icp, lm_it, lins, inserted);
   } else {
     // ICP loop (form.cpp:67-89) with the LM on the host (one sync per linearization)
     DeviceLM lm{c, e, P.planar_constraint_sigma};
@@ -903,35 +987,27 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     lins = lm.linearizations;
   }
   delete hs_icp;
-  HostScope hs_tail(5);
-  match_counts_fetch(c);
-  uint64_t mpl = 0, mpt = 0;
-  for (uint32_t k = 0; k < c->K; ++k) {
-    cj[c->map_scans[k]] = {c->cnt_pl[k], c->cnt_pt[k]};
-    mpl += c->cnt_pl[k];
-    mpt += c->cnt_pt[k];
-  }
-  // insert_matches (form.cpp:98-100) from the last match
-  if (!inserted) {
+  if (!inserted) {  // single-pose mode
+    HostScope hs_tail(5);
+    record_cons(c, e, j);
+    // insert_matches (form.cpp:98-100) from the last match
     ensure_pool_room(c, 0, c->n_qpl);
     ensure_pool_room(c, 1, c->n_qpt);
     run_insert(c, j, nullptr);
+    keyscan_step(c, e, j, fc.planar + fc.point);  // marginalization: deferred (finish_tail)
   }
-  // keyscan selection + marginalization (form.cpp:104-111): deferred (finish_tail)
-  e.tail_pending = true;
-  e.tail_j = j;
-  e.tail_nfeat = fc.planar + fc.point;
   c->stats[0] = icp;
   c->stats[1] = lm_it;
-  c->stats[2] = mpl;
-  c->stats[3] = mpt;
-  c->stats[4] = c->map.n[0];
-  c->stats[5] = c->map.n[1];
+  c->stats[2] = e.last_mpl;
+  c->stats[3] = e.last_mpt;
+  c->stats[4] = e.last_map_pl;
+  c->stats[5] = e.last_map_pt;
   c->stats[6] = lins;
   c->stats[7] = scans.size();
   c->stats[8] = c->host_waits - waits0;
   c->stats[9] = c->spec_launched - spec0;
   c->stats[10] = c->spec_hits - hits0;
+  c->stats[11] = map_spec_used ? 1 : 0;
   if (out) *out = fc;
 }
 

@@ -58,6 +58,35 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
   }
   return v;
 }
+// Value of lane (lane ^ LJ) without the LDS crossbar (ds_bpermute): DPP quad
+// permutes for 1 and 2, row shifts + select for 4, a row rotate for 8, the gfx950
+// permlane16/32 swaps + select for 16 and 32.  VALU only.
+template <int LJ>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
+  static_assert(LJ == 1 || LJ == 2 || LJ == 4 || LJ == 8 || LJ == 16 || LJ == 32, "xor distance");
+  if constexpr (LJ == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+  if constexpr (LJ == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
+  if constexpr (LJ == 4) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0xF, false);  // row_shl:4 (l <- l+4)
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4 (l <- l-4)
+    return (__lane_id() & 4) ? dn : up;
+  }
+  if constexpr (LJ == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+  if constexpr (LJ == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (__lane_id() & 16) ? r[0] : r[1];
+  }
+  if constexpr (LJ == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (__lane_id() & 32) ? r[0] : r[1];
+  }
+  return x;
+}
+template <int LJ>
+__device__ __forceinline__ uint64_t xor_lane(uint64_t v) {
+  return ((uint64_t)xor_lane<LJ>((uint32_t)(v >> 32)) << 32) | xor_lane<LJ>((uint32_t)v);
+}
+
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

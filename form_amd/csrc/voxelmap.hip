@@ -153,38 +153,79 @@ __device__ __forceinline__ RecW rec_world(const BuildArgs& a, uint32_t rec, bool
   return o;
 }
 
+// Lanes of a wave holding equal values, grouped: for each lane (valid ones only) the
+// group's first lane and the lane's rank among the group's lanes; that first lane
+// also gets the group's size.  One round per distinct value (VALU only), so the
+// group's atomics are issued once per group, by its first lane, all groups at once.
+__device__ __forceinline__ void wave_group(bool valid, unsigned long long v, int& leader, uint32_t& rank,
+                                           uint32_t& size) {
+  uint64_t todo = __ballot(valid);
+  leader = -1;
+  rank = 0;
+  size = 0;
+  while (todo) {
+    const int l = __ffsll((unsigned long long)todo) - 1;
+    const unsigned long long lv =
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const bool in = valid && v == lv;
+    const uint64_t m = __ballot(in);
+    if (in) {
+      leader = l;
+      rank = (uint32_t)__popcll(m & lanemask_lt());
+    }
+    if (lane_id() == l) size = (uint32_t)__popcll(m);
+    todo &= ~m;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildState) / 4)  // the next build's state
     reinterpret_cast<uint32_t*>(a.st_next)[threadIdx.x] = 0u;
-  if (rec >= a.n) return;
-  const RecW R = rec_world(a, rec, false);
-  const int cx = (int)floor(R.p[0] / a.w), cy = (int)floor(R.p[1] / a.w), cz = (int)floor(R.p[2] / a.w);
-  if (!key_in_range(cx, cy, cz)) {
-    atomicOr(&a.st->err, 1u);
-    a.rinfo[rec] = make_uint2(0xFFFFFFFFu, 0u);
-    return;
-  }
-  const unsigned long long key = brick_key(cx, cy, cz, a.epoch);
-  const uint64_t boff = R.t == 0 ? 0 : a.off1;
-  Brick* bricks = a.bricks + boff;
-  const uint64_t mask = a.mask[R.t];
-  uint64_t h = mix64(key) & mask;
-  bool claimed = false;
-  for (;;) {  // more buckets than records: a bucket of another epoch always exists
-    const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur == key) break;
-    if (key_epoch(cur) != a.epoch) {  // empty for this build: claim it
-      const unsigned long long prev = atomicCAS(&bricks[h].key, cur, key);
-      if (prev == cur) {
-        claimed = true;
-        break;
-      }
-      if (prev == key) break;
-      if (key_epoch(prev) != a.epoch) continue;  // (not reached: only this epoch's keys are written)
+  if (blockIdx.x * blockDim.x >= a.n) return;  // (whole waves past the records; the rest stay for the groups)
+  bool valid = rec < a.n;
+  int cx = 0, cy = 0, cz = 0, t = 0;
+  if (valid) {
+    const RecW R = rec_world(a, rec, false);
+    cx = (int)floor(R.p[0] / a.w), cy = (int)floor(R.p[1] / a.w), cz = (int)floor(R.p[2] / a.w);
+    t = R.t;
+    if (!key_in_range(cx, cy, cz)) {
+      atomicOr(&a.st->err, 1u);
+      a.rinfo[rec] = make_uint2(0xFFFFFFFFu, 0u);
+      valid = false;
     }
-    h = (h + 1) & mask;
   }
+  // records of one brick (consecutive records are mostly neighbours): its first lane
+  // probes / claims for the group
+  const unsigned long long key = brick_key(cx, cy, cz, a.epoch) ^ (unsigned long long)t << 63;  // (bit 63: type, grouping only)
+  int bl;
+  uint32_t brank, bsize;
+  wave_group(valid, key, bl, brank, bsize);
+  const unsigned long long bkey = brick_key(cx, cy, cz, a.epoch);
+  const uint64_t boff = t == 0 ? 0 : a.off1;
+  Brick* bricks = a.bricks + boff;
+  const uint64_t mask = a.mask[t];
+  uint64_t h = mix64(bkey) & mask;
+  bool claimed = false;
+  const bool prober = valid && brank == 0;
+  if (prober) {
+    for (;;) {  // more buckets than records: a bucket of another epoch always exists
+      const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == bkey) break;
+      if (key_epoch(cur) != a.epoch) {  // empty for this build: claim it
+        const unsigned long long prev = atomicCAS(&bricks[h].key, cur, bkey);
+        if (prev == cur) {
+          claimed = true;
+          break;
+        }
+        if (prev == bkey) break;
+        if (key_epoch(prev) != a.epoch) continue;  // (not reached: only this epoch's keys are written)
+      }
+      h = (h + 1) & mask;
+    }
+  }
+  h = (uint64_t)__shfl((unsigned long long)h, bl < 0 ? 0 : bl, 64);  // the group's bucket
   // claimed bricks onto the claim list: one atomic per wave (a single counter takes
   // every claim of the build: ~1.2e7 at C5)
   const uint64_t cm = __ballot(claimed);
@@ -195,8 +236,15 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
     cb = __shfl(cb, leader, 64);
     if (claimed) a.claim[cb + (uint32_t)__popcll(cm & lanemask_lt())] = (uint32_t)(boff + h);
   }
+  // rank in the cell: one count atomic per (wave, cell) group
   const uint32_t cell = (uint32_t)((boff + h) * 8 + brick_cell(cx, cy, cz));
-  a.rinfo[rec] = make_uint2(cell, atomicAdd(a.bcnt + cell, 1u));
+  int cl;
+  uint32_t crank, csize;
+  wave_group(valid, cell, cl, crank, csize);
+  uint32_t cbase = 0;
+  if (valid && crank == 0) cbase = atomicAdd(a.bcnt + cell, csize);
+  cbase = (uint32_t)__shfl((int)cbase, cl < 0 ? 0 : cl, 64);
+  if (valid) a.rinfo[rec] = make_uint2(cell, cbase + crank);
 }
 
 // One lane per claimed brick: record ranges of its 8 cells, allocated per type from the
@@ -567,6 +615,13 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   __syncthreads();
   const uint32_t t_begin = (uint32_t)wall_clock64();
   uint32_t n_probe = 0, n_cand = 0;
+#ifdef FMX_MATCH_SPLIT  // diagnostic build: candidates of pass 0, of walk 1, of passes >= 1
+  uint32_t n_c0 = 0, n_cw1 = 0, n_cp12 = 0;
+  int cur_pass = 0;
+#define SPLIT_ADD(v, wk) (cur_pass == 0 ? n_c0 : n_cp12) += (v), n_cw1 += (wk) == 1 ? (v) : 0u
+#else
+#define SPLIT_ADD(v, wk) ((void)0)
+#endif
   if (qi < nq) {
     const float4 lq = planar ? q_pl[qi] : q_pt[qi];
     double wq[3];
@@ -656,6 +711,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         constexpr int D = FMX_MATCH_DEPTH_PLAIN;
         const uint32_t end = first + count;
         n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
+        SPLIT_ADD(count / kGroup + (g < (int)(count % kGroup) ? 1 : 0), 0);
         uint32_t i = first + g;
         for (; i + (D - 1) * kGroup < end; i += D * kGroup) {
           double4 pr[D];
@@ -747,6 +803,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
           return base + ks + (v - vbase);
         };
         n_cand += tot / kGroup + ((uint32_t)g < tot % kGroup ? 1 : 0);
+        SPLIT_ADD(tot / kGroup + ((uint32_t)g < tot % kGroup ? 1 : 0), wk);
         constexpr int D = FMX_MATCH_DEPTH;
         uint32_t v = g;
         for (; v + (D - 1) * kGroup < tot; v += D * kGroup) {
@@ -792,6 +849,9 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     // One loop over the passes, so the cell walk is emitted once.
     const int npass = a.rings >= 2 ? 4 : 3;
     for (int ip = 0; ip < npass; ++ip) {
+#ifdef FMX_MATCH_SPLIT
+      cur_pass = ip;
+#endif
       const int s_begin = ip == 0 ? 0 : (ip == 1 ? 1 : (ip == 2 ? 7 : 27));
       const int s_end = ip == 0 ? 1 : (ip == 1 ? 7 : (ip == 2 ? 27 : 125));
       for (int s0 = s_begin; s0 < s_end; s0 += kGroup) {  // one shift per lane per chunk
@@ -820,6 +880,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
           for (int u = 0; u < kSmallCell; ++u)
             if (u < (int)vc) fold(pr[u], vf + u, rk);
           n_cand += vc;
+          SPLIT_ADD(vc, 0);
         }
         const int gsh = (lane_id() / kGroup) * kGroup;
         if ((__ballot(small) >> gsh) & ((1ull << kGroup) - 1)) group_min();
@@ -895,6 +956,18 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     w4[0] = make_uint4(tp, tc, mq, 0u);
     w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), 0u, 0u);
   }
+#ifdef FMX_MATCH_SPLIT
+  __syncthreads();  // after thread 0's plain stores of this block's words
+  {
+    const uint32_t s0 = wave_sum(n_c0), s1 = wave_sum(n_cw1), s2 = wave_sum(n_cp12);
+    uint32_t* wb = work + 8 * blockIdx.x;
+    if (lane_id() == 0) {
+      atomicAdd(wb + 3, s0);
+      atomicAdd(wb + 6, s1);
+      atomicAdd(wb + 7, s2);
+    }
+  }
+#endif
   if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
     __hip_atomic_store(ins_blk + blockIdx.x, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int t = planar ? 0 : 1;

@@ -204,7 +204,9 @@ fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
  * matched_planar, matched_point, map_planar, map_point, linearizations, map_scans,
  * host_waits (host<->device round trips: waits on a completion word or the stream),
  * spec_matches (speculative matches launched at LM-trial poses), spec_hits (ICP
- * iterations that used one instead of matching)};
+ * iterations that used one instead of matching), spec_map (1 when the scan's map was
+ * the one built speculatively during the previous scan's final LM, 0 when built at
+ * the start of this scan)};
  * entries past the known ones read 0. */
 fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t* stats, int n);
 /* Work of the last fmx_match (counted by the kernel, available while profiling is

@@ -38,3 +38,11 @@ if len(starts) >= 3:
     print("per-step kernel time (us):")
     for k, v in sorted(tot.items(), key=lambda x: -x[1]):
         print(f"  {v / nsteps:8.1f}  {k}")
+# step spans (extraction start to the next extraction start) over the timed steps:
+# the last `timed` steps of the trace (bench.py --steps), robust to one odd step
+timed = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+spans = sorted((ev[starts[i + 1]][0] - ev[starts[i]][0]) / 1e3 for i in range(max(0, len(starts) - 1 - timed), len(starts) - 1))
+if spans:
+    import statistics
+    print(f"step span over the last {len(spans)} steps: median {statistics.median(spans):.1f} us, "
+          f"p10 {spans[len(spans) // 10]:.1f}, p90 {spans[(9 * len(spans)) // 10]:.1f}, mean {sum(spans) / len(spans):.1f}")
