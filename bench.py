@@ -62,6 +62,9 @@ def parse():
                     help="ConstraintManager mode: smooth = the reference default (window smoother), "
                          "single = the disable_smoothing ablation (single-pose LM)")
     ap.add_argument("--no-ablation", action="store_true", help="skip the other mode's secondary measurement")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="register without announcing the next scan (fmx_next_scan): each register_scan "
+                         "extracts its own scan first instead of during the previous registration")
     ap.add_argument("--no-pin", action="store_true",
                     help="leave the registering thread unpinned (default: bound to the CPU it runs on for the "
                          "GPU measurements, released before the CPU baseline)")
@@ -199,16 +202,26 @@ def cpu_baseline(scans_host, params, budget_s, single):
                 ms_per_scan=per * 1e3, **hi), poses
 
 
-def ate_block(scans_host, oracle_poses, params, k0, device, single):
+def register(ctx, scans, k, pipeline):
+    """register_scan(scans[k]); pipelined: announce scans[k + 1] first, so this call
+    extracts it while registering scans[k] (fmx_next_scan)."""
+    if pipeline and k + 1 < len(scans):
+        ctx.next_scan(scans[k + 1])
+    ctx.register_scan(scans[k])
+
+
+def ate_block(scans_host, oracle_poses, params, k0, device, single, pipeline):
     """ATE of the GPU path and of the CPU oracle path over the same scans against the
     synthetic ground truth (the newer_college ATE is unavailable
-    offline).  Untimed; a fresh context replays the sample."""
+    offline).  Untimed; a fresh context replays the sample (from device copies, in the
+    bench's pipelined mode)."""
     n = len(oracle_poses)
     ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params),
                                           disable_smoothing=single), device=device)
+    dscans = [torch.from_numpy(s).to(f"cuda:{device}") for s in scans_host[:n]]
     gpu = []
-    for s in scans_host[:n]:
-        ctx.register_scan(s)
+    for k in range(n):
+        register(ctx, dscans, k, pipeline)
         gpu.append(ctx.current_pose())
     gt = [synth.trajectory_pose(k0 + k) for k in range(n)]
     a_gpu, a_cpu = metrics.ate_rmse(gpu, gt), metrics.ate_rmse(oracle_poses, gt)
@@ -363,31 +376,37 @@ def main():
                            device=local)
 
     prev_aff = None if a.no_pin else pin_thread(world, local)
-    ablation = None
-    if not a.no_ablation:  # the other mode over the same scans (secondary, untimed by the driver)
-        actx = new_ctx(not single)
+    pipe = not a.no_pipeline
+
+    def secondary(single_pose, pipeline):  # another mode over the same scans (untimed by the driver)
+        actx = new_ctx(single_pose)
         for k in range(pre + a.warmup):
-            actx.register_scan(scans[k])
+            register(actx, scans, k, pipeline)
         actx.sync()
         ta = time.perf_counter()
         for k in range(pre + a.warmup, pre + a.warmup + a.steps):
-            actx.register_scan(scans[k])
+            register(actx, scans, k, pipeline)
         actx.sync()
         ta = time.perf_counter() - ta
-        ablation = {"mode": "single-pose (disable_smoothing)" if not single else "smoothing (default)",
-                    "scans_per_s": round(a.steps / ta, 3), "ms_per_step": round(ta / a.steps * 1e3, 3)}
         actx.close()
-        del actx
+        return {"scans_per_s": round(a.steps / ta, 3), "ms_per_step": round(ta / a.steps * 1e3, 3)}
+
+    ablation = None
+    if not a.no_ablation:
+        ablation = {"mode": "single-pose (disable_smoothing)" if not single else "smoothing (default)",
+                    **secondary(not single, pipe)}
+    # the same mode with every scan extracted inside its own register_scan (no fmx_next_scan)
+    sequential = secondary(single, False) if pipe else None
     ctx = new_ctx(single)
     for k in range(pre + a.warmup):
-        ctx.register_scan(scans[k])
+        register(ctx, scans, k, pipe)
     ctx.sync()
     stats = []
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(pre + a.warmup, pre + a.warmup + a.steps):
-        ctx.register_scan(scans[k])
+        register(ctx, scans, k, pipe)
     ctx.sync()
     torch.cuda.synchronize()
     barrier(world)
@@ -398,7 +417,7 @@ def main():
     ctx.profile(True)
     ctx.profile_reset()
     for k in range(pre + a.warmup + a.steps, total):
-        ctx.register_scan(scans[k])
+        register(ctx, scans, k, pipe)
         stats.append(ctx.last_stats())
     ctx.sync()
     prof = ctx.profile_read()
@@ -448,7 +467,12 @@ def main():
                                f"register_scan, {'single-pose ablation (disable_smoothing)' if single else 'smoothing mode (ConstraintManager default)'}",
                    "points_per_scan": n_pts, "parallelism": f"replicas x{world}",
                    "timed_scans": [pre + a.warmup, pre + a.warmup + a.steps],
-                   "prefill": pre},
+                   "prefill": pre,
+                   # pipelined: each register_scan also extracts the next scan (announced with
+                   # fmx_next_scan) on a side stream; the timed region runs as many extractions
+                   # as scans (the first timed scan's ran in the warmup, the scan after the last
+                   # timed one's runs inside)
+                   "pipelined_extraction": pipe},
         "mpts_per_s": round(value * n_pts / 1e6, 3),
         "roofline": roof,
         "kernels_ms_per_step": kern_ms,
@@ -462,6 +486,8 @@ def main():
     }
     if ablation is not None:
         out["ablation"] = ablation
+    if sequential is not None:
+        out["sequential_extraction"] = sequential
     if c5 is not None:
         out["sharded_c5"] = c5
     if prev_aff is not None:
@@ -470,7 +496,7 @@ def main():
         host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
         del scans
         out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s, single)
-        out["ate"] = ate_block(host, opos, params, k0, local, single)
+        out["ate"] = ate_block(host, opos, params, k0, local, single, pipe)
     print(json.dumps(out))
     if world > 1:
         import torch.distributed as dist

@@ -1395,8 +1395,8 @@ __global__ __launch_bounds__(256) void k_write_features(const float4* __restrict
 
 }  // namespace
 
-void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
-                 const std::function<void()>& while_waiting) {
+ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
+                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq) {
   const auto& E = c->P.extraction;
   ExArgs a;
   a.R = R;
@@ -1412,7 +1412,6 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   a.max2 = E.max_norm_squared;
   a.radius2 = E.radius * E.radius;
   a.min_points = (int)E.min_points;
-  hipStream_t st = c->stream;
   const size_t N = (size_t)R * C;
   c->planar_mask.ensure(N);
   c->sel_slots.ensure((size_t)R * a.cap_pl);
@@ -1422,7 +1421,6 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
   c->row_off.ensure(3 * ((size_t)R + 1));
   c->closest.ensure((size_t)R * a.cap_pl);
   c->nrm_slots.ensure((size_t)R * a.cap_pl);
-  c->h_u32.ensure(8);
   c->rows = R;
   c->cols = C;
   const size_t lds = (size_t)C * (16 + 4 + 4 + 4 + 4);
@@ -1501,12 +1499,10 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
                          c->row_counts.p, c->closest.p, a, c->nrm_slots.p, c->row_ok.p);
     }
   }
-  uint32_t seq = 0;
   {
     ProfScope ps(c->prof, PROF_COMPACT, 0.0, st);
-    seq = next_flag(c);
     hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, st, c->row_counts.p, c->row_ok.p, R, c->row_off.p,
-                       c->h_u32.d, c->h_flag.d, seq);
+                       tot_d, flag_d, seq);
   }
   FMX_HIP(hipGetLastError());
   // k_write_features needs only the device row offsets, and its outputs are sized for
@@ -1527,10 +1523,20 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
                        c->q_pl_idx.p, c->q_pt_pos.p, c->q_pt_idx.p);
   }
   FMX_HIP(hipGetLastError());
-  if (while_waiting) while_waiting();
-  wait_flag(c, c->h_flag.p, seq);
-  const uint32_t npl = c->h_u32.p[0], npt = c->h_u32.p[1], nsel = c->h_u32.p[2];
-  if (npl > max_pl || npt > max_pt || nsel > max_pl) throw StatusError(FMX_E_HIP, "implausible feature totals");
+  ExLaunch L;
+  L.seq = seq;
+  L.flag = flag_h;
+  L.tot = tot_h;
+  L.max_pl = max_pl;
+  L.max_pt = max_pt;
+  L.st = st;
+  return L;
+}
+
+void extract_collect(fmx_ctx* c, const ExLaunch& L, fmx_feature_counts* out) {
+  wait_flag(c, L.flag, L.seq, L.st);
+  const uint32_t npl = L.tot[0], npt = L.tot[1], nsel = L.tot[2];
+  if (npl > L.max_pl || npt > L.max_pt || nsel > L.max_pl) throw StatusError(FMX_E_HIP, "implausible feature totals");
   c->n_qpl = npl;
   c->n_qpt = npt;
   c->n_sel = nsel;
@@ -1539,6 +1545,15 @@ void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_cou
     out->point = npt;
     out->planar_selected = nsel;
   }
+}
+
+void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
+                 const std::function<void()>& while_waiting) {
+  c->h_u32.ensure(8);
+  const uint32_t seq = next_flag(c);
+  const ExLaunch L = extract_launch(c, d_scan, R, C, c->stream, c->h_u32.p, c->h_u32.d, c->h_flag.p, c->h_flag.d, seq);
+  if (while_waiting) while_waiting();
+  extract_collect(c, L, out);
 }
 
 }  // namespace fmx

@@ -289,6 +289,7 @@ void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const
   c->have_qo = false;
 }
 
+void pf_drop(fmx_ctx* c);
 void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out,
                 const std::function<void()>& while_waiting = nullptr) {
   const auto& E = c->P.extraction;
@@ -299,6 +300,7 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
                                       " != " + std::to_string(n));
   if (C > 4096 || C < 2 * E.neighbor_points + 2 || E.num_sectors == 0 || E.num_sectors > C)
     throw StatusError(FMX_E_INVAL, "unsupported scan geometry (columns must be <= 4096)");
+  pf_drop(c);  // a queued extraction shares the scratch buffers
   const float4* d;
   if (on_dev) {
     d = reinterpret_cast<const float4*>(xyzw);
@@ -312,6 +314,72 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
   c->have_queries = true;
   c->have_match = false;
   c->have_qo = false;
+}
+
+// ---- pipelined extraction (fmx_next_scan)
+// Exchange the current query set (+ planar mask) with the second one.
+void swap_query_set(fmx_ctx* c) {
+  using std::swap;
+  swap(c->q_pl_pos, c->nq_pl_pos); swap(c->q_pl_nrm, c->nq_pl_nrm); swap(c->q_pt_pos, c->nq_pt_pos);
+  swap(c->q_pl_idx, c->nq_pl_idx); swap(c->q_pt_idx, c->nq_pt_idx); swap(c->planar_mask, c->n_planar_mask);
+}
+// Discard a queued extraction of an announced scan (its buffers are then free again).
+void pf_drop(fmx_ctx* c) {
+  if (c->pf_launched) {
+    FMX_HIP(hipStreamSynchronize(c->side));
+    ++c->pf_dropped;
+  }
+  c->pf_launched = false;
+  c->pf_ptr = nullptr;
+}
+// Queue the extraction of the announced scan on the side stream, into the second
+// query set, behind everything queued on the context stream so far (the current scan's
+// extraction and its first match, which read the current set).  Its results are not
+// read until the register_scan of that scan (pf_take).
+void pf_launch(fmx_ctx* c) {
+  if (!c->ann_ptr || c->pf_launched) return;
+  const auto& E = c->P.extraction;
+  const float4* d = reinterpret_cast<const float4*>(c->ann_ptr);
+  c->h_pf.ensure(8);
+  if (c->pf_seq == 0) c->h_pf.p[4] = 0;
+  FMX_HIP(hipEventRecord(c->ev_pf_fork, c->stream));
+  FMX_HIP(hipStreamWaitEvent(c->side, c->ev_pf_fork, 0));
+  swap_query_set(c);
+  try {
+    const uint32_t seq = ++c->pf_seq;
+    c->pf_L = extract_launch(c, d, (int)E.num_rows, (int)E.num_columns, c->side, c->h_pf.p, c->h_pf.d, c->h_pf.p + 4,
+                             c->h_pf.d + 4, seq);
+  } catch (...) {
+    swap_query_set(c);
+    throw;
+  }
+  swap_query_set(c);
+  FMX_HIP(hipEventRecord(c->ev_pf, c->side));
+  c->pf_launched = true;
+  c->pf_ptr = c->ann_ptr;
+  c->pf_n = c->ann_n;
+  c->ann_ptr = nullptr;
+}
+// register_scan(scan): true if `scan` is the one whose extraction was queued; its query
+// set becomes current (the context stream waits for its kernels) and its totals are
+// collected.  Any other scan drops the queued extraction.
+bool pf_take(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, uint64_t scan, fmx_feature_counts* out) {
+  if (!c->pf_launched) return false;
+  if (!on_dev || xyzw != c->pf_ptr || n != c->pf_n) {
+    pf_drop(c);
+    return false;
+  }
+  c->pf_launched = false;
+  c->pf_ptr = nullptr;
+  swap_query_set(c);
+  FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_pf, 0));
+  extract_collect(c, c->pf_L, out);
+  ++c->pf_used;
+  c->q_scan = scan;
+  c->have_queries = true;
+  c->have_match = false;
+  c->have_qo = false;
+  return true;
 }
 
 }  // namespace
@@ -559,7 +627,7 @@ void swap_match_set(fmx_ctx* c) {
 // instead of matching again; results are bit-identical either way.  The speculative
 // set is not read by any queued kernel: it was swapped out at the start of this ICP
 // iteration and every kernel that read it belongs to earlier, completed iterations.
-void spec_match(fmx_ctx* c, const double* pose_j) {
+void spec_match(fmx_ctx* c, const double* pose_j, bool first = false) {
   const fmx_params& P = c->P;
   swap_match_set(c);
   try {
@@ -571,13 +639,15 @@ void spec_match(fmx_ctx* c, const double* pose_j) {
   swap_match_set(c);
   std::memcpy(c->spec_pose, pose_j, sizeof(c->spec_pose));
   c->spec_valid = true;
-  ++c->spec_launched;
+  c->spec_first = first;
+  if (!first) ++c->spec_launched;
 }
 bool use_spec_match(fmx_ctx* c, const double* pose_j) {
   if (!c->spec_valid || std::memcmp(c->spec_pose, pose_j, sizeof(c->spec_pose)) != 0) return false;
   swap_match_set(c);
   c->spec_valid = false;
-  ++c->spec_hits;
+  if (!c->spec_first) ++c->spec_hits;
+  c->spec_first = false;
   return true;
 }
 
@@ -607,6 +677,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     const Pose before = e.values.at(j);
     if (!use_spec_match(c, before.m)) run_match(c, before.m, P.max_dist_matching, P.min_dist_map, true);  // pair-major
     c->spec_valid = false;
+    if (it == 0) pf_launch(c);  // the announced next scan's extraction, behind this match
     // get_graph(true): the current scan's K pairs (empty ones linearize to zero)
     g.pairs.clear();
     for (uint32_t k = 0; k < c->K; ++k) g.pairs.push_back({slot.at(c->map_scans[k]), slot.at(j)});
@@ -884,7 +955,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
                                       " != " + std::to_string(n));
   const uint64_t j = e.init ? e.scan + 1 : 0;
   const uint64_t waits0 = c->host_waits;
-  const uint64_t spec0 = c->spec_launched, hits0 = c->spec_hits;
+  const uint64_t spec0 = c->spec_launched, hits0 = c->spec_hits, pf0 = c->pf_used;
   c->spec_valid = false;  // a new map and query set: no speculation carries over
   // Host work that only needs the estimator state runs while this scan's extraction
   // kernels execute: the previous scan's deferred tail (keyscan step +
@@ -923,26 +994,39 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   // idle CUs, and its host launch cost hides behind the extraction wait).
   fmx_feature_counts fc{};
   FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
+  auto map_inputs = [&] {
+    prepare();
+    const bool spec_ok = e.spec_map && e.spec_map_scans == scans && e.spec_map_poses.size() == poses.size() &&
+                         std::memcmp(e.spec_map_poses.data(), poses.data(), poses.size() * sizeof(double)) == 0;
+    if (e.spec_map) ++(spec_ok ? c->spec_map_hits : c->spec_map_misses);
+    map_spec_used = spec_ok;
+    if (!spec_ok) {
+      HostScope hs_map(3);
+      // a discarded speculative build may still be reading the pinned pose staging
+      // buffer this build rewrites: drain it first (misses are rare)
+      if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));
+      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
+      FMX_HIP(hipEventRecord(c->ev_join, c->side));
+    }
+    e.spec_map = false;
+  };
   {
     HostScope hs_ex(2);
-    do_extract(c, xyzw, n, j, on_dev, &fc, [&] {
-      prepare();
-      const bool spec_ok = e.spec_map && e.spec_map_scans == scans && e.spec_map_poses.size() == poses.size() &&
-                           std::memcmp(e.spec_map_poses.data(), poses.data(), poses.size() * sizeof(double)) == 0;
-      if (e.spec_map) ++(spec_ok ? c->spec_map_hits : c->spec_map_misses);
-      map_spec_used = spec_ok;
-      if (!spec_ok) {
-        HostScope hs_map(3);
-        // a discarded speculative build may still be reading the pinned pose staging
-        // buffer this build rewrites: drain it first (misses are rare)
-        if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));
-        FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-        run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
-        FMX_HIP(hipEventRecord(c->ev_join, c->side));
-      }
-      e.spec_map = false;
+    if (pf_take(c, xyzw, n, on_dev, j, &fc)) {
+      // pipelined: the features were extracted during the previous registration.  The
+      // first ICP match (at the prediction) is queued before the host's finish() work,
+      // which then overlaps it; the ICP loop takes it as a speculative match.
+      map_inputs();
+      FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      if (!P.disable_smoothing) spec_match(c, e.values.at(j).m, true);
       finish();
-    });
+    } else {
+      do_extract(c, xyzw, n, j, on_dev, &fc, [&] {
+        map_inputs();
+        finish();
+      });
+    }
   }
   FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   HostScope* hs_icp = new HostScope(4);
@@ -959,6 +1043,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       ++icp;
       const Pose before = e.values.at(j);
       run_match(c, before.m, P.max_dist_matching, P.min_dist_map, false);  // query order
+      if (it == 0) pf_launch(c);  // the announced next scan's extraction, behind this match
       int li = 0;
       const Pose after = lm.optimize(before, &li);
       lm_it += li;
@@ -1008,6 +1093,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[9] = c->spec_launched - spec0;
   c->stats[10] = c->spec_hits - hits0;
   c->stats[11] = map_spec_used ? 1 : 0;
+  c->stats[12] = c->pf_used - pf0;
   if (out) *out = fc;
 }
 
@@ -1068,6 +1154,8 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     FMX_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_lo));
     FMX_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FMX_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    FMX_HIP(hipEventCreateWithFlags(&c->ev_pf, hipEventDisableTiming));
+    FMX_HIP(hipEventCreateWithFlags(&c->ev_pf_fork, hipEventDisableTiming));
     const uint64_t cap = p->keypoint_pool_capacity ? p->keypoint_pool_capacity : (4u << 20);
     c->pool[0].planar = true;
     c->pool[1].planar = false;
@@ -1101,6 +1189,8 @@ void fmx_destroy(fmx_ctx* c) {
   c->row_counts.release(); c->row_ok.release(); c->row_off.release(); c->closest.release();
   c->nrm_slots.release(); c->scan_scratch.release(); c->dev_u32.release(); c->h_u32.release();
   c->q_pl_pos.release(); c->q_pl_nrm.release(); c->q_pt_pos.release(); c->q_pl_idx.release(); c->q_pt_idx.release();
+  c->nq_pl_pos.release(); c->nq_pl_nrm.release(); c->nq_pt_pos.release(); c->nq_pl_idx.release(); c->nq_pt_idx.release();
+  c->n_planar_mask.release(); c->h_pf.release();
   for (int t = 0; t < 2; ++t) {
     c->pool[t].pos.release(); c->pool[t].nrm.release();
     c->segs[t].release(); c->h_segs[t].release();
@@ -1137,6 +1227,8 @@ void fmx_destroy(fmx_ctx* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->ev_pf) (void)hipEventDestroy(c->ev_pf);
+  if (c->ev_pf_fork) (void)hipEventDestroy(c->ev_pf_fork);
   delete c;
 }
 
@@ -1334,6 +1426,22 @@ fmx_status fmx_comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank
     if (!id) throw StatusError(FMX_E_INVAL, "null id");
     FMX_HIP(hipStreamSynchronize(c->stream));
     comm_init(c, id, nranks, rank);
+  });
+}
+
+fmx_status fmx_next_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev) {
+  return guard(c, [&] {
+    if (!xyzw) {  // withdraw the announcement
+      c->ann_ptr = nullptr;
+      return;
+    }
+    const auto& E = c->P.extraction;
+    if (!on_dev) throw StatusError(FMX_E_INVAL, "fmx_next_scan: pipelined extraction needs a device-resident scan");
+    if (n != (size_t)E.num_rows * (size_t)E.num_columns)
+      throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " +
+                                        std::to_string((size_t)E.num_rows * E.num_columns) + " != " + std::to_string(n));
+    c->ann_ptr = xyzw;
+    c->ann_n = n;
   });
 }
 

@@ -248,9 +248,19 @@ struct MatchSet {
   uint32_t ins_tot[2] = {0, 0};
 };
 
+// An extraction launched on stream `st`: its totals and completion word go to mapped
+// pinned memory (tot / flag); extract_collect waits for them.
+struct ExLaunch {
+  uint32_t seq = 0;
+  const volatile uint32_t* flag = nullptr;
+  const uint32_t* tot = nullptr;
+  size_t max_pl = 0, max_pt = 0;
+  hipStream_t st = nullptr;
+};
+
 }  // namespace fmx
 
-constexpr int kStatsN = 12;  // fmx_last_stats entries
+constexpr int kStatsN = 13;  // fmx_last_stats entries
 
 struct fmx_ctx {
   fmx_params P{};
@@ -278,6 +288,23 @@ struct fmx_ctx {
   fmx::DBuf<float4> q_pl_pos, q_pl_nrm, q_pt_pos;
   fmx::DBuf<uint32_t> q_pl_idx, q_pt_idx;
   bool have_queries = false;
+
+  // ---- pipelined extraction (fmx_next_scan): the scan after the one being registered
+  // is extracted on the side stream, during this registration, into a second query set
+  // (+ planar mask); the next register_scan swaps it in instead of extracting
+  fmx::DBuf<float4> nq_pl_pos, nq_pl_nrm, nq_pt_pos;
+  fmx::DBuf<uint32_t> nq_pl_idx, nq_pt_idx;
+  fmx::DBuf<uint8_t> n_planar_mask;
+  const float* ann_ptr = nullptr;   // announced by fmx_next_scan (device pointer), its size
+  size_t ann_n = 0;
+  const float* pf_ptr = nullptr;    // the scan whose extraction is queued on the side stream
+  size_t pf_n = 0;
+  bool pf_launched = false;
+  fmx::ExLaunch pf_L;
+  uint32_t pf_seq = 0;              // its completion word's sequence number
+  fmx::HBuf<uint32_t> h_pf;         // pinned: [0..2] its totals, [4] its completion word
+  hipEvent_t ev_pf = nullptr, ev_pf_fork = nullptr;
+  uint64_t pf_used = 0, pf_dropped = 0;
 
   // ---- window keypoint store + maps
   fmx::Pool pool[2];
@@ -354,6 +381,7 @@ struct fmx_ctx {
   fmx::MatchSet spec;
   hipStream_t match_stream = nullptr;  // run_match / run_pair_scatter stream override
   bool spec_valid = false;
+  bool spec_first = false;  // the speculative set holds the scan's first match (not a speculation)
   double spec_pose[12] = {};
   uint64_t spec_launched = 0, spec_hits = 0;
   uint64_t spec_map_hits = 0, spec_map_misses = 0;  // speculative map builds kept / rebuilt
@@ -499,13 +527,13 @@ inline void stream_wait(fmx_ctx* c) {
 // seq).  Cheaper than a stream round trip: the host resumes as soon as the word
 // lands, before the kernel retires.  A stream that went idle without the word, or a
 // stream error, throws (no silent hang).
-inline void wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq) {
+inline void wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq, hipStream_t st = nullptr) {
   HostScope hs(1);
   ++c->host_waits;
   for (uint32_t spins = 1;; ++spins) {
     if (*f == seq) break;
     if ((spins & 0x3FFF) == 0) {
-      const hipError_t e = hipStreamQuery(c->stream);
+      const hipError_t e = hipStreamQuery(st ? st : c->stream);
       if (e == hipSuccess) {
         if (*f == seq) break;
         throw HipError("kernel completed without publishing its result flag");
@@ -537,6 +565,9 @@ namespace g8 { FMX_VM_DECLS }
 namespace g4 { FMX_VM_DECLS }
 #undef FMX_VM_DECLS
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
+ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
+                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq);
+void extract_collect(fmx_ctx* c, const ExLaunch& L, fmx_feature_counts* out);
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
                  const std::function<void()>& while_waiting = nullptr);
 // st: stream to build on (default the context stream; register_scan uses the side

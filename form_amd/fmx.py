@@ -78,7 +78,8 @@ EXPORTED = [
     "fmx_extract", "fmx_extract_download", "fmx_set_queries", "fmx_set_queries_device", "fmx_keypoints_add",
     "fmx_keypoints_add_device",
     "fmx_keypoints_remove", "fmx_map_build", "fmx_match", "fmx_match_download", "fmx_map_insert",
-    "fmx_corr_set", "fmx_linearize", "fmx_error", "fmx_linearize_matched", "fmx_register_scan", "fmx_current_pose",
+    "fmx_corr_set", "fmx_linearize", "fmx_error", "fmx_linearize_matched", "fmx_register_scan", "fmx_next_scan",
+    "fmx_current_pose",
     "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
     "fmx_profile_name", "fmx_profile_read", "fmx_sync", "fmx_comm_unique_id", "fmx_comm_init",
 ]
@@ -310,6 +311,20 @@ class Context:
         self.n_planar, self.n_point = c.planar, c.point
         return c.planar, c.point
 
+    def next_scan(self, scan):
+        """fmx_next_scan: announce the scan that follows the one the next register_scan
+        receives (a contiguous (N, 4) float32 CUDA tensor, left unchanged until its own
+        register_scan); that call extracts it while registering.  None withdraws."""
+        if scan is None:
+            self._chk(self._L.fmx_next_scan(self.h, None, C.c_size_t(0), C.c_int(0)))
+            return
+        on_dev, ptr, n, keep = _scan_ptr(scan)
+        if not on_dev or keep is not scan:
+            raise ValueError("next_scan needs a contiguous (N, 4) float32 CUDA tensor")
+        self._chk(self._L.fmx_next_scan(self.h, ptr, C.c_size_t(n), C.c_int(1)))
+        # the tensor must outlive the extraction queued for it
+        self._pf_keep = (getattr(self, "_pf_keep", (None, None))[1], scan)
+
     def current_pose(self) -> np.ndarray:
         T = np.zeros(12)
         self._chk(self._L.fmx_current_pose(self.h, _p(T)))
@@ -317,7 +332,8 @@ class Context:
 
     def last_stats(self) -> dict:
         keys = ["icp_iters", "lm_iters", "matched_planar", "matched_point", "map_planar", "map_point",
-                "linearizations", "map_scans", "host_waits", "spec_matches", "spec_hits", "spec_map"]
+                "linearizations", "map_scans", "host_waits", "spec_matches", "spec_hits", "spec_map",
+                "pipelined"]
         s = np.zeros(len(keys), np.uint64)
         self._chk(self._L.fmx_last_stats(self.h, _p(s), C.c_int(len(keys))))
         return {k: int(v) for k, v in zip(keys, s)}

@@ -197,6 +197,15 @@ fmx_status fmx_comm_init(fmx_ctx* ctx, const uint8_t id[128], int nranks, int ra
  * 235-250).  Every FeatureFactor linearization runs on the device. */
 fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, int src_on_device,
                              fmx_feature_counts* out);
+/* Pipelined extraction (no reference counterpart; an fmx throughput option).
+ * Announces the scan that will FOLLOW the one passed to the next fmx_register_scan:
+ * that call extracts it (FeatureExtractor::extract, extraction.tpp:29-132) on a side
+ * stream while it registers its own scan, and the register_scan of this scan then
+ * skips its extraction.  Results are identical either way: extraction depends only on
+ * the scan.  The scan must be device-resident (src_on_device = 1, else FMX_E_INVAL)
+ * and unchanged until its own fmx_register_scan returns; registering a different
+ * pointer discards the queued extraction.  xyzw = NULL withdraws the announcement. */
+fmx_status fmx_next_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, int src_on_device);
 /* Estimator::current_lidar_estimate (form/form.hpp:79). */
 fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
 
@@ -206,7 +215,8 @@ fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
  * spec_matches (speculative matches launched at LM-trial poses), spec_hits (ICP
  * iterations that used one instead of matching), spec_map (1 when the scan's map was
  * the one built speculatively during the previous scan's final LM, 0 when built at
- * the start of this scan)};
+ * the start of this scan), pipelined (1 when the scan's features were extracted
+ * during the previous registration, fmx_next_scan)};
  * entries past the known ones read 0. */
 fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t* stats, int n);
 /* Work of the last fmx_match (counted by the kernel, available while profiling is

@@ -1,0 +1,96 @@
+"""Pipelined extraction (fmx_next_scan): register_scan(j) also extracts scan j+1 on the
+side stream.  Extraction depends only on the scan, so a pipelined stream must give the
+same features and the same poses, bit for bit, as a sequential one — and as the oracle
+(1e-6).  Also: a registered scan that is not the announced one drops the queued
+extraction; announcing a host array is refused."""
+import numpy as np
+import pytest
+
+from form_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(fmx, p, single=False, window=None):
+    kw = {}
+    if window:
+        kw = dict(max_num_recent_scans=window[0], max_num_keyscans=window[1])
+    return fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**p), disable_smoothing=single,
+                                           **kw))
+
+
+def _stream(config, n):
+    world = synth.World()
+    return [synth.make_scan(config, k, world=world)[0].to("cuda:0") for k in range(n)]
+
+
+@pytest.mark.parametrize("single,n,window", [(True, 8, None), (False, 8, None), (False, 20, (4, 3))])
+def test_pipelined_stream_matches_oracle(fmx_mod, oracle, single, n, window):
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    scans = _stream("tiny", n)
+    ctx = _ctx(fmx_mod, p, single, window)
+    prm = oracle.default_params(p)
+    prm.disable_smoothing = int(single)
+    if window:
+        prm.max_num_recent_scans, prm.max_num_keyscans = window
+    oest = oracle.Estimator(prm)
+    for k in range(n):
+        if k + 1 < n:
+            ctx.next_scan(scans[k + 1])
+        ctx.register_scan(scans[k])
+        assert ctx.last_stats()["pipelined"] == (1 if k > 0 else 0)
+        To, _, _ = oest.register_scan(scans[k].cpu().numpy())
+        assert np.abs(ctx.current_pose() - To).max() < 1e-6, k
+
+
+def test_pipelined_c4_equals_sequential(fmx_mod):
+    """A 24-scan C4 stream (window filling, keyscan marginalizations): features after
+    every registration and every pose are identical with and without pipelining."""
+    geo = synth.GEOMETRIES["c4"]
+    p = synth.default_params(geo)
+    n = 24
+    scans = _stream("c4", n)
+    seq, pip = _ctx(fmx_mod, p), _ctx(fmx_mod, p)
+    for k in range(n):
+        seq.register_scan(scans[k])
+        if k + 1 < n:
+            pip.next_scan(scans[k + 1])
+        pip.register_scan(scans[k])
+        assert np.array_equal(seq.current_pose(), pip.current_pose()), k
+        a, b = seq.extract_download(), pip.extract_download()
+        for key in ("planar_index", "point_index", "planar", "point"):
+            assert np.array_equal(a[key], b[key]), (k, key)
+        assert pip.last_stats()["pipelined"] == (1 if k > 0 else 0)
+    assert seq.last_stats()["icp_iters"] == pip.last_stats()["icp_iters"]
+
+
+def test_unannounced_scan_drops_queued_extraction(fmx_mod, oracle):
+    """Announce scan 2 but register scan 3 instead at that step: the queued extraction is
+    discarded and scan 3 is extracted in its own call; then pipelining resumes."""
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    scans = _stream("tiny", 6)
+    order = [0, 1, 3, 4, 5]
+    ctx = _ctx(fmx_mod, p)
+    oest = oracle.Estimator(oracle.default_params(p))
+    for i, k in enumerate(order):
+        nxt = 2 if k == 1 else (order[i + 1] if i + 1 < len(order) else None)
+        if nxt is not None:
+            ctx.next_scan(scans[nxt])
+        ctx.register_scan(scans[k])
+        expect = 0 if i == 0 or k == 3 else 1
+        assert ctx.last_stats()["pipelined"] == expect, (k, ctx.last_stats())
+        To, _, _ = oest.register_scan(scans[k].cpu().numpy())
+        assert np.abs(ctx.current_pose() - To).max() < 1e-6, k
+
+
+def test_next_scan_rejects_host_array(fmx_mod):
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    ctx = _ctx(fmx_mod, p)
+    s = synth.make_scan("tiny", 0)[0]
+    with pytest.raises(ValueError):
+        ctx.next_scan(s)  # a CPU tensor
+    with pytest.raises(Exception):
+        ctx.next_scan(s[:-1].to("cuda:0").contiguous())  # wrong size
