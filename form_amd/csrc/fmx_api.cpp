@@ -613,6 +613,7 @@ void swap_match_set(fmx_ctx* c) {
   swap(c->have_match, S.have_match); swap(c->have_corr, S.have_corr); swap(c->scatter_pending, S.scatter_pending);
   swap(c->counts_pending, S.counts_pending); swap(c->have_qo, S.have_qo); swap(c->ld_pl, S.ld_pl);
   swap(c->ld_pt, S.ld_pt); swap(c->max_chunks, S.max_chunks); swap(c->work_blocks, S.work_blocks);
+  swap(c->work_copied, S.work_copied);
   swap(c->match_nb_pl, S.match_nb_pl); swap(c->match_nb, S.match_nb); swap(c->n_qo, S.n_qo);
   swap(c->match_group, S.match_group); swap(c->ps, S.ps); swap(c->rows_pl, S.rows_pl); swap(c->rows_pt, S.rows_pt);
   swap(c->cnt_pl, S.cnt_pl); swap(c->cnt_pt, S.cnt_pt); swap(c->last_probes, S.last_probes);

@@ -240,6 +240,7 @@ struct MatchSet {
   bool have_match = false, have_corr = false, scatter_pending = false, counts_pending = false, have_qo = false;
   size_t ld_pl = 0, ld_pt = 0;
   uint32_t max_chunks = 0, work_blocks = 0, match_nb_pl = 0, match_nb = 0, n_qo = 0;
+  bool work_copied = false;
   int match_group = 8;
   PairScatter ps;
   uint64_t rows_pl = 0, rows_pt = 0;
@@ -353,6 +354,7 @@ struct fmx_ctx {
   fmx::DBuf<uint32_t> work;                     // match work counters per block (probes, candidates)
   fmx::HBuf<uint32_t> h_work;
   uint32_t work_blocks = 0;
+  bool work_copied = false;  // h_work holds the last match's counters (profiling was on)
   double last_probes = 0, last_cands = 0;
   bool counts_pending = false;
   bool nrm_attr_set = false;

@@ -1562,6 +1562,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     if (!defer_scatter) run_pair_scatter(c);
   }
   // per-pair counts reach pinned host memory from k_pair_base; consumed at the next sync
+  c->work_copied = c->prof.on;
   if (c->prof.on) {  // per-block work counters, only needed for the profile's byte model
     c->h_work.ensure(kWorkWords * (size_t)nb + 8);
     if (nb)
@@ -1588,7 +1589,7 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
     c->rows_pt += c->cnt_pt[k];
   }
   (void)K;
-  if (c->prof.on) {
+  if (c->work_copied) {  // (a match made before profiling was switched on has none)
     double tp = 0, tc = 0;
     for (uint32_t b = 0; b < c->work_blocks; ++b) {
       tp += c->h_work.p[kWorkWords * b];
