@@ -338,6 +338,7 @@ void pf_drop(fmx_ctx* c) {
 // read until the register_scan of that scan (pf_take).
 void pf_launch(fmx_ctx* c) {
   if (!c->ann_ptr || c->pf_launched) return;
+  HostScope hs(14);
   const auto& E = c->P.extraction;
   const float4* d = reinterpret_cast<const float4*>(c->ann_ptr);
   c->h_pf.ensure(8);
@@ -944,6 +945,17 @@ void finish_tail(fmx_ctx* c) {
 
 void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
   HostScope hs_all(0);
+  // host time spent outside register_scan since the previous call returned (diagnostic)
+  static double last_ret = 0.0;
+  struct RetStamp {
+    ~RetStamp() {
+      if (host_timing().on) last_ret = now_s();
+    }
+  } ret_stamp;
+  if (host_timing().on && last_ret > 0.0) {
+    host_timing().t[15] += now_s() - last_ret;
+    host_timing().n[15]++;
+  }
   if (!c->est) {
     c->est = new fmx_ctx::Est();
     c->est->ks.P = &c->P;
