@@ -326,16 +326,18 @@ void swap_query_set(fmx_ctx* c) {
 // Discard a queued extraction of an announced scan (its buffers are then free again).
 void pf_drop(fmx_ctx* c) {
   if (c->pf_launched) {
-    FMX_HIP(hipStreamSynchronize(c->side));
+    FMX_HIP(hipStreamSynchronize(c->side2));
     ++c->pf_dropped;
   }
   c->pf_launched = false;
   c->pf_ptr = nullptr;
 }
-// Queue the extraction of the announced scan on the side stream, into the second
+// Queue the extraction of the announced scan on its own low-priority stream (side2:
+// the speculative map build on `side` is not serialized behind it), into the second
 // query set, behind everything queued on the context stream so far (the current scan's
 // extraction and its first match, which read the current set).  Its results are not
-// read until the register_scan of that scan (pf_take).
+// read until the register_scan of that scan (pf_take).  Placement measured: here or at
+// the start of the full LM (optimize(false)) is the same within the box-to-box noise.
 void pf_launch(fmx_ctx* c) {
   if (!c->ann_ptr || c->pf_launched) return;
   HostScope hs(14);
@@ -344,18 +346,18 @@ void pf_launch(fmx_ctx* c) {
   c->h_pf.ensure(8);
   if (c->pf_seq == 0) c->h_pf.p[4] = 0;
   FMX_HIP(hipEventRecord(c->ev_pf_fork, c->stream));
-  FMX_HIP(hipStreamWaitEvent(c->side, c->ev_pf_fork, 0));
+  FMX_HIP(hipStreamWaitEvent(c->side2, c->ev_pf_fork, 0));
   swap_query_set(c);
   try {
     const uint32_t seq = ++c->pf_seq;
-    c->pf_L = extract_launch(c, d, (int)E.num_rows, (int)E.num_columns, c->side, c->h_pf.p, c->h_pf.d, c->h_pf.p + 4,
+    c->pf_L = extract_launch(c, d, (int)E.num_rows, (int)E.num_columns, c->side2, c->h_pf.p, c->h_pf.d, c->h_pf.p + 4,
                              c->h_pf.d + 4, seq);
   } catch (...) {
     swap_query_set(c);
     throw;
   }
   swap_query_set(c);
-  FMX_HIP(hipEventRecord(c->ev_pf, c->side));
+  FMX_HIP(hipEventRecord(c->ev_pf, c->side2));
   c->pf_launched = true;
   c->pf_ptr = c->ann_ptr;
   c->pf_n = c->ann_n;
@@ -1165,6 +1167,7 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     FMX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     FMX_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
     FMX_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_lo));
+    FMX_HIP(hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, prio_lo));
     FMX_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FMX_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     FMX_HIP(hipEventCreateWithFlags(&c->ev_pf, hipEventDisableTiming));
@@ -1189,6 +1192,7 @@ void fmx_destroy(fmx_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->side2) (void)hipStreamSynchronize(c->side2);
   for (auto& e : c->prof.free_events) (void)hipEventDestroy(e);
   for (auto& pe : c->prof.pending) {
     (void)hipEventDestroy(pe.second.first);
@@ -1238,6 +1242,7 @@ void fmx_destroy(fmx_ctx* c) {
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->side2) (void)hipStreamDestroy(c->side2);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_pf) (void)hipEventDestroy(c->ev_pf);

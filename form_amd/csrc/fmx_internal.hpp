@@ -268,6 +268,7 @@ struct fmx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;                    // map build, overlapped with extraction
+  hipStream_t side2 = nullptr;                   // pipelined extraction of the announced next scan
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // stream -> side -> stream ordering
   std::string err;
   fmx::Prof prof;
