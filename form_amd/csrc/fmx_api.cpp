@@ -22,35 +22,36 @@ namespace fmx {
 
 // ---------------------------------------------------------------- match-path dispatch
 // Lanes per query of k_match: 8 while the whole query set is resident at once (a
-// C4 scan's ~4e4 queries: more lanes shorten each query's chain of dependent loads),
-// 4 for large sets (>= 128k queries, e.g. C5's 2M): they run in several waves of
-// blocks, so more queries per wave raise the loads in flight (C5 match 1.42 -> 1.04 ms,
-// C4 8 lanes 0.22 vs 4 lanes 0.28 ms per scan).
-#ifndef FMX_MATCH_G4_MIN
-#define FMX_MATCH_G4_MIN (128u << 10)  // queries from which 4 lanes per query are used
+// C4 scan's ~4e4 queries: more lanes shorten each query's chain of dependent loads,
+// and split the walks of dense cells), 1 for large sets (>= 128k queries, e.g. C5's 2M,
+// ~2 probes and ~2 candidates per query): they run in many waves of blocks, so more
+// queries per wave raise the loads in flight.  C5 match per launch: 4 lanes 0.55 ms,
+// 2 lanes 0.40, 1 lane 0.245 (C4: 8 lanes 0.22 vs 4 lanes 0.28 ms per scan).
+#ifndef FMX_MATCH_LARGE_MIN
+#define FMX_MATCH_LARGE_MIN (128u << 10)  // queries from which the large-set build (fmx::gl) is used
 #endif
-int match_group_for(uint64_t nq) {
-  return nq >= (uint64_t)(FMX_MATCH_G4_MIN) ? 4 : 8;
+int match_group_for(uint64_t nq, uint32_t K) {
+  return nq >= (uint64_t)(FMX_MATCH_LARGE_MIN) && K <= kMatchTileMaxPairs ? 1 : 8;
 }
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, hipStream_t st) {
   g8::run_map_build(c, scans, poses34, w, st);  // the same build in both variants
 }
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
-  c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt);
-  if (c->match_group == 4) g4::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
+  c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K);
+  if (c->match_group != 8) gl::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
   else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
 }
 void run_pair_scatter(fmx_ctx* c) {
-  if (c->match_group == 4) g4::run_pair_scatter(c);
+  if (c->match_group != 8) gl::run_pair_scatter(c);
   else g8::run_pair_scatter(c);
 }
 void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
-  if (c->match_group == 4) g4::run_insert(c, scan, n_inserted);
+  if (c->match_group != 8) gl::run_insert(c, scan, n_inserted);
   else g8::run_insert(c, scan, n_inserted);
 }
 void match_counts_fetch(fmx_ctx* c, bool wait) {
-  if (c->match_group == 4) g4::match_counts_fetch(c, wait);
+  if (c->match_group != 8) gl::match_counts_fetch(c, wait);
   else g8::match_counts_fetch(c, wait);
 }
 

@@ -343,7 +343,7 @@ struct fmx_ctx {
   fmx::DBuf<fmx::Chunk> chunks;
   fmx::DBuf<uint32_t> n_chunks;
   uint32_t max_chunks = 0;
-  int match_group = 8;  // lanes per query of the last run_match (voxelmap.hip g8 / g4)
+  int match_group = 8;  // lanes per query of the last run_match (voxelmap.hip g8 / gl)
   bool have_corr = false;
   fmx::PairScatter ps;          // the last sorted match's scatter (voxelmap.hip)
   bool scatter_pending = false; // ... not yet launched (deferred by fmx_match)
@@ -554,8 +554,8 @@ inline uint32_t next_flag(fmx_ctx* c) {
   }
   return ++c->flag_seq;
 }
-// voxelmap.hip is built twice: 8 lanes per query (fmx::g8, per-scan query sets) and 4
-// (fmx::g4, large query sets: more queries in flight per wave); the fmx:: entry points
+// voxelmap.hip is built twice: 8 lanes per query (fmx::g8, per-scan query sets) and 1
+// (fmx::gl, large query sets: more queries in flight per wave); the fmx:: entry points
 // below dispatch on c->match_group, chosen by run_match.
 #define FMX_VM_DECLS                                                                                   \
   void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, \
@@ -565,8 +565,12 @@ inline uint32_t next_flag(fmx_ctx* c) {
   void run_pair_scatter(fmx_ctx* c);                                                                 \
   void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);                                  \
   void match_counts_fetch(fmx_ctx* c, bool wait = true);
+// Windows of at most this many map scans (pairs) use the tiled pair sort; wider ones a
+// per-match-block histogram whose scatter ranks within one wave, so they take the g8
+// build (32 queries per block) whatever the query count.
+constexpr uint32_t kMatchTileMaxPairs = 256;
 namespace g8 { FMX_VM_DECLS }
-namespace g4 { FMX_VM_DECLS }
+namespace gl { FMX_VM_DECLS }
 #undef FMX_VM_DECLS
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,

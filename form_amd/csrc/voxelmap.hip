@@ -55,7 +55,7 @@
 #endif
 
 namespace fmx {
-// This file is compiled twice (Makefile): FMX_MATCH_GROUP 8 -> fmx::g8 and 4 -> fmx::g4;
+// This file is compiled twice (Makefile): FMX_MATCH_GROUP 8 -> fmx::g8 and 1 -> fmx::gl;
 // run_match picks one per launch (fmx_api.cpp, match_group_for).
 namespace FMX_VM_NS {
 namespace {
@@ -480,7 +480,7 @@ constexpr int kSmallCell = FMX_SMALL_CELL;  // neighbour cells with at most this
 // k_pair_scatter_t block; the match counts matches per (type, pair, tile).
 constexpr int kTileBlocks = 1024 / kQPB;
 constexpr int kTileQ = kTileBlocks * kQPB;  // 1024
-constexpr int kTileMaxPairs = 256;          // LDS bound of the tiled path (wider windows: per-block path)
+constexpr int kTileMaxPairs = (int)kMatchTileMaxPairs;  // LDS bound of the tiled path (wider windows: per-block path)
 constexpr int kWorkWords = 8;               // per-block match work / diagnostic words
 
 // Outputs of the tiled pair sort's last-block pass (consumed by later launches).
@@ -693,11 +693,12 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
           best_i = oi;
         }
       };
-      static_assert(kGroup == 4 || kGroup == 8 || kGroup == 16, "DPP reduction assumes 4-, 8- or 16-lane groups");
+      static_assert(kGroup == 1 || kGroup == 2 || kGroup == 4 || kGroup == 8 || kGroup == 16,
+                    "DPP reduction assumes 1-, 2-, 4-, 8- or 16-lane groups");
       if constexpr (kGroup == 16) step(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
       if constexpr (kGroup >= 8) step(std::integral_constant<int, 0x141>{});  // row_half_mirror
-      step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
-      step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+      if constexpr (kGroup >= 4) step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+      if constexpr (kGroup >= 2) step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
     };
     // Records of one cell, walked by the whole group (group-uniform arguments).  A
     // dense cell (k_map_dense) starts with a header of its 64 sub-cell ends: the
@@ -1126,7 +1127,8 @@ __global__ __launch_bounds__(1024) void k_pair_base(int K, uint32_t nb_pl, uint3
 }
 
 // Stable scatter of accepted matches into pair-major SoA correspondences:
-// one (partial) wave per match block (kQPB queries), rank by ballot within the wave.
+// one (partial) wave per match block (kQPB queries), rank by ballot within the wave
+// (only the g8 build runs it: match_group_for).
 __global__ __launch_bounds__(kQPB) void k_pair_scatter(uint32_t nq_pl, uint32_t nq_pt, uint32_t nb_pl, int K,
                                                      const int32_t* __restrict__ m_pair,
                                                      const double4* __restrict__ m_pi,
@@ -1264,8 +1266,18 @@ __global__ __launch_bounds__(kQPB) void k_insert(InsArgs a) {
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
   const bool f = qi < nq && a.ins[planar ? qi : a.nq_pl + qi] != 0;
   const uint64_t m = __ballot(f);
+  // a match block of several waves (large-set build): earlier waves' counts first
+  constexpr int kW = (kQPB + kWave - 1) / kWave;
+  uint32_t wbase = 0;
+  if constexpr (kW > 1) {
+    __shared__ uint32_t s_w[kW];
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    for (int i = 0; i < w; ++i) wbase += s_w[i];
+  }
   if (!f) return;
-  const uint32_t o = a.ins_off[b] + (uint32_t)__popcll(m & lanemask_lt());
+  const uint32_t o = a.ins_off[b] + wbase + (uint32_t)__popcll(m & lanemask_lt());
   if (planar) {
     a.d_pl_pos[o] = a.q_pl[qi];
     a.d_pl_nrm[o] = a.q_pl_nrm[qi];
@@ -1441,6 +1453,8 @@ void run_pair_scatter(fmx_ctx* c) {
     hipLaunchKernelGGL(k_pair_scatter_t, dim3(s.ntl_pl + s.ntl_pt), dim3(kTileQ), 0, st, c->n_qpl, c->n_qpt, s.ntl_pl,
                        s.ntl_pt, s.K, c->m_pair.p, c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p,
                        c->c_pl.p, c->ld_pl, c->c_pt.p, c->ld_pt);
+  else if (kQPB > kWave)  // (match_group_for sends wide windows to the g8 build)
+    throw StatusError(FMX_E_STATE, "per-block pair scatter needs one wave per match block");
   else
     hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(kQPB), 0, st, c->n_qpl, c->n_qpt, s.nb_pl, s.K, c->m_pair.p,
                        c->m_pi.p, c->m_ni.p, c->q_pl_pos.p, c->q_pt_pos.p, c->hist_off.p, s.nb_pt, c->pair_base.p,

@@ -125,8 +125,10 @@ def test_match_matches_oracle(fmx_mod, oracle, config, subdiv, rot, trans):
 
 
 def test_match_large_query_set_matches_oracle(fmx_mod, oracle):
-    """>= 128k queries: run_match takes the 4-lanes-per-query build (fmx::g4, the C5
-    path); same bit-exact contract as the 8-lane path above."""
+    """>= 128k queries: run_match takes the large-set build (fmx::gl, one lane per
+    query and 256 queries per block: the C5 path); same bit-exact contract as the 8-lane
+    path above, and insert_matches appends exactly the oracle's insert set (the blocks
+    span four waves, each ranked after the earlier ones)."""
     feats = stream_features(oracle, "c2", 6)
     p = feats[0]["params"]
     ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p)))
@@ -170,6 +172,21 @@ def test_match_large_query_set_matches_oracle(fmx_mod, oracle):
             assert np.array_equal(got["ni"][acc_ref], ref["ni"][acc_ref])
         counts = np.bincount(ref["scan"][acc_ref].astype(np.int64), minlength=5)
         assert np.array_equal((cpl if t == 0 else cpt), counts)
+    # insert_matches (map.tpp:148-165): queries whose NN lies farther than min_dist_map
+    ins_ref = []
+    for om, Q in zip(omaps, (Qpl, Qpt)):
+        ref = om.match(Q, Tj)
+        ins_ref.append(~ref["found"] | (ref["d2"] > 0.01))
+    n_pl, n_pt = ctx.map_insert(0.1)
+    assert (n_pl, n_pt) == (int(ins_ref[0].sum()), int(ins_ref[1].sum()))
+    # every inserted keypoint landed in scan 5's range: a map of scan 5 alone (identity
+    # pose) holds exactly the inserted queries, each its own nearest neighbour (d2 = 0)
+    ctx.map_build([5], np.eye(4)[:3][None], w)
+    ctx.set_queries(Qpl, Qpt, 6)
+    ctx.match(np.eye(4)[:3], w)
+    d2 = ctx.match_download()["d2"]
+    assert np.array_equal(d2[:npl] == 0.0, ins_ref[0])
+    assert np.array_equal(d2[npl:] == 0.0, ins_ref[1])
 
 
 @pytest.mark.parametrize("single", [False, True])
