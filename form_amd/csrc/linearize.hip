@@ -68,14 +68,17 @@ struct QoRows {
 
 __global__ __launch_bounds__(kTotWaves * kWave) void k_linearize_total(
     QoRows qo, const double* __restrict__ poses, double inv, double* __restrict__ bpart, uint32_t* __restrict__ ticket,
-    double* __restrict__ out, Pose34 tjv, uint32_t* __restrict__ flag, uint32_t seq) {
+    double* __restrict__ out, Pose34 tjv, uint32_t* __restrict__ flag, uint32_t seq, uint32_t cpw) {
   constexpr int NG = 28;
   constexpr int kTotGroups = kTotWaves * kWave / NG;  // final reduction: lane groups x 28 entries
   const int w = threadIdx.x / kWave, lane = lane_id();
-  const uint32_t ch = blockIdx.x * kTotWaves + w;
   double acc[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) acc[i] = 0.0;
+  // cpw consecutive 64-row chunks per wave (large query sets: one reduce-scatter per
+  // cpw chunks instead of per chunk)
+  for (uint32_t c = 0; c < cpw; ++c) {
+  const uint32_t ch = (blockIdx.x * kTotWaves + w) * cpw + c;
   const uint32_t gq = ch * kWave + lane;
   const int32_t pair = gq < qo.nq ? qo.pair[gq] : -1;
   if (pair >= 0) {
@@ -110,6 +113,7 @@ __global__ __launch_bounds__(kTotWaves * kWave) void k_linearize_total(
       }
     }
   }
+  }  // chunks
   __shared__ double sw[kTotWaves][NG];
   __shared__ double sq[kTotGroups][NG];
   __shared__ int s_last;
@@ -235,9 +239,14 @@ namespace fmx {
 // blocks of k_linearize_total over the last query-order match (64 queries per wave)
 // (+ the partial / ticket buffers it needs; the ticket starts at 0 and the last block
 // resets it)
-static uint32_t tot_blocks(fmx_ctx* c) {
+constexpr uint32_t kTotTargetWaves = 8192;  // waves enough to fill the chip; beyond, chunks per wave grow
+static uint32_t tot_chunks_per_wave(fmx_ctx* c) {
   const uint32_t nch = (c->n_qo + kWave - 1) / kWave;
-  const uint32_t nblk = std::max<uint32_t>((nch + kTotWaves - 1) / kTotWaves, 1);
+  return std::max<uint32_t>((nch + kTotTargetWaves - 1) / kTotTargetWaves, 1);
+}
+static uint32_t tot_blocks(fmx_ctx* c) {
+  const uint32_t nch = (c->n_qo + kWave - 1) / kWave, cpw = tot_chunks_per_wave(c);
+  const uint32_t nblk = std::max<uint32_t>((nch + kTotWaves * cpw - 1) / (kTotWaves * cpw), 1);
   c->bpart.ensure((size_t)nblk * kTotLd);
   ensure_zeroed(c->ticket, 1, c->stream);
   return nblk;
@@ -272,7 +281,7 @@ void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, doubl
     // (p_i 32 B, p_j 16 B) per accepted point pair
     ProfScope ps(c->prof, PROF_LINEARIZE, 4.0 * c->n_qo + 80.0 * c->rows_pl + 48.0 * c->rows_pt, st);
     hipLaunchKernelGGL(k_linearize_total, dim3(nblk), dim3(kTotWaves * kWave), 0, st, qo_rows(c), c->map_poses_p,
-                       1.0 / sigma, c->bpart.p, c->ticket.p, dst, tjv, flag, seq);
+                       1.0 / sigma, c->bpart.p, c->ticket.p, dst, tjv, flag, seq, tot_chunks_per_wave(c));
     FMX_HIP(hipGetLastError());
   }
   if (comm) {
