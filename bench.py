@@ -267,7 +267,7 @@ def c5_register(ctx, w, max_iters=30, thr=1e-4):
     from form_amd import shard
     T = np.hstack([np.eye(3), np.zeros((3, 1))])
     for it in range(max_iters):
-        ctx.match(T, w)
+        ctx.match(T, w, counts=False)  # no wait: linearize_matched is queued behind it
         S, _ = ctx.linearize_matched(T, 0.1)
         dx = shard.gauss_newton_step(S)
         T = shard.compose(T, shard.expmap(dx))

@@ -1344,11 +1344,18 @@ fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint3
     if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
     if (!(max_dist > 0)) throw StatusError(FMX_E_INVAL, "max_dist must be > 0");
     run_match(c, pose_j, max_dist, c->P.min_dist_map, true, true);  // rows scattered when read
+    // the map's range-error word is read back once per build; with no count outputs
+    // requested the call then returns without waiting (the next consumer of the match
+    // results waits for them: fmx_linearize_matched, fmx_match_download, ...)
+    if (!c->map_err_checked) {
+      c->h_u32.ensure(8);
+      FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->map_err_p, 4, hipMemcpyDeviceToHost, c->stream));
+      FMX_HIP(hipStreamSynchronize(c->stream));
+      if (c->h_u32.p[0]) throw StatusError(FMX_E_RANGE, "voxel coordinate outside the packed-key range");
+      c->map_err_checked = true;
+    }
+    if (!cpl && !cpt) return;
     match_counts_fetch(c);
-    c->h_u32.ensure(8);
-    FMX_HIP(hipMemcpyAsync(c->h_u32.p, c->map_err_p, 4, hipMemcpyDeviceToHost, c->stream));
-    FMX_HIP(hipStreamSynchronize(c->stream));
-    if (c->h_u32.p[0]) throw StatusError(FMX_E_RANGE, "voxel coordinate outside the packed-key range");
     if (cpl) std::memcpy(cpl, c->cnt_pl.data(), c->K * sizeof(uint32_t));
     if (cpt) std::memcpy(cpt, c->cnt_pt.data(), c->K * sizeof(uint32_t));
   });

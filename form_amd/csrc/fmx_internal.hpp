@@ -323,6 +323,7 @@ struct fmx_ctx {
   int cell_m = 1;       // subdivision: rings searched
   bool have_map = false;
   uint32_t* map_err_p = nullptr;  // range-error word of the last build (in map.state)
+  bool map_err_checked = false;   // ... already read back (once per build)
   fmx::HBuf<unsigned long long> h_mapinfo;  // pinned: epoch << 32 | dense cells of the last finished build
 
   // ---- match results (query-indexed; planar then point)

@@ -1376,6 +1376,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   M.epoch += 1;
   BuildState* bst = reinterpret_cast<BuildState*>(M.state.p);
   c->map_err_p = &bst[M.epoch & 1].err;
+  c->map_err_checked = false;
   M.rinfo.ensure(n + 1);
   M.claim.ensure(n + 1);
   M.dense.ensure(n / kDenseMin + 1);

@@ -239,8 +239,12 @@ class Context:
                                         C.c_double(voxel_width)))
         self.K = len(scans)
 
-    def match(self, pose_j34, max_dist: float):
+    def match(self, pose_j34, max_dist: float, counts: bool = True):
+        """fmx_match; counts=False returns None without waiting for the kernel."""
         pose = np.ascontiguousarray(pose_j34, np.float64).reshape(12)
+        if not counts:
+            self._chk(self._L.fmx_match(self.h, _p(pose), C.c_double(max_dist), None, None))
+            return None
         cpl = np.zeros(max(self.K, 1), np.uint32)
         cpt = np.zeros(max(self.K, 1), np.uint32)
         self._chk(self._L.fmx_match(self.h, _p(pose), C.c_double(max_dist), _p(cpl), _p(cpt)))

@@ -136,7 +136,9 @@ fmx_status fmx_map_build(fmx_ctx* ctx, const uint64_t* scans, const double* pose
  * nearest map keypoint of every query at pose_j (VoxelMap::find_closest,
  * map.tpp:70-91), moved back to its scan's frame, accepted if d^2 < max_dist^2 and
  * bucketed per pair on the device.  counts_planar / counts_point (may be NULL):
- * K = n_scans accepted correspondences per pair. */
+ * K = n_scans accepted correspondences per pair.  With both NULL the call returns
+ * without waiting for the device (once the map build's range check has been read);
+ * the calls that read the results wait for them. */
 fmx_status fmx_match(fmx_ctx* ctx, const double pose_j34[12], double max_dist,
                      uint32_t* counts_planar, uint32_t* counts_point);
 /* Per-query match results of the last fmx_match, planar queries then point
