@@ -1,6 +1,7 @@
 #!/bin/bash
-# C5 A/B: this build (4-lane groups for large query sets) vs form_amd/ab/libfmx_g2.so
-# (2-lane groups), after the large-query-set parity tests on the g2 build.
+# C5 A/B of builds: TAGS (default "g4 g2") — "g4" = this build (form_amd/libfmx.so), any
+# other tag = form_amd/ab/libfmx_<tag>.so — after the large-query-set parity tests on
+# form_amd/ab/libfmx_$TEST_TAG.so.
 mkdir -p gpurun_out
 FMX_LIB=$PWD/form_amd/ab/libfmx_${TEST_TAG:-g2}.so timeout -k 10 400 python -u -m pytest tests/test_gpu_c5.py tests/test_gpu_parity.py -k "c5 or large or C5" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_g2.log 2>&1 || { tail -40 gpurun_out/pytest_g2.log; exit 1; }
 tail -1 gpurun_out/pytest_g2.log
