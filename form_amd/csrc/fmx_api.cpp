@@ -81,10 +81,16 @@ ProfScope::~ProfScope() {
   pr.pending.push_back({id, {a, b}});
   pr.pending_bytes.push_back(bytes);
 }
+// every stream of the context: main, side (map build), side2 (pipelined extraction)
+static void sync_all(fmx_ctx* c) {
+  FMX_HIP(hipStreamSynchronize(c->stream));
+  if (c->side) FMX_HIP(hipStreamSynchronize(c->side));
+  if (c->side2) FMX_HIP(hipStreamSynchronize(c->side2));
+}
 static void prof_collect(fmx_ctx* c) {
   Prof& pr = c->prof;
   if (pr.pending.empty()) return;
-  FMX_HIP(hipStreamSynchronize(c->stream));
+  sync_all(c);  // profiled launches run on all three streams
   for (size_t i = 0; i < pr.pending.size(); ++i) {
     auto& [id, ev] = pr.pending[i];
     float ms = 0.f;
@@ -1528,7 +1534,7 @@ fmx_status fmx_profile_read(fmx_ctx* c, double* ms, uint64_t* launches, double* 
   });
 }
 fmx_status fmx_sync(fmx_ctx* c) {
-  return guard(c, [&] { FMX_HIP(hipStreamSynchronize(c->stream)); });
+  return guard(c, [&] { sync_all(c); });
 }
 
 }  // extern "C"

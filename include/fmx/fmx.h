@@ -235,7 +235,8 @@ int fmx_profile_count(void);
 const char* fmx_profile_name(int k);
 fmx_status fmx_profile_read(fmx_ctx* ctx, double* ms, uint64_t* launches, double* bytes, int n);
 
-/* Synchronize the context stream. */
+/* Wait for all of the context's device work (its stream and the side streams of the
+ * map build and the pipelined extraction). */
 fmx_status fmx_sync(fmx_ctx* ctx);
 
 #ifdef __cplusplus
