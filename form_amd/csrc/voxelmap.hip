@@ -44,7 +44,12 @@
 #define FMX_MATCH_WAVES 4  // waves per SIMD k_match is compiled for (register budget 128)
 #endif
 #ifndef FMX_MATCH_WAVES_PLAIN
+#if defined(FMX_MATCH_GROUP) && FMX_MATCH_GROUP == 1
+#define FMX_MATCH_WAVES_PLAIN 7  // ... without the dense-cell walk, one lane per query (71 VGPRs;
+                                 // C5 match 0.243 -> 0.230 ms per launch, 8 waves spill)
+#else
 #define FMX_MATCH_WAVES_PLAIN 6  // ... and without the dense-cell walk (register budget 80)
+#endif
 #endif
 #ifndef FMX_MATCH_DEPTH_PLAIN
 #define FMX_MATCH_DEPTH_PLAIN 2  // record loads in flight per lane without the dense-cell walk
