@@ -36,11 +36,16 @@ def allreduce_sum(x: np.ndarray, device=None) -> np.ndarray:
     return t.cpu().numpy()
 
 
+_TRIU: dict[int, tuple[np.ndarray, np.ndarray]] = {}
+
+
 def unpack_sym(G: np.ndarray) -> np.ndarray:
     """Packed upper triangle (row-major) -> full symmetric matrix."""
     m = int(round((math.sqrt(8 * len(G) + 1) - 1) / 2))
-    M = np.zeros((m, m))
-    iu = np.triu_indices(m)
+    iu = _TRIU.get(m)
+    if iu is None:
+        iu = _TRIU[m] = np.triu_indices(m)
+    M = np.empty((m, m))
     M[iu] = G
     M.T[iu] = G
     return M
@@ -50,27 +55,37 @@ def gauss_newton_step(G28: np.ndarray, lam: float = 0.0) -> np.ndarray:
     """Solve (H + lam I) dx = g from the packed single-pose 7x7 [H_j b]^T[H_j b]
     (H = A^T A, g = A^T b): the increment in GTSAM's tangent [w; v]."""
     M = unpack_sym(G28)
-    H, g = M[:6, :6], M[:6, 6]
-    return np.linalg.solve(H + lam * np.eye(6), g)
+    H = M[:6, :6]
+    if lam:
+        H = H + lam * np.eye(6)
+    return np.linalg.solve(H, M[:6, 6])
 
 
-def expmap(xi: np.ndarray) -> np.ndarray:
-    w, v = xi[:3], xi[3:]
-    th = float(np.linalg.norm(w))
-    W = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+def expmap(xi) -> np.ndarray:
+    """SE(3) exponential of [w; v] as a 3x4 [R | t] (Rodrigues; scalar arithmetic, the
+    per-iteration host step of the C5 loop)."""
+    wx, wy, wz, vx, vy, vz = (float(v) for v in xi)
+    th2 = wx * wx + wy * wy + wz * wz
+    th = math.sqrt(th2)
     if th < 1e-12:
-        R, V = np.eye(3) + W, np.eye(3) + 0.5 * W
+        a, b, c = 1.0, 0.5, 1.0 / 6.0
     else:
-        R = np.eye(3) + math.sin(th) / th * W + (1 - math.cos(th)) / th**2 * W @ W
-        V = np.eye(3) + (1 - math.cos(th)) / th**2 * W + (th - math.sin(th)) / th**3 * W @ W
-    T = np.zeros((3, 4))
-    T[:, :3] = R
-    T[:, 3] = V @ v
+        a, b, c = math.sin(th) / th, (1 - math.cos(th)) / th2, (th - math.sin(th)) / (th2 * th)
+    # W, W^2 entries
+    W = ((0.0, -wz, wy), (wz, 0.0, -wx), (-wy, wx, 0.0))
+    W2 = ((-(wy * wy + wz * wz), wx * wy, wx * wz), (wx * wy, -(wx * wx + wz * wz), wy * wz),
+          (wx * wz, wy * wz, -(wx * wx + wy * wy)))
+    v = (vx, vy, vz)
+    T = np.empty((3, 4))
+    for r in range(3):
+        for s in range(3):
+            T[r, s] = (1.0 if r == s else 0.0) + a * W[r][s] + b * W2[r][s]
+        T[r, 3] = sum(((1.0 if r == s else 0.0) + b * W[r][s] + c * W2[r][s]) * v[s] for s in range(3))
     return T
 
 
 def compose(A: np.ndarray, B: np.ndarray) -> np.ndarray:
-    T = np.zeros((3, 4))
+    T = np.empty((3, 4))
     T[:, :3] = A[:, :3] @ B[:, :3]
     T[:, 3] = A[:, :3] @ B[:, 3] + A[:, 3]
     return T
