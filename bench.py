@@ -75,10 +75,35 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(n):
+    """--gpus N without a launcher (WORLD_SIZE unset): start N ranks as child processes
+    (torch.distributed.run, one per GPU, rendezvous on 127.0.0.1) and exit with their
+    status.  Runs before anything touches the GPU (torch.cuda.device_count() does not
+    initialise it); N larger than the visible devices is an error, never a smaller run."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    sys.exit(subprocess.call(cmd))
+
+
 def dist_setup(n):
+    if "WORLD_SIZE" not in os.environ:
+        ndev = torch.cuda.device_count()
+        if n > ndev:
+            print(f"bench.py: --gpus {n} but {ndev} HIP device(s) visible", file=sys.stderr)
+            sys.exit(2)
+        if n > 1:
+            spawn_ranks(n)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        print(f"bench.py: --gpus {n} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -232,15 +257,11 @@ def ate_block(scans_host, oracle_poses, params, k0, device, single, pipeline):
 
 
 def c5_setup(a, rank, world, local):
-    """The sharded C5 problem on this rank: the replicated 50M-voxel terrain map, this
-    rank's shard of the 2M-point scan, an RCCL communicator over all ranks."""
+    """The sharded C5 problem on this rank: the replicated 50M-voxel terrain map and an
+    RCCL communicator over all ranks (queries: c5_queries)."""
     from form_amd import shard
-    dev = f"cuda:{local}"
     w = 0.8
-    pos4, nrm4 = shard.terrain_map(a.c5_side, w, synth.SEED, dev)
-    Ttrue = shard.c5_offset()
-    q4, n4 = shard.make_queries(pos4, nrm4, a.c5_queries, Ttrue, 0.03, synth.SEED + 1)
-    b, e = shard.shard_bounds(a.c5_queries, rank, world)
+    pos4, nrm4 = shard.terrain_map(a.c5_side, w, synth.SEED, f"cuda:{local}")
     n_map = pos4.shape[0]
     prm = fmx.EstimatorParams(keypoint_pool_capacity=n_map + 1024, voxel_subdivision=a.subdiv or 1)
     ctx = fmx.Context(prm, device=local)
@@ -252,10 +273,29 @@ def c5_setup(a, rank, world, local):
     ctx.keypoints_add_device(0, pos4, nrm4)
     I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
     ctx.map_build([0], I34[None], w)
-    ctx.set_queries_device(q4[b:e].contiguous(), n4[b:e].contiguous())
-    del pos4, nrm4, q4, n4
     torch.cuda.synchronize()
-    return ctx, Ttrue, n_map, w
+    return ctx, pos4, nrm4, n_map, w
+
+
+C5_DISTS = {
+    # a 240 m scan of the terrain (drawn with replacement, grid order): the round-1/2 line
+    "local": "2M samples (with replacement) of the terrain within 240 m of the sensor, grid order",
+    # 2M distinct features across the whole map, ring/azimuth order
+    "wholemap": "2M distinct features drawn across the whole map, 128 range rings in azimuth order",
+}
+
+
+def c5_queries(a, dist_name, pos4, nrm4, rank, world):
+    """This rank's contiguous shard of the C5 query set `dist_name` and the true offset."""
+    from form_amd import shard
+    if dist_name == "local":
+        Ttrue = shard.c5_offset()
+        q4, n4 = shard.make_queries(pos4, nrm4, a.c5_queries, Ttrue, 0.03, synth.SEED + 1)
+    else:
+        Ttrue = shard.c5_offset(shard.C5_WHOLEMAP_ROT_SCALE)
+        q4, n4 = shard.make_queries_wholemap(pos4, nrm4, a.c5_queries, Ttrue, 0.03, synth.SEED + 2)
+    b, e = shard.shard_bounds(a.c5_queries, rank, world)
+    return q4[b:e].contiguous(), n4[b:e].contiguous(), Ttrue
 
 
 def c5_register(ctx, w, max_iters=30, thr=1e-4):
@@ -263,11 +303,12 @@ def c5_register(ctx, w, max_iters=30, thr=1e-4):
     (this rank's shard) -> the shard's single-pose 7x7 normal equations, all-reduced
     over the ranks on the device (RCCL) -> the identical Gauss-Newton step on every
     rank, from the identity to convergence (form.cpp:83-88's 1e-4 threshold on the
-    increment).  Returns (pose, ICP iterations)."""
+    increment).  fmx_match without counts + fmx_linearize_matched at the same pose run
+    as ONE fused launch (no per-query results).  Returns (pose, ICP iterations)."""
     from form_amd import shard
     T = np.hstack([np.eye(3), np.zeros((3, 1))])
     for it in range(max_iters):
-        ctx.match(T, w, counts=False)  # no wait: linearize_matched is queued behind it
+        ctx.match(T, w, counts=False)  # deferred: fused with the linearization below
         S, _ = ctx.linearize_matched(T, 0.1)
         dx = shard.gauss_newton_step(S)
         T = shard.compose(T, shard.expmap(dx))
@@ -276,12 +317,9 @@ def c5_register(ctx, w, max_iters=30, thr=1e-4):
     return T, max_iters
 
 
-def run_c5(a, rank, world, local, steps, warmup, profile=True):
-    """C5 (SURVEY.md §8e): a 2M-point scan vs a 50M-voxel terrain submap, the scan's
-    points sharded over the ranks, the map replicated.  A step = one registration
-    (c5_register); strong scaling: the total work per step is fixed."""
+def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmup, profile):
+    """Time `steps` registrations of the current query set (max over ranks)."""
     from form_amd import shard
-    ctx, Ttrue, n_map, w = c5_setup(a, rank, world, local)
     for _ in range(warmup):
         T, iters = c5_register(ctx, w)
     barrier(world)
@@ -295,17 +333,17 @@ def run_c5(a, rank, world, local, steps, warmup, profile=True):
     barrier(world)
     t_local = time.perf_counter() - t0
     prof, work = {}, {"queries": 1.0}
+    nprof = max(steps // 2, 1)
     if profile:
         ctx.profile(True)
         ctx.profile_reset()
-        for _ in range(max(steps // 2, 1)):
+        for _ in range(nprof):
             c5_register(ctx, w)
         ctx.sync()
         prof = ctx.profile_read()
         work = ctx.match_work()
         ctx.profile(False)
     t_max = max_over_ranks(t_local, world, local)
-    ctx.close()
     if rank != 0:
         return None
     value = steps / t_max
@@ -319,27 +357,58 @@ def run_c5(a, rank, world, local, steps, warmup, profile=True):
         "icp_iters_per_registration": round(it_total / steps, 3),
         "icp_iters_per_s": round(it_total / t_max, 3),
         "mpts_per_s": round(value * a.c5_queries / 1e6, 3),
-        "config": {"workload": f"c5: {a.c5_queries} points within {shard.C5_RANGE_M:.0f} m vs a {n_map}-voxel "
-                               "terrain submap; points sharded contiguously, map replicated; single-pose 7x7 "
-                               "normal equations all-reduced (RCCL, device buffers, context stream) per ICP "
-                               "iteration", "points_per_scan": a.c5_queries,
-                   "parallelism": f"point shards x{world} + all_reduce"},
+        "config": {"workload": f"c5/{dist_name}: {a.c5_queries} points vs a {n_map}-voxel terrain submap "
+                               f"({C5_DISTS[dist_name]}); points sharded contiguously, map replicated; match + "
+                               "single-pose 7x7 normal equations fused in one launch, all-reduced (RCCL, device "
+                               "buffers, context stream) per ICP iteration", "points_per_scan": a.c5_queries,
+                   "query_distribution": dist_name, "parallelism": f"point shards x{world} + all_reduce"},
         "pose_error": {"initial_m": round(e0t, 6), "initial_rad": round(e0r, 8), "final_m": round(et, 6),
                        "final_rad": round(er, 8)},
     }
     if prof:
         name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
-        avg_ms = d["ms"] / max(d["launches"], 1)
-        bytes_per = d["bytes"] / max(d["launches"], 1)
-        achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        nprof = max(steps // 2, 1)
-        out["roofline"] = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                               frac=round(achieved / HBM_PEAK_GBS, 6), traffic=pmc_traffic(a, name, "c5"),
-                               avg_launch_us=round(avg_ms * 1e3, 3), alg_bytes_per_launch=bytes_per)
+        out["roofline"] = roofline(a, name, d, "c5" if dist_name == "local" else "c5_wholemap")
         out["kernels_ms_per_step"] = {k: round(v["ms"] / nprof, 4) for k, v in prof.items() if v["ms"] > 0}
         out["match_work_per_query"] = {k: round(v / max(work["queries"], 1), 3) for k, v in work.items()
                                        if k != "queries"}
     return out
+
+
+def run_c5(a, rank, world, local, steps, warmup, profile=True, dists=("local", "wholemap")):
+    """C5 (SURVEY.md §8e): a 2M-point scan vs a 50M-voxel terrain submap, the scan's
+    points sharded over the ranks, the map replicated (built once, both query sets run
+    against it).  A step = one registration (c5_register); strong scaling: the total
+    work per step is fixed.  Returns {dist: line} on rank 0."""
+    ctx, pos4, nrm4, n_map, w = c5_setup(a, rank, world, local)
+    out = {}
+    for dn in dists:
+        q4, n4, Ttrue = c5_queries(a, dn, pos4, nrm4, rank, world)
+        ctx.set_queries_device(q4, n4)
+        torch.cuda.synchronize()
+        del q4, n4
+        out[dn] = c5_line(a, ctx, dn, Ttrue, n_map, w, rank, world, local, steps, warmup, profile)
+    del pos4, nrm4
+    ctx.close()
+    return out if rank == 0 else None
+
+
+def roofline(a, name, d, workload):
+    """The roofline block of the dominant kernel class `name` (profile entry d): the §8(d)
+    algorithmic bytes per launch over the HIP-event average launch time (frac), and the
+    PMC-measured HBM bytes per launch (traffic, profiles/traffic_<workload>.json) over
+    the same time (hbm_frac): what the memory system actually moved."""
+    avg_ms = d["ms"] / max(d["launches"], 1)
+    bytes_per = d["bytes"] / max(d["launches"], 1)
+    achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = pmc_traffic(a, name, workload)
+    roof = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, avg_launch_us=round(avg_ms * 1e3, 3),
+                alg_bytes_per_launch=bytes_per)
+    if traffic and avg_ms > 0:
+        hbm = traffic / (avg_ms * 1e-3) / 1e9
+        roof["hbm_achieved"] = round(hbm, 3)
+        roof["hbm_frac"] = round(hbm / HBM_PEAK_GBS, 6)
+    return roof
 
 
 def main():
@@ -347,8 +416,10 @@ def main():
     rank, world, local = dist_setup(a.gpus)
     if a.workload == "c5":
         torch.cuda.set_device(local)
-        out = run_c5(a, rank, world, local, a.steps, a.warmup)
-        if out is not None:
+        res = run_c5(a, rank, world, local, a.steps, a.warmup)
+        if res is not None:
+            out = res["local"]
+            out["wholemap"] = res["wholemap"]
             print(json.dumps(out))
         if world > 1:
             import torch.distributed as dist
@@ -430,6 +501,9 @@ def main():
     c5 = None
     if not a.no_c5:
         c5 = run_c5(a, rank, world, local, a.c5_steps, a.c5_warmup, profile=False)
+    if rank == 0 and c5 is not None:
+        c5_whole = c5["wholemap"]
+        c5 = c5["local"]
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
@@ -438,15 +512,8 @@ def main():
     value = scans_total / t_max
     ms_per_step = t_max / a.steps * 1e3
     # dominant kernel by device time in the timed region
-    dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
-    name, d = dom
-    avg_ms = d["ms"] / max(d["launches"], 1)
-    bytes_per = d["bytes"] / max(d["launches"], 1)
-    achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = pmc_traffic(a, name)
-    roof = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, avg_launch_us=round(avg_ms * 1e3, 3),
-                alg_bytes_per_launch=bytes_per)
+    name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    roof = roofline(a, name, d, a.workload)
     st_mean = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]} if stats else {}
     kern_ms = {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()}
     kern_sum = sum(kern_ms.values())
@@ -490,6 +557,7 @@ def main():
         out["sequential_extraction"] = sequential
     if c5 is not None:
         out["sharded_c5"] = c5
+        out["sharded_c5_wholemap"] = c5_whole
     if prev_aff is not None:
         os.sched_setaffinity(0, prev_aff)  # the CPU baseline's threads use every host core
     if not a.no_cpu_baseline and world == 1:

@@ -17,6 +17,7 @@
 
 #include <rccl/rccl.h>
 
+#include "fmx_device.hpp"
 #include "fmx_internal.hpp"
 
 namespace fmx {
@@ -105,6 +106,32 @@ void comm_allreduce_sum(fmx_ctx* c, double* dev, size_t n) {
   if (!c->comm) return;
   check(rccl().all_reduce(dev, dev, n, ncclFloat64, ncclSum, static_cast<ncclComm_t>(c->comm), c->stream),
         "ncclAllReduce");
+}
+
+// The all-reduced sums to the caller's pinned host buffer, then the completion word:
+// one block behind the collective on the context stream, every element stored
+// write-through at system scope (host_store), each wave drained, then one lane
+// publishes seq.  The sharded path thus keeps the single-GPU path's flag wait
+// (wait_flag, a few us after the data lands) instead of a hipMemcpyAsync D2H plus a
+// hipStreamQuery spin (~20-50 us per round trip on this image).
+constexpr int kPublishThreads = 256;
+__global__ __launch_bounds__(kPublishThreads) void k_publish_sums(const double* __restrict__ src, double* dst,
+                                                                  uint32_t n, uint32_t* flag, uint32_t seq) {
+  for (uint32_t i = threadIdx.x; i < n; i += kPublishThreads) host_store(dst + i, src[i]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) publish_flag(flag, seq);
+}
+
+void comm_allreduce_publish(fmx_ctx* c, double* dev, size_t n, HBuf<double>& host) {
+  if (n > 0xFFFFFFFFu) throw StatusError(FMX_E_INVAL, "all-reduce too large");
+  comm_allreduce_sum(c, dev, n);
+  host.ensure(n);
+  const uint32_t seq = next_flag(c);
+  hipLaunchKernelGGL(k_publish_sums, dim3(1), dim3(kPublishThreads), 0, c->stream, dev, host.d, (uint32_t)n,
+                     c->h_flag.d, seq);
+  FMX_HIP(hipGetLastError());
+  wait_flag(c, c->h_flag.p, seq);
 }
 
 }  // namespace fmx

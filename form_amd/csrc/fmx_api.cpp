@@ -50,6 +50,12 @@ void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted) {
   if (c->match_group != 8) gl::run_insert(c, scan, n_inserted);
   else g8::run_insert(c, scan, n_inserted);
 }
+void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* dst,
+                         uint32_t* flag, uint32_t seq) {
+  if (match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) != 1)
+    throw StatusError(FMX_E_STATE, "fused match + linearization needs the one-lane-per-query build");
+  gl::run_match_linearize(c, pose_j34, max_dist, sigma, dst, flag, seq);
+}
 void match_counts_fetch(fmx_ctx* c, bool wait) {
   if (c->match_group != 8) gl::match_counts_fetch(c, wait);
   else g8::match_counts_fetch(c, wait);
@@ -57,7 +63,8 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
 
 // ============================================================================ profiling
 static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest",   "fit",       "compact", "map_build",
-                                             "match",        "pair_sort", "linearize", "insert",  "window"};
+                                             "match",        "pair_sort", "linearize", "insert",  "window",
+                                             "match_linearize"};
 
 ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), bytes(by), st(s) {
   if (!pr.on) return;
@@ -150,11 +157,29 @@ struct KeyScanner {
   }
 };
 
-template <class F>
+// FMX_NO_FUSED (A/B diagnostic): never defer fmx_match, so nothing runs fused
+bool no_fused() {
+  static const bool v = std::getenv("FMX_NO_FUSED") != nullptr;
+  return v;
+}
+
+// A deferred fmx_match (ctx->lazy): launched now, before anything reads or changes
+// the state it depends on.
+void settle_match(fmx_ctx* c) {
+  if (!c->lazy.pending) return;
+  c->lazy.pending = false;
+  run_match(c, c->lazy.pose, c->lazy.max_dist, c->P.min_dist_map, true, true);
+}
+
+// SETTLE: run a deferred fmx_match first — every entry point but fmx_match itself,
+// fmx_linearize_matched (which may consume it fused) and those that read no match
+// state (pose, stats, profile counters, fmx_sync: a deferred match is no queued work)
+template <bool SETTLE = true, class F>
 fmx_status guard(fmx_ctx* c, F&& f) {
   if (!c) return FMX_E_INVAL;
   try {
     FMX_HIP(hipSetDevice(c->device));
+    if constexpr (SETTLE) settle_match(c);
     f();
     c->err.clear();
     return FMX_OK;
@@ -1345,11 +1370,23 @@ fmx_status fmx_map_build(fmx_ctx* c, const uint64_t* scans, const double* poses,
 }
 
 fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint32_t* cpl, uint32_t* cpt) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
+    c->lazy.pending = false;  // a newer match replaces a deferred one
     if (!c->have_map) throw StatusError(FMX_E_STATE, "fmx_map_build first");
     if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
     if (!(max_dist > 0)) throw StatusError(FMX_E_INVAL, "max_dist must be > 0");
-    run_match(c, pose_j, max_dist, c->P.min_dist_map, true, true);  // rows scattered when read
+    if (!pose_j) throw StatusError(FMX_E_INVAL, "null pose");
+    // no count outputs on a large query set (the one-lane-per-query build): deferred,
+    // so that fmx_linearize_matched at this pose can run fused with it
+    const bool defer = !cpl && !cpt && match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) == 1 &&
+                       !no_fused();
+    if (defer) {
+      c->lazy.pending = true;
+      std::memcpy(c->lazy.pose, pose_j, sizeof(c->lazy.pose));
+      c->lazy.max_dist = max_dist;
+    } else {
+      run_match(c, pose_j, max_dist, c->P.min_dist_map, true, true);  // rows scattered when read
+    }
     // the map's range-error word is read back once per build; with no count outputs
     // requested the call then returns without waiting (the next consumer of the match
     // results waits for them: fmx_linearize_matched, fmx_match_download, ...)
@@ -1433,9 +1470,16 @@ fmx_status fmx_error(fmx_ctx* c, const double* pi, const double* pj, double sigm
 }
 
 fmx_status fmx_linearize_matched(fmx_ctx* c, const double pose_j[12], double sigma, double out[29]) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
     if (!(sigma > 0)) throw StatusError(FMX_E_INVAL, "sigma must be > 0");
     if (!pose_j || !out) throw StatusError(FMX_E_INVAL, "null pose / output");
+    if (c->lazy.pending && std::memcmp(pose_j, c->lazy.pose, sizeof(c->lazy.pose)) == 0) {
+      // the deferred match at this very pose: match + linearization fused, no per-query
+      // results (the match stays deferred for any later reader)
+      run_match_linearize_total(c, pose_j, c->lazy.max_dist, sigma, out);
+      return;
+    }
+    settle_match(c);
     if (!c->have_match) throw StatusError(FMX_E_STATE, "no match results");
     run_linearize_total(c, pose_j, sigma, out);
   });
@@ -1482,7 +1526,7 @@ fmx_status fmx_register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev
 }
 
 fmx_status fmx_current_pose(fmx_ctx* c, double pose[12]) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
     if (!c->est || !c->est->init) {
       const Pose I = identity();
       std::memcpy(pose, I.m, sizeof(I.m));
@@ -1492,8 +1536,58 @@ fmx_status fmx_current_pose(fmx_ctx* c, double pose[12]) {
   });
 }
 
-fmx_status fmx_last_stats(fmx_ctx* c, uint64_t* stats, int n) {
+fmx_status fmx_map_download(fmx_ctx* c, double voxel_width, double* planar, uint64_t* planar_scan,
+                            uint32_t* n_planar, double* point, uint64_t* point_scan, uint32_t* n_point) {
   return guard(c, [&] {
+    if (!c->est || !c->est->init) throw StatusError(FMX_E_STATE, "no registered scan (fmx_register_scan)");
+    if (!(voxel_width > 0)) throw StatusError(FMX_E_INVAL, "voxel width must be > 0");
+    if (!n_planar || !n_point) throw StatusError(FMX_E_INVAL, "null count pointers");
+    finish_tail(c);  // the reference's register_scan ends with marginalization + KeypointMap::remove
+    fmx_ctx::Est& e = *c->est;
+    // m_keypoint_map's scans, each at its current estimate (map.tpp:135-137)
+    std::set<uint64_t> sset;
+    for (int t = 0; t < 2; ++t)
+      for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
+    std::vector<uint64_t> scans(sset.begin(), sset.end());
+    std::vector<double> poses(12 * scans.size());
+    for (size_t k = 0; k < scans.size(); ++k) {
+      auto it = e.values.find(scans[k]);
+      if (it == e.values.end()) throw StatusError(FMX_E_STATE, "keypoints of a scan without an estimate");
+      std::memcpy(&poses[12 * k], it->second.m, 12 * sizeof(double));
+    }
+    uint32_t cnt[2] = {0, 0};
+    for (int t = 0; t < 2; ++t)
+      for (uint64_t s : scans) {
+        auto it = c->pool[t].ranges.find(s);
+        if (it != c->pool[t].ranges.end()) cnt[t] += it->second.second;
+      }
+    double* outs[2] = {planar, point};
+    uint64_t* sids[2] = {planar_scan, point_scan};
+    uint32_t* ns[2] = {n_planar, n_point};
+    for (int t = 0; t < 2; ++t) {
+      if (!outs[t] && !sids[t]) {
+        *ns[t] = cnt[t];
+        continue;
+      }
+      if (*ns[t] < cnt[t]) throw StatusError(FMX_E_SIZE, "map_download: buffer smaller than the map");
+      std::vector<double> xyz, nrm;
+      std::vector<uint64_t> sid;
+      const uint32_t m = map_snapshot(c, t, scans, poses, voxel_width, xyz, nrm, sid);
+      const int stride = t == 0 ? 6 : 3;
+      for (uint32_t r = 0; r < m; ++r) {
+        if (outs[t]) {
+          std::memcpy(outs[t] + (size_t)stride * r, &xyz[3 * (size_t)r], 3 * sizeof(double));
+          if (t == 0) std::memcpy(outs[t] + (size_t)stride * r + 3, &nrm[3 * (size_t)r], 3 * sizeof(double));
+        }
+        if (sids[t]) sids[t][r] = sid[r];
+      }
+      *ns[t] = m;
+    }
+  });
+}
+
+fmx_status fmx_last_stats(fmx_ctx* c, uint64_t* stats, int n) {
+  return guard<false>(c, [&] {
     if (!stats || n < 0) throw StatusError(FMX_E_INVAL, "null stats");
     for (int k = 0; k < n; ++k) stats[k] = k < kStatsN ? c->stats[k] : 0;
   });
@@ -1509,10 +1603,10 @@ fmx_status fmx_match_work(fmx_ctx* c, double work[3]) {
 }
 
 fmx_status fmx_profile_enable(fmx_ctx* c, int on) {
-  return guard(c, [&] { c->prof.on = on != 0; });
+  return guard<false>(c, [&] { c->prof.on = on != 0; });
 }
 fmx_status fmx_profile_reset(fmx_ctx* c) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
     prof_collect(c);
     for (int i = 0; i < PROF_COUNT; ++i) {
       c->prof.ms[i] = 0;
@@ -1524,7 +1618,7 @@ fmx_status fmx_profile_reset(fmx_ctx* c) {
 int fmx_profile_count(void) { return PROF_COUNT; }
 const char* fmx_profile_name(int k) { return (k >= 0 && k < PROF_COUNT) ? kProfNames[k] : ""; }
 fmx_status fmx_profile_read(fmx_ctx* c, double* ms, uint64_t* launches, double* bytes, int n) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
     prof_collect(c);
     for (int i = 0; i < std::min(n, (int)PROF_COUNT); ++i) {
       if (ms) ms[i] = c->prof.ms[i];
@@ -1534,7 +1628,7 @@ fmx_status fmx_profile_read(fmx_ctx* c, double* ms, uint64_t* launches, double* 
   });
 }
 fmx_status fmx_sync(fmx_ctx* c) {
-  return guard(c, [&] { sync_all(c); });
+  return guard<false>(c, [&] { sync_all(c); });
 }
 
 }  // extern "C"

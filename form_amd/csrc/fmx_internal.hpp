@@ -103,6 +103,7 @@ enum ProfId {
   PROF_LINEARIZE,
   PROF_INSERT,
   PROF_WINDOW,
+  PROF_MATCH_LIN,
   PROF_COUNT
 };
 
@@ -365,6 +366,7 @@ struct fmx_ctx {
   // ---- linearize
   fmx::DBuf<double> bpart;                        // k_linearize_total block partials
   fmx::DBuf<uint32_t> ticket;                     // its last-block ticket
+  fmx::DBuf<uint32_t> fz_tickets;                 // fused match + linearization: per block-group tickets
   fmx::DBuf<uint32_t> mcnt, mticket;              // query-order match: per-pair counters + ticket
   fmx::DBuf<uint32_t> ins_blk, ins_off;           // per match block insert counts / offsets
   uint32_t ins_tot[2] = {0, 0};                   // insert totals of the last match
@@ -373,6 +375,15 @@ struct fmx_ctx {
   fmx::HBuf<uint32_t> h_flag;                     // mapped completion word (wait_flag)
   uint32_t flag_seq = 0;
   bool have_qo = false;
+  // fmx_match without count outputs on a large query set is not launched at once: if
+  // the next consumer is fmx_linearize_matched at the same pose, match and
+  // linearization run fused (no per-query results); any other consumer launches the
+  // match first (fmx_api.cpp, settle_match)
+  struct LazyMatch {
+    bool pending = false;
+    double pose[12];
+    double max_dist = 0.0;
+  } lazy;
   fmx::HBuf<double> h_poses, h_G;
   fmx::HBuf<int32_t> h_i32;
 
@@ -565,7 +576,9 @@ inline uint32_t next_flag(fmx_ctx* c) {
                  bool sorted = true, bool defer_scatter = false);                                    \
   void run_pair_scatter(fmx_ctx* c);                                                                 \
   void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);                                  \
-  void match_counts_fetch(fmx_ctx* c, bool wait = true);
+  void match_counts_fetch(fmx_ctx* c, bool wait = true);                                             \
+  void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* dst, \
+                           uint32_t* flag, uint32_t seq);
 // Windows of at most this many map scans (pairs) use the tiled pair sort; wider ones a
 // per-match-block histogram whose scatter ranks within one wave, so they take the g8
 // build (32 queries per block) whatever the query count.
@@ -595,6 +608,9 @@ void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);
 // wait = false: the caller knows the match kernel has completed (a later kernel in
 // stream order published a flag)
 void match_counts_fetch(fmx_ctx* c, bool wait = true);
+int match_group_for(uint64_t nq, uint32_t K);
+void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* dst,
+                         uint32_t* flag, uint32_t seq);
 // out[0..27]: summed single-pose system over all pairs at pose_j; out[28]: error
 void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, double* out);
 void upload_corr(fmx_ctx* c, uint32_t K, const uint32_t* np, const double* ppi, const double* pni,
@@ -609,10 +625,17 @@ void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double si
 void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
 void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* called with G_out = null
 // comm.cpp: RCCL communicator of the sharded path, all-reduce on the context stream
+// FORM::map() snapshot (snapshot.hip): world-frame keypoints of feature type t of
+// `scans` at `poses`, grouped by voxel of width w; returns the record count
+uint32_t map_snapshot(fmx_ctx* c, int t, const std::vector<uint64_t>& scans, const std::vector<double>& poses,
+                      double w, std::vector<double>& xyz, std::vector<double>& nrm, std::vector<uint64_t>& sid);
 void comm_unique_id(uint8_t id[128]);
 void comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank);
 void comm_destroy(fmx_ctx* c);
+void run_match_linearize_total(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* out);
 void comm_allreduce_sum(fmx_ctx* c, double* dev, size_t n);  // no-op without a communicator
+// all-reduce n device doubles, copy them to host.p (write-through + completion word), wait
+void comm_allreduce_publish(fmx_ctx* c, double* dev, size_t n, HBuf<double>& host);
 // fmx_linearize / fmx_error on k_win_linearize: mode 0 13 x 13 (91), 1 single-pose 7 x 7 (28), 2 errors only
 void win_linearize_pairs(fmx_ctx* c, const double* poses_i34, const double* poses_j34, double sigma, int mode,
                          double* G_out, double* err_out);

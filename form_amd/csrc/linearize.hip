@@ -285,13 +285,36 @@ void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, doubl
     FMX_HIP(hipGetLastError());
   }
   if (comm) {
-    comm_allreduce_sum(c, c->d_sum.p, 29);
-    FMX_HIP(hipMemcpyAsync(c->h_G.p, c->d_sum.p, 29 * sizeof(double), hipMemcpyDeviceToHost, st));
-    stream_wait(c);
+    comm_allreduce_publish(c, c->d_sum.p, 29, c->h_G);
   } else {
     wait_flag(c, c->h_flag.p, seq);
   }
   match_counts_fetch(c, false);  // the match kernel finished before this one started
+  std::memcpy(out, c->h_G.p, 29 * sizeof(double));
+}
+
+
+// fmx_linearize_matched on a deferred match at the same pose: match + linearization in
+// one launch (k_match's FUSED build), no per-query results materialized; the same
+// completion-word / all-reduce handling as run_linearize_total.
+void run_match_linearize_total(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* out) {
+  if (!c->have_map) throw StatusError(FMX_E_STATE, "no map");
+  c->h_G.ensure(32);
+  const bool comm = c->comm != nullptr;
+  if (comm) c->d_sum.ensure(32);
+  const uint32_t seq = next_flag(c);
+  run_match_linearize(c, pose_j34, max_dist, sigma, comm ? c->d_sum.p : c->h_G.d, comm ? nullptr : c->h_flag.d, seq);
+  if (comm) {
+    comm_allreduce_publish(c, c->d_sum.p, 29, c->h_G);
+  } else if (c->n_qpl + c->n_qpt == 0) {  // no launch: the zero system was set on the stream
+    stream_wait(c);
+  } else {
+    wait_flag(c, c->h_flag.p, seq);
+  }
+  if (c->counts_pending && c->prof.on) {  // the work counters of this launch (byte model)
+    stream_wait(c);
+    match_counts_fetch(c, false);
+  }
   std::memcpy(out, c->h_G.p, 29 * sizeof(double));
 }
 

@@ -591,9 +591,400 @@ __device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist,
   if (threadIdx.x == 0) *so.n_chunks = carry;
 }
 
+// Lanes of a wave holding G-lane group g's bits of a ballot.
+template <int G>
+__device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
+  if constexpr (G == kWave) return ballot;
+  else return (ballot >> ((lane_id() / G) * G)) & ((1ull << G) - 1);
+}
+
+// VoxelMap::find_closest (map.tpp:70-91) of one query by a group of G lanes (lane g of
+// the group), bounded by the incoming best (a.bound, or +inf).  Returns false when the
+// query was abandoned as heavy: a cell walk of more than `cap` records (group-uniform);
+// the caller then searches it again with a whole wave.
+template <int G, bool DENSE>
+__device__ __forceinline__ bool nn_search(const MatchArgs& a, const MapView& M, const double (&wq)[3], int g,
+                                          uint32_t* hd, uint32_t cap, double& best, uint32_t& best_rid,
+                                          uint32_t& best_i, uint32_t& n_probe, uint32_t& n_cand) {
+  const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
+  bool heavy = false;
+  // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
+  // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
+  // the record's build order (= insertion order inside a voxel, map.tpp:41-52)
+  const int sh = a.rings >= 2 ? 1 : 0;  // cells of w/2: reference voxel = cell >> 1
+  auto srank = [&](int sx, int sy, int sz) -> uint32_t {
+    const int dx = ((bx + sx) >> sh) - (bx >> sh), dy = ((by + sy) >> sh) - (by >> sh),
+              dz = ((bz + sz) >> sh) - (bz >> sh);
+    return (uint32_t)c_refrank[(dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)] << 27;
+  };
+  // one bucket read per probe: key, the cell's two boundaries and its dense bit in
+  // flight together; a bucket of another build epoch ends the chain (empty)
+  auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count, bool& dense) {
+    const int X = bx + sx, Y = by + sy, Z = bz + sz;
+    const unsigned long long key = brick_key(X, Y, Z, M.epoch);
+    const uint32_t ci = brick_cell(X, Y, Z);
+    uint64_t h = mix64(key) & M.mask;
+    first = 0;
+    count = 0;
+    dense = false;
+    for (;;) {
+      ++n_probe;
+      const Brick* b = M.bricks + h;
+      const unsigned long long k = b->key;
+      const uint32_t b0 = b->beg[ci], b1 = b->beg[ci + 1], dm = b->dense;
+      if (k == key) {
+        first = b0;
+        count = b1 - b0;
+        dense = (dm >> ci) & 1;
+        return;
+      }
+      if (key_epoch(k) != M.epoch) return;
+      h = (h + 1) & M.mask;
+    }
+  };
+  // a record is one double4: world position + its build order in .w (exact in a
+  // double), so a candidate test is one 32-B load
+  auto fold = [&](const double4& p, uint32_t i, uint32_t rk) {
+    const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
+    const double d2 = (dx * dx + dz * dz) + dy * dy;
+    const uint32_t tk = rk | ((uint32_t)(unsigned long long)p.w & 0x07FFFFFFu);  // build order: low bits
+    if (d2 <= best && (d2 < best || tk < best_rid)) {
+      best = d2;
+      best_rid = tk;
+      best_i = i;
+    }
+  };
+  // argmin over (d^2, tie key) across the group's lanes: DPP moves (VALU latency, no LDS
+  // crossbar) inside a row — [row_mirror l <-> 15-l,] row_half_mirror l <-> 7-l, quad
+  // xor 2, quad xor 1 — after ds_bpermute exchanges across rows for a whole wave
+  auto take = [&](double ob, uint32_t orid, uint32_t oi) {
+    if (oi != 0xFFFFFFFFu && (best_i == 0xFFFFFFFFu || ob < best || (ob == best && orid < best_rid))) {
+      best = ob;
+      best_rid = orid;
+      best_i = oi;
+    }
+  };
+  auto group_min = [&]() {
+    auto step = [&](auto ctrl_tag) {
+      constexpr int CTRL = decltype(ctrl_tag)::value;
+      const long long bb = __double_as_longlong(best);
+      const int blo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)bb, CTRL, 0xF, 0xF, false);
+      const int bhi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(bb >> 32), CTRL, 0xF, 0xF, false);
+      const double ob = __longlong_as_double((long long)(((unsigned long long)(uint32_t)bhi << 32) | (uint32_t)blo));
+      const uint32_t orid = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_rid, CTRL, 0xF, 0xF, false);
+      const uint32_t oi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_i, CTRL, 0xF, 0xF, false);
+      take(ob, orid, oi);
+    };
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 64,
+                  "group reduction assumes 1-, 2-, 4-, 8-, 16- or 64-lane groups");
+    if constexpr (G == 64) {
+#pragma unroll
+      for (int o = 32; o >= 16; o >>= 1) {
+        const double ob = __shfl_xor(best, o, 64);
+        const uint32_t orid = (uint32_t)__shfl_xor((int)best_rid, o, 64);
+        const uint32_t oi = (uint32_t)__shfl_xor((int)best_i, o, 64);
+        take(ob, orid, oi);
+      }
+    }
+    if constexpr (G >= 16) step(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
+    if constexpr (G >= 8) step(std::integral_constant<int, 0x141>{});   // row_half_mirror
+    if constexpr (G >= 4) step(std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]
+    if constexpr (G >= 2) step(std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]
+  };
+  // Records of one cell, walked by the whole group (group-uniform arguments).  A
+  // dense cell (k_map_dense) starts with a header of its 64 sub-cell ends: the
+  // query's own sub-cell first, then every other sub-cell whose box lower bound does
+  // not exceed the best so far, each group-walked (lane g holds sub-cells g, g + G, ...
+  // for the bounds; the header copy in LDS `hd` is shared by the group).
+  const double sw = a.w / kSubPerAxis;
+  auto scan_cell = [&](uint32_t first, uint32_t count, bool dense, int X, int Y, int Z, uint32_t rk) {
+    if constexpr (!DENSE) {  // no dense cell in the map: the cell's records, split over the lanes
+      constexpr int D = FMX_MATCH_DEPTH_PLAIN;
+      const uint32_t end = first + count;
+      n_cand += count / G + (g < (int)(count % G) ? 1 : 0);
+      uint32_t i = first + g;
+      for (; i + (D - 1) * G < end; i += D * G) {
+        double4 pr[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) pr[d] = M.pos[i + d * G];
+#pragma unroll
+        for (int d = 0; d < D; ++d) fold(pr[d], i + d * G, rk);
+      }
+      for (; i < end; i += G) fold(M.pos[i], i, rk);
+      group_min();
+      return;
+    }
+    constexpr int kPer = kSubCells / G;  // sub-cells per lane
+    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(M.pos + first);
+    const uint32_t base = dense ? first + kHdr : first;
+    const bool sorted = DENSE && dense && hdr[0] != kUnsorted;
+    // per sub-cell lower bound (1e-9 slack over the fp rounding of the sub-cell index)
+    auto axis_lb = [&](double q, int C, int i) {
+      const double lo = C * a.w + i * sw, hi = lo + sw;
+      const double d = q < lo ? lo - q : (q > hi ? q - hi : 0.0);
+      const double m = fmax(d - 1e-9, 0.0);
+      return m * m;
+    };
+    auto sub_lb = [&](int sub) {
+      return axis_lb(wq[0], X, sub % kSubPerAxis) + axis_lb(wq[1], Y, (sub / kSubPerAxis) % kSubPerAxis) +
+             axis_lb(wq[2], Z, sub / (kSubPerAxis * kSubPerAxis));
+    };
+    auto sub_beg = [&](int sub) { return sub == 0 ? 0u : hd[sub - 1]; };
+    // A sorted dense cell's sub-cell ranges in hd[] (LDS; coalesced copy: lane g
+    // copies entries [g * kPer, (g + 1) * kPer)); any other cell is one range.  The
+    // s_waitcnt + memory clobbers order the copy after the previous cell's reads and
+    // before the other lanes' reads.
+    if (sorted) {
+      if (g == 0) n_probe += kHdr * 32 / 64;  // the header's 64-B lines (byte model)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (kPer >= 4) {
+#pragma unroll
+        for (int u = 0; u < kPer; u += 4)
+          *reinterpret_cast<uint4*>(hd + g * kPer + u) = *reinterpret_cast<const uint4*>(hdr + g * kPer + u);
+      } else {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) hd[g * kPer + u] = hdr[g * kPer + u];
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    const int qs = sub_axis(wq[0], X * a.w, sw) + kSubPerAxis * sub_axis(wq[1], Y * a.w, sw) +
+                   kSubPerAxis * kSubPerAxis * sub_axis(wq[2], Z * a.w, sw);
+    // Walk 0: the whole cell, or (sorted) the query's own / nearest sub-cell.  Walk 1
+    // (sorted only): every other sub-cell whose box can still hold a closer record.
+    // A walk is ONE virtual range — the chosen ranges' records concatenated in
+    // sub-cell order, split over the group's lanes, FMX_MATCH_DEPTH loads in flight
+    // per lane across range boundaries — then one group min.
+    for (int wk = 0; wk < (sorted ? 2 : 1); ++wk) {
+      uint64_t mask = 0;
+      uint32_t tot = 0;
+      if (!sorted) {
+        mask = 1;
+        tot = first + count - base;
+      } else if (wk == 0) {
+        const uint32_t s0 = sub_beg(qs), e0 = hd[qs];
+        if (e0 > s0 && sub_lb(qs) <= best) {
+          mask = 1ull << qs;
+          tot = e0 - s0;
+        }
+      } else {  // lane g bounds sub-cells g, g + G, ...; a ballot per stride
+#pragma unroll 1
+        for (int u = 0; u < kPer; ++u) {
+          const int sub = u * G + g;
+          const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
+          const bool lv = sub != qs && e0 > s0 && sub_lb(sub) <= best;
+          if (lv) tot += e0 - s0;
+          mask |= group_bits<G>(__ballot(lv)) << (u * G);
+        }
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) tot += __shfl_xor(tot, o, G);
+      }
+      if (tot == 0) continue;
+      if (tot > cap) {  // a heavy walk: the whole query goes to a wave of its own
+        heavy = true;
+        return;
+      }
+      int k = __ffsll((unsigned long long)mask) - 1;
+      uint32_t ks = sorted ? sub_beg(k) : 0u, ke = sorted ? hd[k] : tot, vbase = 0;  // (not sorted: never advances)
+      auto locate = [&](uint32_t v) {  // v ascending per lane
+        while (v - vbase >= ke - ks) {
+          vbase += ke - ks;
+          mask &= mask - 1;
+          k = __ffsll((unsigned long long)mask) - 1;
+          ks = sub_beg(k);
+          ke = hd[k];
+        }
+        return base + ks + (v - vbase);
+      };
+      n_cand += tot / G + ((uint32_t)g < tot % G ? 1 : 0);
+      constexpr int D = FMX_MATCH_DEPTH;
+      uint32_t v = g;
+      for (; v + (D - 1) * G < tot; v += D * G) {
+        uint32_t ix[D];
+        double4 pr[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) ix[d] = locate(v + d * G);
+#pragma unroll
+        for (int d = 0; d < D; ++d) pr[d] = M.pos[ix[d]];
+#pragma unroll
+        for (int d = 0; d < D; ++d) fold(pr[d], ix[d], rk);
+      }
+      for (; v < tot; v += G) {
+        const uint32_t i = locate(v);
+        fold(M.pos[i], i, rk);
+      }
+      group_min();
+    }
+  };
+  const bool inr = key_in_range(bx, by, bz);
+  // lower bound on d^2 from the query to any point of the cell at shift s
+  auto shift_lb = [&](int s) {
+    double lb = 0.0;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      // distance from the query to its cell's face on the side of the shift (recomputed
+      // here rather than kept live: registers)
+      const int sa = c_shift[s][ax];
+      const int ba = ax == 0 ? bx : (ax == 1 ? by : bz);
+      const double hi = (ba + 1) * a.w - wq[ax], lo = wq[ax] - ba * a.w;
+      const double e = sa > 0 ? hi + (sa - 1) * a.w : (sa < 0 ? lo + (-sa - 1) * a.w : 0.0);
+      const double m = fmax(e - 1e-9, 0.0);
+      lb += m * m;
+    }
+    return lb;
+  };
+  // The cells in passes of increasing lower bound — the query's own cell (shift 0,
+  // visited first by the reference too), ring-1 faces (shifts 1..6), ring-1 edges +
+  // corners (7..26), then ring 2 (27..124) when the map uses half-width cells — each
+  // pass pruned against the best found so far.  In a pass a lane bounds and probes
+  // its shifts in parallel, then the group walks every surviving cell together
+  // (records split over the lanes), re-checking each bound against the shared best.
+  // One loop over the passes, so the cell walk is emitted once.
+  const int npass = a.rings >= 2 ? 4 : 3;
+  for (int ip = 0; ip < npass && !heavy; ++ip) {
+    const int s_begin = ip == 0 ? 0 : (ip == 1 ? 1 : (ip == 2 ? 7 : 27));
+    const int s_end = ip == 0 ? 1 : (ip == 1 ? 7 : (ip == 2 ? 27 : 125));
+    for (int s0 = s_begin; s0 < s_end && !heavy; s0 += G) {  // one shift per lane per chunk
+      uint32_t vf = 0, vc = 0;
+      bool vd = false;
+      double vlb = INFINITY;
+      const int s = s0 + g;
+      if (inr && s < s_end) {
+        const double lb = shift_lb(s);
+        if (lb <= best) {  // else conservative: no point inside can win
+          probe(c_shift[s][0], c_shift[s][1], c_shift[s][2], vf, vc, vd);
+          vlb = lb;
+        }
+      }
+      // small cells (<= kSmallCell records): the lane that probed one folds its
+      // records itself, every lane's loads in flight together, one group min after;
+      // the argmin on (d^2, tie key) does not depend on the folding order
+      const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
+      if (small) {
+        const uint32_t rk = srank(c_shift[s][0], c_shift[s][1], c_shift[s][2]);
+        double4 pr[kSmallCell];
+#pragma unroll
+        for (int u = 0; u < kSmallCell; ++u)
+          if (u < (int)vc) pr[u] = M.pos[vf + u];
+#pragma unroll
+        for (int u = 0; u < kSmallCell; ++u)
+          if (u < (int)vc) fold(pr[u], vf + u, rk);
+        n_cand += vc;
+      }
+      if (group_bits<G>(__ballot(small))) group_min();
+      uint64_t live = group_bits<G>(__ballot(vc > (uint32_t)kSmallCell));  // larger cells: walked by the group
+      while (live) {
+        const int l = __ffsll((unsigned long long)live) - 1;
+        live &= live - 1;
+        const double lb = __shfl(vlb, l, G);
+        if (lb > best) continue;  // best is group-uniform here
+        const uint32_t cnt = __shfl(vc, l, G);
+        const uint32_t first = __shfl(vf, l, G);
+        const bool dn = __shfl((int)vd, l, G) != 0;
+        const int sl = s0 + l;
+        scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2],
+                  srank(c_shift[sl][0], c_shift[sl][1], c_shift[sl][2]));
+        if (heavy) break;
+      }
+    }
+  }
+  return !heavy;
+}
+
 // DENSE = false: the map has no dense cell (known from the build's pinned info word),
 // so the sub-cell walk is compiled out (fewer registers, more waves in flight).
-template <bool DENSE>
+//
+// Heavy queries (DENSE): a query whose search reaches a cell walk of more than
+// kHeavyCap records (a dense ground cell near the sensor: ~500 candidates) would hold
+// its whole block for ~40 us at kGroup lanes and set the launch's span.  Its group
+// abandons it, and once the wave's other queries are done the whole wave (64 lanes,
+// 8x the loads in flight) searches it again from the start; its result, pair count
+// and insert flag stay in this block, so the bookkeeping below is unchanged.
+#ifndef FMX_HEAVY_CAP
+#define FMX_HEAVY_CAP 0  // 0: off (measured slower, DESIGN.md: heavy queries cluster in whole waves)
+#endif
+constexpr uint32_t kHeavyCap = FMX_HEAVY_CAP;
+
+#include "factor_rows.hpp"
+
+// FUSED: the match and the single-pose linearization at the SAME pose in one launch,
+// for callers that only want the summed 7 x 7 system (fmx_match without counts, then
+// fmx_linearize_matched at the match pose: the sharded C5 loop).  No per-query result
+// is written: each lane moves its accepted match back to the map scan's frame
+// (matcher.hpp:92-96) and builds the whitened row(s) a = [H_j b] / sigma of its
+// PlanePoint / PointPoint (factor.cpp:30-128, gtsam.hpp:67-86, 144-170) exactly as
+// k_linearize_total would from the stored results; the wave's rows go through LDS
+// into v_mfma_f64_16x16x4_f64 (A^T A of 64 rows x 7 columns in 4 registers per lane),
+// waves meet in LDS in a fixed order, block partials + ticket, and the last block sums
+// the partials in block order (deterministic) into G + error.
+struct FusedArgs {
+  const double* poses;  // map scan poses [K][12] (T_i)
+  double inv;           // 1 / sigma
+  double* bpart;        // [block][32]
+  double* gpart;        // [block group][32]
+  uint32_t* gticket;    // [block group], self-resetting
+  uint32_t* ticket;     // self-resetting
+  double* out;          // 28 G entries + error (pinned host memory, or a device buffer to all-reduce)
+  uint32_t* flag;       // completion word (null: none)
+  uint32_t seq;
+};
+constexpr int kFzLd = 32;    // doubles per block partial (28 used)
+constexpr uint32_t kFzGroup = 64;  // blocks per first-level reduction group
+// Sum entry e (< 28) of n partials src[i * kFzLd + e], i in [0, n), in a fixed order:
+// the block's first 9 * 28 threads take strided subsets (several loads in flight
+// each), then 28 threads add the 9 subset sums in order.  Returns the sum in threads
+// tid < 28 (entry tid); every thread of the block must call it.
+__device__ __forceinline__ double fz_sum_partials(const double* src, uint32_t n, double (*sq)[28]) {
+  constexpr int kSub = kMatchThreads / 28;
+  const int tid = threadIdx.x;
+  if (tid < kSub * 28) {
+    const int e = tid % 28, j = tid / 28;
+    double sum = 0.0;
+#pragma unroll 8
+    for (uint32_t b = j; b < n; b += kSub)
+      sum += __longlong_as_double((long long)__hip_atomic_load(
+          reinterpret_cast<const unsigned long long*>(src + (size_t)b * kFzLd + e), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT));
+    sq[j][e] = sum;
+  }
+  __syncthreads();
+  double sum = 0.0;
+  if (tid < 28) {
+    sum = sq[0][tid];
+#pragma unroll
+    for (int j = 1; j < kSub; ++j) sum += sq[j][tid];
+  }
+  __syncthreads();
+  return sum;
+}
+constexpr int kFzStride = 7;  // doubles per staged row
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// sum over the wave's 64 staged rows of a a^T (7 x 7 in the top-left of a 16 x 16 MFMA
+// tile): lane l feeds a_{4t + l/16}[l % 16] (0 past column 6) as both operands of MFMA t
+__device__ __forceinline__ void fz_stage_mfma(double* __restrict__ rows, const double (&av)[7], bool valid,
+                                              f64x4 (&acc)[2]) {
+  const int lane = lane_id();
+  double* mine = rows + lane * kFzStride;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) mine[i] = valid ? av[i] : 0.0;
+  __builtin_amdgcn_wave_barrier();
+  const int col = lane & 15;
+  const double* src = rows + (lane >> 4) * kFzStride + (col < 7 ? col : 0);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    double v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = src[4 * (8 * h + t) * kFzStride];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const double x = col < 7 ? v[t] : 0.0;
+      acc[t & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, acc[t & 1], 0, 0, 0);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <bool DENSE, bool FUSED = false>
 __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
                                                          const float4* __restrict__ q_pt,
@@ -605,11 +996,12 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
                                                          uint32_t* __restrict__ mcnt, uint32_t* __restrict__ mticket,
                                                          uint32_t* __restrict__ host_counts,
                                                          uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off,
-                                                         uint32_t* __restrict__ thist, SortOut so) {
+                                                         uint32_t* __restrict__ thist, SortOut so, FusedArgs fz) {
   extern __shared__ uint32_t s_hist[];  // [K]
   const double* Tj = a.Tj;
   const bool planar = blockIdx.x < a.nb_pl;
-  const uint32_t qi = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kQPB + threadIdx.x / kGroup;
+  const uint32_t qb = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kQPB;  // the block's first query
+  const uint32_t qi = qb + threadIdx.x / kGroup;
   const int g = threadIdx.x % kGroup;
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
   const MapView& M = planar ? mp : mt;
@@ -619,321 +1011,72 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   if (threadIdx.x == 0) s_ins = 0;
   __syncthreads();
   const uint32_t t_begin = (uint32_t)wall_clock64();
-  uint32_t n_probe = 0, n_cand = 0;
-#ifdef FMX_MATCH_SPLIT  // diagnostic build: candidates of pass 0, of walk 1, of passes >= 1
-  uint32_t n_c0 = 0, n_cw1 = 0, n_cp12 = 0;
-  int cur_pass = 0;
-#define SPLIT_ADD(v, wk) (cur_pass == 0 ? n_c0 : n_cp12) += (v), n_cw1 += (wk) == 1 ? (v) : 0u
-#else
-#define SPLIT_ADD(v, wk) ((void)0)
-#endif
-  if (qi < nq) {
-    const float4 lq = planar ? q_pl[qi] : q_pt[qi];
-    double wq[3];
+  uint32_t n_probe = 0, n_cand = 0, heavy_cand = 0;
+  auto world_query = [&](uint32_t q, double (&wq)[3]) {
+    const float4 lq = planar ? q_pl[q] : q_pt[q];
     d_xform(Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
-    const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
-    double best = a.bound;
-    // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
-    // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
-    // the record's build order (= insertion order inside a voxel, map.tpp:41-52)
-    uint32_t best_rid = 0xFFFFFFFFu, best_i = 0xFFFFFFFFu;
-    const int sh = a.rings >= 2 ? 1 : 0;  // cells of w/2: reference voxel = cell >> 1
-    auto srank = [&](int sx, int sy, int sz) -> uint32_t {
-      const int dx = ((bx + sx) >> sh) - (bx >> sh), dy = ((by + sy) >> sh) - (by >> sh),
-                dz = ((bz + sz) >> sh) - (bz >> sh);
-      return (uint32_t)c_refrank[(dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)] << 27;
-    };
-    // one bucket read per probe: key, the cell's two boundaries and its dense bit in
-    // flight together; a bucket of another build epoch ends the chain (empty)
-    auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count, bool& dense) {
-      const int X = bx + sx, Y = by + sy, Z = bz + sz;
-      const unsigned long long key = brick_key(X, Y, Z, M.epoch);
-      const uint32_t ci = brick_cell(X, Y, Z);
-      uint64_t h = mix64(key) & M.mask;
-      first = 0;
-      count = 0;
-      dense = false;
-      for (;;) {
-        ++n_probe;
-        const Brick* b = M.bricks + h;
-        const unsigned long long k = b->key;
-        const uint32_t b0 = b->beg[ci], b1 = b->beg[ci + 1], dm = b->dense;
-        if (k == key) {
-          first = b0;
-          count = b1 - b0;
-          dense = (dm >> ci) & 1;
-          return;
-        }
-        if (key_epoch(k) != M.epoch) return;
-        h = (h + 1) & M.mask;
+  };
+  // the query's result (one lane): the match moved back to its scan's frame
+  // (matcher.hpp:92-96), acceptance (:103-105), insert decision (map.tpp:160-163)
+  auto emit = [&](uint32_t q, double best, uint32_t best_i) {
+    const bool found = best_i != 0xFFFFFFFFu;
+    int32_t pair = -1;
+    double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
+    if (found) {
+      const double4 p = M.pos[best_i];
+      const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);  // in flight with p
+      const uint32_t sg = (uint32_t)((unsigned long long)p.w >> 32);     // the record's segment
+      const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
+      double o[3];
+      d_xform(Ti, p.x, p.y, p.z, o);
+      pi = make_double4(o[0], o[1], o[2], 0.0);
+      if (planar) {
+        d_rot(Ti, n.x, n.y, n.z, o);
+        ni = make_double4(o[0], o[1], o[2], 0.0);
       }
-    };
-    // a record is one double4: world position + its build order in .w (exact in a
-    // double), so a candidate test is one 32-B load
-    auto fold = [&](const double4& p, uint32_t i, uint32_t rk) {
-      const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
-      const double d2 = (dx * dx + dz * dz) + dy * dy;
-      const uint32_t tk = rk | ((uint32_t)(unsigned long long)p.w & 0x07FFFFFFu);  // build order: low bits
-      if (d2 <= best && (d2 < best || tk < best_rid)) {
-        best = d2;
-        best_rid = tk;
-        best_i = i;
-      }
-    };
-    // argmin over (d^2, tie key) across the group's lanes with DPP moves (VALU
-    // latency, no LDS crossbar): [row_mirror l <-> 15-l,] row_half_mirror l <-> 7-l,
-    // quad xor 2, quad xor 1 leave every lane with the group minimum
-    auto group_min = [&]() {
-      auto step = [&](auto ctrl_tag) {
-        constexpr int CTRL = decltype(ctrl_tag)::value;
-        const long long bb = __double_as_longlong(best);
-        const int blo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)bb, CTRL, 0xF, 0xF, false);
-        const int bhi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(bb >> 32), CTRL, 0xF, 0xF, false);
-        const double ob = __longlong_as_double((long long)(((unsigned long long)(uint32_t)bhi << 32) | (uint32_t)blo));
-        const uint32_t orid = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_rid, CTRL, 0xF, 0xF, false);
-        const uint32_t oi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_i, CTRL, 0xF, 0xF, false);
-        if (oi != 0xFFFFFFFFu && (best_i == 0xFFFFFFFFu || ob < best || (ob == best && orid < best_rid))) {
-          best = ob;
-          best_rid = orid;
-          best_i = oi;
-        }
-      };
-      static_assert(kGroup == 1 || kGroup == 2 || kGroup == 4 || kGroup == 8 || kGroup == 16,
-                    "DPP reduction assumes 1-, 2-, 4-, 8- or 16-lane groups");
-      if constexpr (kGroup == 16) step(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
-      if constexpr (kGroup >= 8) step(std::integral_constant<int, 0x141>{});  // row_half_mirror
-      if constexpr (kGroup >= 4) step(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
-      if constexpr (kGroup >= 2) step(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
-    };
-    // Records of one cell, walked by the whole group (group-uniform arguments).  A
-    // dense cell (k_map_dense) starts with a header of its 64 sub-cell ends: the
-    // query's own sub-cell first, then every other sub-cell whose box lower bound does
-    // not exceed the best so far, each group-walked (lane g holds sub-cells 8g..8g+7's
-    // ends; with kGroup < 8 a lane holds several such blocks).
-    const double sw = a.w / kSubPerAxis;
-    uint32_t* hd = s_hdr[DENSE ? threadIdx.x / kGroup : 0];  // this query's copy of a dense cell's header
-    auto scan_cell = [&](uint32_t first, uint32_t count, bool dense, int X, int Y, int Z, uint32_t rk) {
-      if constexpr (!DENSE) {  // no dense cell in the map: the cell's records, split over the lanes
-        constexpr int D = FMX_MATCH_DEPTH_PLAIN;
-        const uint32_t end = first + count;
-        n_cand += count / kGroup + (g < (int)(count % kGroup) ? 1 : 0);
-        SPLIT_ADD(count / kGroup + (g < (int)(count % kGroup) ? 1 : 0), 0);
-        uint32_t i = first + g;
-        for (; i + (D - 1) * kGroup < end; i += D * kGroup) {
-          double4 pr[D];
-#pragma unroll
-          for (int d = 0; d < D; ++d) pr[d] = M.pos[i + d * kGroup];
-#pragma unroll
-          for (int d = 0; d < D; ++d) fold(pr[d], i + d * kGroup, rk);
-        }
-        for (; i < end; i += kGroup) fold(M.pos[i], i, rk);
-        group_min();
-        return;
-      }
-      constexpr int kPer = kSubCells / kGroup;  // sub-cells per lane
-      const uint32_t* hdr = reinterpret_cast<const uint32_t*>(M.pos + first);
-      const uint32_t base = dense ? first + kHdr : first;
-      const bool sorted = DENSE && dense && hdr[0] != kUnsorted;
-      // per sub-cell lower bound (1e-9 slack over the fp rounding of the sub-cell index)
-      auto axis_lb = [&](double q, int C, int i) {
-        const double lo = C * a.w + i * sw, hi = lo + sw;
-        const double d = q < lo ? lo - q : (q > hi ? q - hi : 0.0);
-        const double m = fmax(d - 1e-9, 0.0);
-        return m * m;
-      };
-      auto sub_lb = [&](int sub) {
-        return axis_lb(wq[0], X, sub % kSubPerAxis) + axis_lb(wq[1], Y, (sub / kSubPerAxis) % kSubPerAxis) +
-               axis_lb(wq[2], Z, sub / (kSubPerAxis * kSubPerAxis));
-      };
-      auto sub_beg = [&](int sub) { return sub == 0 ? 0u : hd[sub - 1]; };
-      // A sorted dense cell's sub-cell ranges in hd[] (LDS; coalesced copy: lane g
-      // copies entries [g * kPer, (g + 1) * kPer)); any other cell is one range.  The
-      // s_waitcnt + memory clobbers order the copy after the previous cell's reads and
-      // before the other lanes' reads.
-      if (sorted) {
-        if (g == 0) n_probe += kHdr * 32 / 64;  // the header's 64-B lines (byte model)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (kPer >= 4) {
-#pragma unroll
-          for (int u = 0; u < kPer; u += 4)
-            *reinterpret_cast<uint4*>(hd + g * kPer + u) = *reinterpret_cast<const uint4*>(hdr + g * kPer + u);
-        } else {
-#pragma unroll
-          for (int u = 0; u < kPer; ++u) hd[g * kPer + u] = hdr[g * kPer + u];
-        }
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      }
-      const int qs = sub_axis(wq[0], X * a.w, sw) + kSubPerAxis * sub_axis(wq[1], Y * a.w, sw) +
-                     kSubPerAxis * kSubPerAxis * sub_axis(wq[2], Z * a.w, sw);
-      const int gsh = (lane_id() / kGroup) * kGroup;
-      // Walk 0: the whole cell, or (sorted) the query's own / nearest sub-cell.  Walk 1
-      // (sorted only): every other sub-cell whose box can still hold a closer record.
-      // A walk is ONE virtual range — the chosen ranges' records concatenated in
-      // sub-cell order, split over the group's lanes, FMX_MATCH_DEPTH loads in flight
-      // per lane across range boundaries — then one group min.
-      for (int wk = 0; wk < (sorted ? 2 : 1); ++wk) {
-        uint64_t mask = 0;
-        uint32_t tot = 0;
-        if (!sorted) {
-          mask = 1;
-          tot = first + count - base;
-        } else if (wk == 0) {
-          const uint32_t s0 = sub_beg(qs), e0 = hd[qs];
-          if (e0 > s0 && sub_lb(qs) <= best) {
-            mask = 1ull << qs;
-            tot = e0 - s0;
-          }
-        } else {  // lane g bounds sub-cells g, g + kGroup, ...; a ballot per stride
-#pragma unroll 1
-          for (int u = 0; u < kPer; ++u) {
-            const int sub = u * kGroup + g;
-            const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
-            const bool lv = sub != qs && e0 > s0 && sub_lb(sub) <= best;
-            if (lv) tot += e0 - s0;
-            mask |= ((__ballot(lv) >> gsh) & ((1ull << kGroup) - 1)) << (u * kGroup);
-          }
-#pragma unroll
-          for (int o = 1; o < kGroup; o <<= 1) tot += __shfl_xor(tot, o, kGroup);
-        }
-        if (tot == 0) continue;
-        int k = __ffsll((unsigned long long)mask) - 1;
-        uint32_t ks = sorted ? sub_beg(k) : 0u, ke = sorted ? hd[k] : tot, vbase = 0;  // (not sorted: never advances)
-        auto locate = [&](uint32_t v) {  // v ascending per lane
-          while (v - vbase >= ke - ks) {
-            vbase += ke - ks;
-            mask &= mask - 1;
-            k = __ffsll((unsigned long long)mask) - 1;
-            ks = sub_beg(k);
-            ke = hd[k];
-          }
-          return base + ks + (v - vbase);
-        };
-        n_cand += tot / kGroup + ((uint32_t)g < tot % kGroup ? 1 : 0);
-        SPLIT_ADD(tot / kGroup + ((uint32_t)g < tot % kGroup ? 1 : 0), wk);
-        constexpr int D = FMX_MATCH_DEPTH;
-        uint32_t v = g;
-        for (; v + (D - 1) * kGroup < tot; v += D * kGroup) {
-          uint32_t ix[D];
-          double4 pr[D];
-#pragma unroll
-          for (int d = 0; d < D; ++d) ix[d] = locate(v + d * kGroup);
-#pragma unroll
-          for (int d = 0; d < D; ++d) pr[d] = M.pos[ix[d]];
-#pragma unroll
-          for (int d = 0; d < D; ++d) fold(pr[d], ix[d], rk);
-        }
-        for (; v < tot; v += kGroup) {
-          const uint32_t i = locate(v);
-          fold(M.pos[i], i, rk);
-        }
-        group_min();
-      }
-    };
-    const bool inr = key_in_range(bx, by, bz);
-    // lower bound on d^2 from the query to any point of the cell at shift s
-    auto shift_lb = [&](int s) {
-      double lb = 0.0;
-#pragma unroll
-      for (int ax = 0; ax < 3; ++ax) {
-        // distance from the query to its cell's face on the side of the shift (recomputed
-        // here rather than kept live: registers)
-        const int sa = c_shift[s][ax];
-        const int ba = ax == 0 ? bx : (ax == 1 ? by : bz);
-        const double hi = (ba + 1) * a.w - wq[ax], lo = wq[ax] - ba * a.w;
-        const double e = sa > 0 ? hi + (sa - 1) * a.w : (sa < 0 ? lo + (-sa - 1) * a.w : 0.0);
-        const double m = fmax(e - 1e-9, 0.0);
-        lb += m * m;
-      }
-      return lb;
-    };
-    // The cells in passes of increasing lower bound — the query's own cell (shift 0,
-    // visited first by the reference too), ring-1 faces (shifts 1..6), ring-1 edges +
-    // corners (7..26), then ring 2 (27..124) when the map uses half-width cells — each
-    // pass pruned against the best found so far.  In a pass a lane bounds and probes
-    // its shifts in parallel, then the group walks every surviving cell together
-    // (records split over the lanes), re-checking each bound against the shared best.
-    // One loop over the passes, so the cell walk is emitted once.
-    const int npass = a.rings >= 2 ? 4 : 3;
-    for (int ip = 0; ip < npass; ++ip) {
-#ifdef FMX_MATCH_SPLIT
-      cur_pass = ip;
-#endif
-      const int s_begin = ip == 0 ? 0 : (ip == 1 ? 1 : (ip == 2 ? 7 : 27));
-      const int s_end = ip == 0 ? 1 : (ip == 1 ? 7 : (ip == 2 ? 27 : 125));
-      for (int s0 = s_begin; s0 < s_end; s0 += kGroup) {  // one shift per lane per chunk
-        uint32_t vf = 0, vc = 0;
-        bool vd = false;
-        double vlb = INFINITY;
-        const int s = s0 + g;
-        if (inr && s < s_end) {
-          const double lb = shift_lb(s);
-          if (lb <= best) {  // else conservative: no point inside can win
-            probe(c_shift[s][0], c_shift[s][1], c_shift[s][2], vf, vc, vd);
-            vlb = lb;
-          }
-        }
-        // small cells (<= kSmallCell records): the lane that probed one folds its
-        // records itself, every lane's loads in flight together, one group min after;
-        // the argmin on (d^2, tie key) does not depend on the folding order
-        const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
-        if (small) {
-          const uint32_t rk = srank(c_shift[s][0], c_shift[s][1], c_shift[s][2]);
-          double4 pr[kSmallCell];
-#pragma unroll
-          for (int u = 0; u < kSmallCell; ++u)
-            if (u < (int)vc) pr[u] = M.pos[vf + u];
-#pragma unroll
-          for (int u = 0; u < kSmallCell; ++u)
-            if (u < (int)vc) fold(pr[u], vf + u, rk);
-          n_cand += vc;
-          SPLIT_ADD(vc, 0);
-        }
-        const int gsh = (lane_id() / kGroup) * kGroup;
-        if ((__ballot(small) >> gsh) & ((1ull << kGroup) - 1)) group_min();
-        uint64_t live = __ballot(vc > (uint32_t)kSmallCell);  // larger cells: walked by the group
-        live = (live >> ((lane_id() / kGroup) * kGroup)) & ((1ull << kGroup) - 1);
-        while (live) {
-          const int l = __ffsll((unsigned long long)live) - 1;
-          live &= live - 1;
-          const double lb = __shfl(vlb, l, kGroup);
-          if (lb > best) continue;  // best is group-uniform here
-          const uint32_t cnt = __shfl(vc, l, kGroup);
-          const uint32_t first = __shfl(vf, l, kGroup);
-          const bool dn = __shfl((int)vd, l, kGroup) != 0;
-          const int sl = s0 + l;
-          scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2],
-                    srank(c_shift[sl][0], c_shift[sl][1], c_shift[sl][2]));
-        }
+      if (best < a.max_d2) pair = (int32_t)sg;
+    }
+    const uint32_t gq = planar ? q : a.nq_pl + q;
+    m_pair[gq] = pair;
+    m_d2[gq] = found ? best : DBL_MAX;
+    m_pi[gq] = pi;
+    if (planar) m_ni[q] = ni;
+    const bool ins = !found || best > a.min_d2;
+    m_ins[gq] = ins ? 1 : 0;
+    if (ins) atomicAdd(&s_ins, 1u);
+    if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
+  };
+  bool heavy = false;
+  double best = a.bound;
+  uint32_t best_i = 0xFFFFFFFFu;
+  if (qi < nq) {
+    double wq[3];
+    world_query(qi, wq);
+    uint32_t best_rid = 0xFFFFFFFFu;
+    heavy = !nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0],
+                                       DENSE && kHeavyCap ? kHeavyCap : 0xFFFFFFFFu, best, best_rid, best_i,
+                                       n_probe, n_cand);
+  }
+  if constexpr (DENSE && kGroup < kWave && kHeavyCap > 0) {
+    // the wave's abandoned queries, one at a time, 64 lanes each; the result goes back
+    // to the query's own group leader (lane l)
+    uint64_t hv = __ballot(heavy && g == 0);
+    const uint32_t c0 = n_cand;
+    while (hv) {
+      const int l = __ffsll((unsigned long long)hv) - 1;
+      hv &= hv - 1;
+      const uint32_t gi = (threadIdx.x / kWave) * (kWave / kGroup) + l / kGroup;  // query slot in the block
+      double wq[3];
+      world_query(qb + gi, wq);
+      double hb = a.bound;
+      uint32_t hr = 0xFFFFFFFFu, hi = 0xFFFFFFFFu;
+      nn_search<kWave, DENSE>(a, M, wq, lane_id(), s_hdr[gi], 0xFFFFFFFFu, hb, hr, hi, n_probe, n_cand);
+      if (lane_id() == l) {
+        best = hb;
+        best_i = hi;
       }
     }
-    if (g == 0) {
-      const bool found = best_i != 0xFFFFFFFFu;
-      int32_t pair = -1;
-      double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
-      if (found) {
-        const double4 p = M.pos[best_i];
-        const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);  // in flight with p
-        const uint32_t sg = (uint32_t)((unsigned long long)p.w >> 32);     // the record's segment
-        const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
-        double o[3];
-        d_xform(Ti, p.x, p.y, p.z, o);
-        pi = make_double4(o[0], o[1], o[2], 0.0);
-        if (planar) {
-          d_rot(Ti, n.x, n.y, n.z, o);
-          ni = make_double4(o[0], o[1], o[2], 0.0);
-        }
-        if (best < a.max_d2) pair = (int32_t)sg;
-      }
-      const uint32_t gq = planar ? qi : a.nq_pl + qi;
-      m_pair[gq] = pair;
-      m_d2[gq] = found ? best : DBL_MAX;
-      m_pi[gq] = pi;
-      if (planar) m_ni[qi] = ni;
-      const bool ins = !found || best > a.min_d2;
-      m_ins[gq] = ins ? 1 : 0;
-      if (ins) atomicAdd(&s_ins, 1u);
-      if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
-    }
+    heavy_cand = wave_sum(n_cand - c0);  // the heavy queries' candidates (diagnostics)
   }
   // work counters for the algorithmic-byte model and the match diagnostics (one plain
   // store per block, summed on the host): probes, candidate records, the largest
@@ -944,6 +1087,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   for (int o = 1; o < kGroup; o <<= 1) qc += __shfl_xor(qc, o, 64);
 #pragma unroll
   for (int o = kGroup; o < kWave; o <<= 1) qc = max(qc, (uint32_t)__shfl_xor(qc, o, 64));
+  qc = max(qc, heavy_cand);
   const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
   if (lane_id() == 0) {
     s_work[0][threadIdx.x / kWave] = wp;
@@ -962,18 +1106,109 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     w4[0] = make_uint4(tp, tc, mq, 0u);
     w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), 0u, 0u);
   }
-#ifdef FMX_MATCH_SPLIT
-  __syncthreads();  // after thread 0's plain stores of this block's words
-  {
-    const uint32_t s0 = wave_sum(n_c0), s1 = wave_sum(n_cw1), s2 = wave_sum(n_cp12);
-    uint32_t* wb = work + 8 * blockIdx.x;
-    if (lane_id() == 0) {
-      atomicAdd(wb + 3, s0);
-      atomicAdd(wb + 6, s1);
-      atomicAdd(wb + 7, s2);
+  if constexpr (!FUSED) {
+    if (qi < nq && g == 0) emit(qi, best, best_i);
+  } else {
+    static_assert(kGroup == 1, "the fused match + linearization runs one lane per query");
+    // this lane's accepted match in its map scan's frame, then its row(s)
+    const bool acc_q = qi < nq && best_i != 0xFFFFFFFFu && best < a.max_d2;
+    double pi[3] = {0, 0, 0}, ni[3] = {0, 0, 0}, pj[3] = {0, 0, 0};
+    const double* Ti = fz.poses;
+    if (acc_q) {
+      const double4 p = M.pos[best_i];
+      const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);
+      const uint32_t sg = (uint32_t)((unsigned long long)p.w >> 32);
+      const double* Tinv = inv_poses + 12 * sg;  // matcher.hpp:95
+      d_xform(Tinv, p.x, p.y, p.z, pi);
+      if (planar) d_rot(Tinv, n.x, n.y, n.z, ni);
+      Ti = fz.poses + 12 * sg;
+      const float4 lq = planar ? q_pl[qi] : q_pt[qi];
+      pj[0] = (double)lq.x;
+      pj[1] = (double)lq.y;
+      pj[2] = (double)lq.z;
     }
+    __shared__ double s_rows[kMatchThreads / kWave][kWave * kFzStride];
+    __shared__ double s_g[kMatchThreads / kWave][28];
+    double* rows = s_rows[threadIdx.x / kWave];
+    f64x4 accs[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
+    double H[12], av[7];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) H[i] = 0.0;
+    if (planar) {  // block-uniform: a block holds one feature type
+      double r = 0.0;
+      if (acc_q) plane_row<1>(Ti, Tj, pi, ni, pj, r, H);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) av[c] = H[6 + c] * fz.inv;
+      av[6] = -r * fz.inv;
+      fz_stage_mfma(rows, av, acc_q, accs);
+    } else {
+      double wpi[3], wpj[3];
+      d_xform(Ti, pi[0], pi[1], pi[2], wpi);
+      d_xform(Tj, pj[0], pj[1], pj[2], wpj);
+      for (int ax = 0; ax < 3; ++ax) {
+        double r = 0.0;
+        if (acc_q) point_row<1>(Ti, Tj, pi, pj, wpi, wpj, ax, r, H);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) av[c] = H[6 + c] * fz.inv;
+        av[6] = -r * fz.inv;
+        fz_stage_mfma(rows, av, acc_q, accs);
+      }
+    }
+    const f64x4 acc = accs[0] + accs[1];
+    {
+      const int col = lane_id() & 15;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane_id() >> 4) + 4 * r;
+        if (rr <= col && col < 7) s_g[threadIdx.x / kWave][rr * 7 - rr * (rr - 1) / 2 + (col - rr)] = acc[r];
+      }
+    }
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (tid < 28) {
+      double bp = s_g[0][tid];
+#pragma unroll
+      for (int i = 1; i < kMatchThreads / kWave; ++i) bp += s_g[i][tid];
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(fz.bpart + (size_t)blockIdx.x * kFzLd + tid),
+                         (unsigned long long)__double_as_longlong(bp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // two-level deterministic reduction: the last block of each group of kFzGroup
+    // blocks sums the group's partials (block order), the last group finisher sums the
+    // group partials (group order) into G + error
+    __shared__ int s_flast;
+    __shared__ double s_q[kMatchThreads / 28][28];
+    const uint32_t grp = blockIdx.x / kFzGroup, ngrp = (gridDim.x + kFzGroup - 1) / kFzGroup;
+    const uint32_t gsize = min(kFzGroup, gridDim.x - grp * kFzGroup);
+    if (tid == 0)
+      s_flast = __hip_atomic_fetch_add(fz.gticket + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
+    __syncthreads();
+    if (!s_flast) return;
+    const double gs = fz_sum_partials(fz.bpart + (size_t)grp * kFzGroup * kFzLd, gsize, s_q);
+    if (tid < 28)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(fz.gpart + (size_t)grp * kFzLd + tid),
+                         (unsigned long long)__double_as_longlong(gs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_store(fz.gticket + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flast = __hip_atomic_fetch_add(fz.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngrp - 1;
+    }
+    __syncthreads();
+    if (!s_flast) return;
+    const double tot = fz_sum_partials(fz.gpart, ngrp, s_q);
+    if (tid < 28) {
+      host_store(fz.out + tid, tot);
+      if (tid == 27) host_store(fz.out + 28, 0.5 * tot);  // error = 0.5 ||r / sigma||^2
+    }
+    if (tid == 0) {
+      __hip_atomic_store(fz.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fz.flag) publish_flag(fz.flag, fz.seq);  // fz.out was stored by this wave (threads 0..27)
+    }
+    return;
   }
-#endif
+  __syncthreads();  // every emit's LDS counts are in
   if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
     __hip_atomic_store(ins_blk + blockIdx.x, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int t = planar ? 0 : 1;
@@ -1548,7 +1783,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     hipLaunchKernelGGL(dense ? k_match<true> : k_match<false>, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
                        c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
                        c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d,
-                       c->ins_blk.p, c->ins_off.p, c->thist.p, so);
+                       c->ins_blk.p, c->ins_off.p, c->thist.p, so, FusedArgs{});
     FMX_HIP(hipGetLastError());
   }
   // no queries: no launch, so zero the counts and insert totals the kernel would write
@@ -1592,6 +1827,84 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->have_match = true;
   c->have_corr = sorted;  // pair-major correspondences for fmx_linearize
   c->have_qo = true;      // query-order correspondences for register_scan
+}
+
+// The match at pose_j fused with its single-pose linearization (k_match<.., FUSED>):
+// the summed 7 x 7 + error to dst (28 + 1 doubles), completion word `flag` (null: none).
+// No per-query results are written, so the context's match state is left as it was.
+void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* dst,
+                         uint32_t* flag, uint32_t seq) {
+  hipStream_t st = c->stream;
+  MatchArgs a;
+  std::memcpy(a.Tj, pose_j34, sizeof(a.Tj));
+  a.w = c->cell_w;
+  a.rings = c->cell_m;
+  a.max_d2 = max_dist * max_dist;
+  a.min_d2 = c->P.min_dist_map * c->P.min_dist_map;
+  const double reach = c->cell_m * c->cell_w;  // = the map's voxel width
+  if (a.max_d2 > reach * reach && c->cell_m > 1)
+    throw StatusError(FMX_E_INVAL, "max_dist exceeds the voxel width of a subdivided map");
+  // only acceptance is observable here: the search is bounded by max_dist alone
+  a.bound = a.max_d2 <= reach * reach ? a.max_d2 : INFINITY;
+  a.nq_pl = c->n_qpl;
+  a.nq_pt = c->n_qpt;
+  a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
+  a.nb_pt = (c->n_qpt + kQPB - 1) / kQPB;
+  a.K = (int)c->K;
+  a.sorted = 0;
+  a.tiles = 0;
+  a.ntl_pl = a.ntl_pt = 0;
+  const uint32_t nb = a.nb_pl + a.nb_pt;
+  c->work.ensure(kWorkWords * (size_t)nb + 8);
+  c->work_blocks = nb;
+  const uint32_t ngrp = (nb + kFzGroup - 1) / kFzGroup;
+  c->bpart.ensure((size_t)(nb + ngrp + 1) * kFzLd);
+  ensure_zeroed(c->ticket, 1, st);
+  ensure_zeroed(c->fz_tickets, ngrp + 1, st);
+  if (nb == 0) {  // nothing to match: a zero system
+    FMX_HIP(hipMemsetAsync(dst, 0, 29 * sizeof(double), st));
+    return;
+  }
+  auto view = [&](int t) {
+    VoxMap& M = c->map;
+    return MapView{reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
+                   M.pos.p, M.nrm.p, M.epoch};
+  };
+  bool dense = c->map.n[0] + c->map.n[1] > 0;
+  if (dense && c->h_mapinfo.p) {
+    const unsigned long long w = __atomic_load_n(c->h_mapinfo.p, __ATOMIC_ACQUIRE);
+    if ((uint32_t)(w >> 32) == c->map.epoch && (uint32_t)w == 0) dense = false;
+  }
+  const FusedArgs fz{c->map_poses_p, 1.0 / sigma, c->bpart.p, c->bpart.p + (size_t)nb * kFzLd, c->fz_tickets.p,
+                     c->ticket.p, dst, flag, seq};
+  const SortOut so{};
+  // bytes: query read (16 B) + 64 B per probe + 32 B per candidate + the accepted
+  // match's normal (32 B, planar) + 32 * 8 B block partials
+  const double nq = (double)c->n_qpl + c->n_qpt;
+  const double bytes = 16.0 * nq + 32.0 * c->n_qpl + 64.0 * c->last_probes + 32.0 * c->last_cands + 256.0 * nb;
+  ProfScope ps(c->prof, PROF_MATCH_LIN, bytes, st);
+#if FMX_MATCH_GROUP == 1
+  {
+    auto kern = dense ? k_match<true, true> : k_match<false, true>;
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(kMatchThreads),
+                       std::max<int>(a.K, 1) * sizeof(uint32_t), st, a, view(0), view(1), c->q_pl_pos.p,
+                       c->q_pt_pos.p, c->map_inv_p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, c->work.p,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, so, fz);
+    FMX_HIP(hipGetLastError());
+  }
+#else
+  (void)view;
+  (void)fz;
+  (void)a;
+  throw StatusError(FMX_E_STATE, "fused match + linearization needs the one-lane-per-query build");
+#endif
+  c->work_copied = c->prof.on;
+  if (c->prof.on) {  // per-block work counters (byte model of the next launch)
+    c->h_work.ensure(kWorkWords * (size_t)nb + 8);
+    FMX_HIP(hipMemcpyAsync(c->h_work.p, c->work.p, kWorkWords * (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           st));
+    c->counts_pending = true;  // the counters are read with the next counts fetch
+  }
 }
 
 // Consume the asynchronously copied match counts (caller has synchronized or will).

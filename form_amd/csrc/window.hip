@@ -687,9 +687,7 @@ void win_linearize_pairs(fmx_ctx* c, const double* poses_i, const double* poses_
   win_start(c, a, c->max_chunks, table.data(), 2 * K, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * K,
             comm ? c->d_sum.p : nullptr);
   if (comm) {  // every pair's G (and error) summed over the ranks on this stream
-    comm_allreduce_sum(c, c->d_sum.p, (size_t)K * kWinG);
-    FMX_HIP(hipMemcpyAsync(W.hG.p, c->d_sum.p, (size_t)K * kWinG * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    stream_wait(c);
+    comm_allreduce_publish(c, c->d_sum.p, (size_t)K * kWinG, W.hG);
   } else {
     win_finish(c, nullptr);
   }

@@ -82,11 +82,22 @@ EXPORTED = [
     "fmx_current_pose",
     "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
     "fmx_profile_name", "fmx_profile_read", "fmx_sync", "fmx_comm_unique_id", "fmx_comm_init",
+    "fmx_map_download",
 ]
 
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _ready(*tensors):
+    """Device tensors handed to a context's stream: wait for the torch stream that
+    produced them (fmx copies them on its own stream, unordered with torch's)."""
+    import torch
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()
+            return
 
 
 @dataclass
@@ -210,6 +221,7 @@ class Context:
         """Device-resident queries: (N,4) float32 CUDA tensors."""
         npt = 0 if point_pos4 is None else point_pos4.shape[0]
         pp = C.c_void_p(point_pos4.data_ptr()) if npt else None
+        _ready(planar_pos4, planar_nrm4, point_pos4)
         self._chk(self._L.fmx_set_queries_device(self.h, C.c_uint64(scan_idx), C.c_void_p(planar_pos4.data_ptr()),
                                                  C.c_void_p(planar_nrm4.data_ptr()), C.c_uint32(planar_pos4.shape[0]),
                                                  pp, C.c_uint32(npt)))
@@ -219,6 +231,7 @@ class Context:
     def keypoints_add_device(self, scan_idx: int, planar_pos4, planar_nrm4, point_pos4=None):
         npt = 0 if point_pos4 is None else point_pos4.shape[0]
         pp = C.c_void_p(point_pos4.data_ptr()) if npt else None
+        _ready(planar_pos4, planar_nrm4, point_pos4)
         self._chk(self._L.fmx_keypoints_add_device(self.h, C.c_uint64(scan_idx), C.c_void_p(planar_pos4.data_ptr()),
                                                    C.c_void_p(planar_nrm4.data_ptr()), C.c_uint32(planar_pos4.shape[0]),
                                                    pp, C.c_uint32(npt)))
@@ -334,6 +347,22 @@ class Context:
         self._chk(self._L.fmx_current_pose(self.h, _p(T)))
         return T.reshape(3, 4)
 
+    def map_download(self, voxel_width: float):
+        """fmx_map_download: FORM::map()'s to_voxel_map of both feature types at the
+        current estimates (bindings.cpp:96-119), voxel by voxel.  Returns {"planar":
+        (xyz (M,3), normals (M,3), scans (M,)), "point": (xyz, None, scans)}."""
+        npl, npt = C.c_uint32(0), C.c_uint32(0)
+        self._chk(self._L.fmx_map_download(self.h, C.c_double(voxel_width), None, None, C.byref(npl), None, None,
+                                           C.byref(npt)))
+        pl = np.zeros((npl.value, 6))
+        spl = np.zeros(npl.value, np.uint64)
+        pt = np.zeros((npt.value, 3))
+        spt = np.zeros(npt.value, np.uint64)
+        self._chk(self._L.fmx_map_download(self.h, C.c_double(voxel_width), _p(pl), _p(spl), C.byref(npl), _p(pt),
+                                           _p(spt), C.byref(npt)))
+        return {"planar": (pl[:npl.value, :3].copy(), pl[:npl.value, 3:].copy(), spl[:npl.value]),
+                "point": (pt[:npt.value], None, spt[:npt.value])}
+
     def last_stats(self) -> dict:
         keys = ["icp_iters", "lm_iters", "matched_planar", "matched_point", "map_planar", "map_point",
                 "linearizations", "map_scans", "host_waits", "spec_matches", "spec_hits", "spec_map",
@@ -423,3 +452,182 @@ def extract_keypoints(points, params: KeypointExtractionParams, lidar_params=Non
         ctx.close()
     planar = d["planar"].astype(np.float64)
     return planar[:, :3].copy(), planar[:, 3:].copy(), d["point"].astype(np.float64)
+
+
+# ---------------------------------------------------------------------------- evalio
+# The evalio pipeline surface of form._core.FORM (python/bindings.cpp:48-180), backed by
+# fmx.  evalio itself is not needed: lidar parameters, measurements and poses are
+# duck-typed (attributes / numpy arrays), and results are numpy arrays.
+
+# EVALIO_SETUP_PARAMS (bindings.cpp:66-88): YAML key -> (type, default, where it lands).
+# Note the reference's key `max_dist_map` sets KeypointMapParams::min_dist_map (:85),
+# and `num_threads` sizes the reference's TBB pool (no role on the GPU path).
+PIPELINE_PARAMS = {
+    "neighbor_points": (int, 5, "extraction.neighbor_points"),
+    "num_sectors": (int, 6, "extraction.num_sectors"),
+    "planar_threshold": (float, 1.0, "extraction.planar_threshold"),
+    "planar_feats_per_sector": (int, 50, "extraction.planar_feats_per_sector"),
+    "point_feats_per_sector": (int, 3, "extraction.point_feats_per_sector"),
+    "radius": (float, 1.0, "extraction.radius"),
+    "min_points": (int, 5, "extraction.min_points"),
+    "max_dist_matching": (float, 0.8, "max_dist_matching"),
+    "new_pose_threshold": (float, 1e-4, "new_pose_threshold"),
+    "max_num_rematches": (int, 30, "max_num_rematches"),
+    "disable_smoothing": (bool, False, "disable_smoothing"),
+    "max_num_keyscans": (int, 50, "max_num_keyscans"),
+    "max_num_recent_scans": (int, 10, "max_num_recent_scans"),
+    "max_steps_unused_keyscan": (int, 10, "max_steps_unused_keyscan"),
+    "keyscan_match_ratio": (float, 0.1, "keyscan_match_ratio"),
+    "max_dist_map": (float, 0.1, "min_dist_map"),
+    "num_threads": (int, 0, None),
+}
+# keys of an evalio config's pipeline entry that are not pipeline parameters
+CONFIG_KEYS = ("pipeline", "name")
+
+
+def _pose44(T) -> np.ndarray:
+    T = np.asarray(T, np.float64)
+    if T.shape == (4, 4):
+        return T.copy()
+    out = np.eye(4)
+    out[:3, :] = T.reshape(3, 4)
+    return out
+
+
+def _points_xyz(mm) -> np.ndarray:
+    """A LidarMeasurement's points as (N, 3): an (N, >=3) array, a measurement with a
+    `points` attribute, or a sequence of objects with x, y, z (evalio.Point)."""
+    pts = getattr(mm, "points", mm)
+    try:
+        a = np.asarray(pts, np.float64)
+        if a.ndim == 2 and a.shape[1] >= 3:
+            return a[:, :3]
+    except (TypeError, ValueError):
+        pass
+    return np.array([[p.x, p.y, p.z] for p in pts], np.float64).reshape(-1, 3)
+
+
+class FORM:
+    """form._core.FORM (bindings.cpp:48-180) on the MI355X path.
+
+    Same call sequence as evalio drives the reference: ``set_params`` (YAML keys),
+    ``set_lidar_params``, ``set_imu_T_lidar``, ``initialize``, then ``add_lidar`` per
+    scan, ``pose()`` and ``map()``.  ``add_lidar`` returns {"planar", "point"} as
+    (F, 4) arrays of (x, y, z, scan) in the scan's frame — the reference's evalio
+    Points carry the scan index in `col` (bindings.cpp:31-41); ``map()`` the same in the
+    world frame, voxel by voxel (bindings.cpp:96-119)."""
+
+    def __init__(self, device: int = 0):
+        self.params = EstimatorParams()
+        self.num_threads = 0
+        self.device = device
+        self.lidar_T_imu = np.eye(4)
+        self._est = None
+        self._scan = -1
+        self._pose = np.eye(4)
+
+    @staticmethod
+    def name() -> str:
+        return "form"
+
+    @staticmethod
+    def url() -> str:
+        return "https://github.com/rpl-cmu/form"
+
+    @staticmethod
+    def default_params() -> dict:
+        return {k: d for k, (_, d, _) in PIPELINE_PARAMS.items()}
+
+    def set_params(self, params: dict) -> dict:
+        """Apply YAML parameter overrides (EVALIO_SETUP_PARAMS keys, bindings.cpp:66-88);
+        an evalio config entry's own keys (pipeline, name) are skipped.  Unknown keys
+        raise KeyError.  Returns the full parameter dict now in effect."""
+        for k, v in params.items():
+            if k in CONFIG_KEYS:
+                continue
+            if k not in PIPELINE_PARAMS:
+                raise KeyError(f"unknown FORM parameter {k!r}")
+            typ, _, dest = PIPELINE_PARAMS[k]
+            v = typ(v)
+            if dest is None:
+                self.num_threads = v
+            elif dest.startswith("extraction."):
+                setattr(self.params.extraction, dest.split(".", 1)[1], v)
+            else:
+                setattr(self.params, dest, v)
+        return self.get_params()
+
+    def get_params(self) -> dict:
+        out = {}
+        for k, (_, _, dest) in PIPELINE_PARAMS.items():
+            if dest is None:
+                out[k] = self.num_threads
+            elif dest.startswith("extraction."):
+                out[k] = getattr(self.params.extraction, dest.split(".", 1)[1])
+            else:
+                out[k] = getattr(self.params, dest)
+        return out
+
+    def set_imu_params(self, params) -> None:  # bindings.cpp:123 (unused)
+        pass
+
+    def set_lidar_params(self, params) -> None:
+        """bindings.cpp:126-132: range limits (squared) and the organized geometry."""
+        e = self.params.extraction
+        e.min_norm_squared = float(params.min_range) * float(params.min_range)
+        e.max_norm_squared = float(params.max_range) * float(params.max_range)
+        e.num_columns = int(params.num_columns)
+        e.num_rows = int(params.num_rows)
+
+    def set_imu_T_lidar(self, T) -> None:
+        """bindings.cpp:135-137: lidar_T_imu = (imu_T_lidar)^-1."""
+        self.lidar_T_imu = np.linalg.inv(_pose44(T))
+
+    def initialize(self) -> None:
+        """bindings.cpp:141: a fresh estimator with the current parameters."""
+        if self._est is not None:
+            self._est.close()
+        self._est = Context(self.params, self.device)
+        self._scan = -1
+        self._pose = np.eye(4)
+
+    def add_imu(self, mm) -> None:  # bindings.cpp:144 (unused)
+        pass
+
+    def add_lidar(self, mm) -> dict:
+        """bindings.cpp:147-179: register the scan, update the pose
+        (current_lidar_estimate * lidar_T_imu) and return its features."""
+        if self._est is None:
+            raise RuntimeError("FORM.add_lidar before initialize()")
+        xyz = _points_xyz(mm)
+        scan = np.zeros((len(xyz), 4), np.float32)
+        scan[:, :3] = xyz.astype(np.float32)  # point_to_form: PointXYZf(x, y, z), bindings.cpp:43-45
+        self._est.register_scan(scan)
+        self._scan += 1
+        self._pose = _pose44(self._est.current_pose()) @ self.lidar_T_imu
+        d = self._est.extract_download()
+        planar = np.zeros((len(d["planar"]), 4))
+        planar[:, :3] = d["planar"][:, :3]
+        planar[:, 3] = self._scan
+        point = np.zeros((len(d["point"]), 4))
+        point[:, :3] = d["point"]
+        point[:, 3] = self._scan
+        return {"planar": planar, "point": point}
+
+    def pose(self) -> np.ndarray:
+        """bindings.cpp:93: the latest pose (4 x 4)."""
+        return self._pose.copy()
+
+    def map(self) -> dict:
+        """bindings.cpp:96-119: the window's keypoints in the world frame, to_voxel_map
+        at voxel width min_dist_map, as (M, 4) arrays of (x, y, z, scan)."""
+        if self._est is None or self._scan < 0:
+            return {"planar": np.zeros((0, 4)), "point": np.zeros((0, 4))}
+        m = self._est.map_download(self.params.min_dist_map)
+        out = {}
+        for name, (xyz, _, sc) in m.items():
+            a = np.zeros((len(xyz), 4))
+            a[:, :3] = xyz
+            a[:, 3] = sc
+            out[name] = a
+        return out

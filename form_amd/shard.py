@@ -104,11 +104,17 @@ TERRAIN_A, TERRAIN_LX, TERRAIN_LY = 0.6, 9.7, 13.3
 C5_RANGE_M = 240.0
 
 
-def c5_offset() -> np.ndarray:
+def c5_offset(rot_scale: float = 1.0) -> np.ndarray:
     """The injected sensor-pose error (truth): 5 cm translation, 0.1 deg yaw, 0.05 deg
-    roll and pitch (GTSAM tangent [w; v])."""
+    roll and pitch (GTSAM tangent [w; v]); rot_scale scales the rotation (the whole-map
+    query set reaches ~4 km, where 0.1 deg is 7 m: it uses 1/20 of it)."""
     d = np.radians
-    return expmap(np.array([d(0.05), d(-0.05), d(0.1), 0.03, -0.04, 0.0]))
+    return expmap(np.array([d(0.05) * rot_scale, d(-0.05) * rot_scale, d(0.1) * rot_scale, 0.03, -0.04, 0.0]))
+
+
+# the whole-map query set (SURVEY.md §8(d): 2M features drawn across the whole map)
+C5_WHOLEMAP_ROT_SCALE = 0.05
+C5_RINGS = 128
 
 
 def terrain_map(n_side: int, w: float, seed: int, device="cpu"):
@@ -157,6 +163,34 @@ def make_queries(pos4, nrm4, n_query: int, offset: np.ndarray, noise: float, see
     n4 = torch.zeros((n_query, 4), dtype=torch.float32, device=dev)
     q4[:, :3] = ql.float()
     n4[:, :3] = nl.float()
+    return q4, n4
+
+
+def make_queries_wholemap(pos4, nrm4, n_query: int, offset: np.ndarray, noise: float, seed: int,
+                          rings: int = C5_RINGS):
+    """n_query DISTINCT map features drawn uniformly over the whole map,
+    each with N(0, noise) noise, in the sensor frame (q = offset^-1 (p + e)), ordered
+    like a spinning LiDAR's output: `rings` range bands of equal counts, each in azimuth
+    order.  Unlike make_queries (a 240 m scan drawn with replacement, grid order), most
+    queries here touch bricks no other query touches: the match reads the map from HBM."""
+    dev = pos4.device
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    n = pos4.shape[0]
+    sel = torch.randperm(n, generator=g)[:n_query].to(dev)
+    p = pos4[sel, :3].double() + noise * torch.randn((n_query, 3), generator=g, dtype=torch.float64).to(dev)
+    R = torch.as_tensor(offset[:, :3], dtype=torch.float64, device=dev)
+    t = torch.as_tensor(offset[:, 3], dtype=torch.float64, device=dev)
+    ql = (p - t) @ R  # R^T (p - t)
+    nl = nrm4[sel, :3].double() @ R
+    rng = torch.sqrt(ql[:, 0] ** 2 + ql[:, 1] ** 2)
+    az = torch.atan2(ql[:, 1], ql[:, 0])
+    ring = torch.empty(n_query, dtype=torch.int64, device=dev)
+    ring[torch.argsort(rng)] = torch.arange(n_query, device=dev) * rings // n_query
+    order = torch.argsort(ring.double() * 8.0 + (az + math.pi))  # ring-major, azimuth inside a ring
+    q4 = torch.zeros((n_query, 4), dtype=torch.float32, device=dev)
+    n4 = torch.zeros((n_query, 4), dtype=torch.float32, device=dev)
+    q4[:, :3] = ql[order].float()
+    n4[:, :3] = nl[order].float()
     return q4, n4
 
 

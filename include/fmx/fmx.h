@@ -210,6 +210,18 @@ fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, i
 fmx_status fmx_next_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, int src_on_device);
 /* Estimator::current_lidar_estimate (form/form.hpp:79). */
 fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
+/* FORM::map() (python/bindings.cpp:96-119): KeypointMap::to_voxel_map of both feature
+ * types (map.tpp:128-146) at the current window estimates, voxel width voxel_width
+ * (the binding passes min_dist_map, bindings.cpp:100), every voxel's points in turn —
+ * world frame, planar: 6 doubles (x, y, z, nx, ny, nz), point: 3 doubles, plus the
+ * scan id of each (the binding ships it as the point's column, bindings.cpp:31-41).
+ * Voxel order is unspecified (the reference iterates a robin_map); inside a voxel,
+ * push_back order (scans ascending, then keypoint order).  Two calls: with NULL
+ * buffers *n_planar / *n_point receive the sizes; with buffers they are the
+ * capacities on entry (FMX_E_SIZE if too small) and the counts on return.  Needs a
+ * registered scan (FMX_E_STATE otherwise). */
+fmx_status fmx_map_download(fmx_ctx* ctx, double voxel_width, double* planar, uint64_t* planar_scan,
+                            uint32_t* n_planar, double* point, uint64_t* point_scan, uint32_t* n_point);
 
 /* Statistics of the last register_scan, the first n of: {icp_iters, lm_iters,
  * matched_planar, matched_point, map_planar, map_point, linearizations, map_scans,

@@ -17,11 +17,14 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <deque>
 #include <functional>
 #include <limits>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <optional>
 #include <set>
 #include <thread>
@@ -31,23 +34,98 @@
 namespace {
 
 // ----------------------------------------------------------------------------
-// std::thread parallel_for: mirrors the reference's two tbb::parallel_for sites
-// (extraction.tpp:99-118 normals, matcher.hpp:86-100 match queries).
+// parallel_for on a persistent worker pool: mirrors the reference's tbb::parallel_for
+// sites (extraction.tpp:99-118 normals, matcher.hpp:86-100 match queries) and GTSAM's
+// TBB-parallel NonlinearFactorGraph::linearize over the pair factors.  Like TBB's
+// arena the workers live across calls (spinning briefly, then sleeping) and take
+// chunks from a shared counter, the caller working too; spawning nthreads std::threads
+// per call would cost milliseconds at 256 threads and misstate the CPU baseline.
+// Every site writes results by index, so the chunking never changes a result.
 // ----------------------------------------------------------------------------
-void parallel_for(size_t n, int nthreads, const std::function<void(size_t, size_t)>& fn) {
+class Pool {
+ public:
+  explicit Pool(int n) : nthreads_(n) {
+    for (int t = 1; t < n; ++t) th_.emplace_back([this] { worker(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      gen_.fetch_add(1);
+    }
+    cv_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  void run(size_t n, const std::function<void(size_t, size_t)>& fn) {
+    std::lock_guard<std::mutex> call(call_m_);  // one parallel region at a time per pool
+    fn_ = &fn;
+    n_ = n;
+    grain_ = std::max<size_t>(1, n / (4 * (size_t)nthreads_));
+    next_.store(0);
+    pending_.store((int)th_.size());
+    {
+      std::lock_guard<std::mutex> g(m_);
+      gen_.fetch_add(1);
+    }
+    cv_.notify_all();
+    work();
+    while (pending_.load() != 0) std::this_thread::yield();
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const size_t b = next_.fetch_add(grain_);
+      if (b >= n_) return;
+      (*fn_)(b, std::min(n_, b + grain_));
+    }
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      uint64_t g = gen_.load();
+      for (int spin = 0; g == seen && spin < 20000; ++spin) g = gen_.load();  // ~tens of us
+      if (g == seen) {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_.load() != seen; });
+        g = gen_.load();
+      }
+      seen = g;
+      if (stop_) return;
+      work();
+      pending_.fetch_sub(1);
+    }
+  }
+  int nthreads_;
+  std::vector<std::thread> th_;
+  std::mutex m_, call_m_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<size_t> next_{0};
+  std::atomic<int> pending_{0};
+  const std::function<void(size_t, size_t)>* fn_ = nullptr;
+  size_t n_ = 0, grain_ = 1;
+  bool stop_ = false;
+};
+
+Pool& pool_for(int nthreads) {
+  static std::mutex m;
+  static std::map<int, std::unique_ptr<Pool>> pools;
+  std::lock_guard<std::mutex> g(m);
+  auto& p = pools[nthreads];
+  if (!p) p = std::make_unique<Pool>(nthreads);
+  return *p;
+}
+
+// min_n: below it the call runs serially (per-element work too small to share); the
+// pair-factor sites pass 2 (each pair is thousands of rows).
+void parallel_for(size_t n, int nthreads, const std::function<void(size_t, size_t)>& fn, size_t min_n = 256) {
   if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
-  if (nthreads == 1 || n < 256) {
+  if (nthreads == 1 || n < min_n) {
     fn(0, n);
     return;
   }
-  std::vector<std::thread> th;
-  size_t chunk = (n + nthreads - 1) / nthreads;
-  for (int t = 0; t < nthreads; ++t) {
-    size_t b = t * chunk, e = std::min(n, b + chunk);
-    if (b >= e) break;
-    th.emplace_back([&, b, e] { fn(b, e); });
-  }
-  for (auto& x : th) x.join();
+  pool_for(nthreads).run(n, fn);
 }
 
 // ----------------------------------------------------------------------------
@@ -950,7 +1028,7 @@ struct WindowGraph {
     parallel_for(pairs.size(), nthreads, [&](size_t b, size_t en) {
       for (size_t p = b; p < en; ++p)
         linearize_pair(*pairs[p].d, x.at(pairs[p].i), x.at(pairs[p].j), sigma, 0, &G[91 * p], &e[p]);
-    });
+    }, 2);
     double err = 0;
     for (auto* P : priors) {
       double info[49], pe;
@@ -984,7 +1062,7 @@ struct WindowGraph {
     std::vector<double> e(pairs.size());
     parallel_for(pairs.size(), nthreads, [&](size_t b, size_t en) {
       for (size_t p = b; p < en; ++p) e[p] = error_pair(*pairs[p].d, x.at(pairs[p].i), x.at(pairs[p].j), sigma);
-    });
+    }, 2);
     double err = 0;
     for (auto* P : priors) {
       double info[49], pe;
@@ -1638,6 +1716,30 @@ void orc_estimator_free(void* e) { delete static_cast<Estimator*>(e); }
 int orc_register_scan(void* e, const float* xyzw, size_t n, double pose_out[12], uint32_t* stats,
                       double* times_ms) {
   return static_cast<Estimator*>(e)->register_scan(xyzw, n, pose_out, stats, times_ms);
+}
+
+// FORM::map() (bindings.cpp:96-119) = KeypointMap::to_voxel_map (map.tpp:128-146) of the
+// stored keypoints of feature type `kind` at the current values, in push_back order
+// (scans ascending, keypoint order; the grouping into voxels is left to the caller).
+// Returns the record count; xyz (3n), nrm (3n, planar only) and scans (n) may be NULL.
+uint32_t orc_estimator_map(void* ev, int kind, double* xyz, double* nrm, uint64_t* scans) {
+  Estimator& e = *static_cast<Estimator*>(ev);
+  const auto& kp = kind == 0 ? e.kp_planar : e.kp_point;
+  const int stride = kind == 0 ? 6 : 3;
+  uint32_t n = 0;
+  for (auto& [s, f] : kp) {
+    const Pose& T = e.values.at(s);  // values.at<Pose3>(X(scan_index)), map.tpp:137
+    for (size_t i = 0; i < f.size() / stride; ++i, ++n) {
+      double lp[3] = {f[stride * i], f[stride * i + 1], f[stride * i + 2]};
+      if (xyz) xform(T, lp, xyz + 3 * (size_t)n);  // PlanarFeat::transform, features.hpp:137-140
+      if (nrm && kind == 0) {
+        double ln[3] = {f[stride * i + 3], f[stride * i + 4], f[stride * i + 5]};
+        matvec(T.R, ln, nrm + 3 * (size_t)n);
+      }
+      if (scans) scans[n] = s;
+    }
+  }
+  return n;
 }
 
 }  // extern "C"

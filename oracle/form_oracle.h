@@ -115,6 +115,10 @@ void orc_estimator_free(void* e);
  * times_ms[0..3] = {extract, map_build, icp(match+lm), total} */
 int orc_register_scan(void* e, const float* xyzw, size_t n, double pose_out34[12],
                       uint32_t* stats, double* times_ms);
+/* FORM::map() restated: the stored keypoints of feature type kind (0 planar, 1 point)
+ * in the world frame at the current values, push_back order (scans ascending); returns
+ * the count; any output pointer may be NULL. */
+uint32_t orc_estimator_map(void* e, int kind, double* xyz, double* nrm, uint64_t* scans);
 
 #ifdef __cplusplus
 }

@@ -192,6 +192,7 @@ class Estimator:
     def __init__(self, params: Params, nthreads: int = 0):
         lib().orc_estimator_new.restype = C.c_void_p
         self.h = C.c_void_p(lib().orc_estimator_new(C.byref(params), C.c_int(nthreads)))
+        lib().orc_estimator_map.restype = C.c_uint32
 
     def __del__(self):
         try:
@@ -209,3 +210,16 @@ class Estimator:
         if rc != 0:
             raise RuntimeError("scan size mismatch")
         return pose.reshape(3, 4), stats, tms
+
+    def map(self):
+        """FORM::map() restated (bindings.cpp:96-119): {"planar": (xyz (M,3), normals
+        (M,3), scans (M,)), "point": (xyz, None, scans)} in push_back order."""
+        out = {}
+        for kind, name in ((0, "planar"), (1, "point")):
+            n = lib().orc_estimator_map(self.h, C.c_int(kind), None, None, None)
+            xyz = np.zeros((n, 3))
+            nrm = np.zeros((n, 3)) if kind == 0 else None
+            sc = np.zeros(n, np.uint64)
+            lib().orc_estimator_map(self.h, C.c_int(kind), _p(xyz), _p(nrm), _p(sc))
+            out[name] = (xyz, nrm, sc)
+        return out

@@ -100,8 +100,8 @@ def test_c5_registration_converges(fmx_mod, c5_map):
             S0, e0 = ctx.linearize_matched(T, 0.1)
         ctx.match(T, W, counts=False)  # as bench.py's c5_register
         S, err = ctx.linearize_matched(T, 0.1)
-        if it == 0:
-            assert np.array_equal(S, S0) and err == e0
+        if it == 0:  # fused match + linearization vs the stored-results path: summation order only
+            assert np.all(np.abs(S - S0) <= 1e-10 * np.abs(S0).max()) and abs(err - e0) <= 1e-10 * e0
         dx = shard.gauss_newton_step(S)
         T = shard.compose(T, shard.expmap(dx))
         if np.linalg.norm(dx) < 1e-4:
@@ -110,6 +110,45 @@ def test_c5_registration_converges(fmx_mod, c5_map):
     e0t, e0r = shard.pose_error(I34, Tt)
     assert it < 10
     assert et < 0.02 * e0t and er < 0.02 * e0r, (et, er, e0t, e0r)
+
+
+def test_fused_match_linearize(fmx_mod, oracle, c5_map):
+    """fmx_match without counts on a large query set is deferred; fmx_linearize_matched
+    at the same pose then runs match + linearization in one launch (no per-query
+    results): the system equals the two-step path's to 1e-10 (summation order), the
+    profile shows the fused kernel, and a later fmx_match_download still gets the
+    match (launched on demand), bit-equal to a counted match."""
+    pos4, nrm4 = c5_map
+    q4, n4 = shard.make_queries(pos4, nrm4, 300000, shard.c5_offset(), 0.03, 81)
+    ctx = _ctx(fmx_mod, pos4.shape[0])
+    ctx.keypoints_add_device(0, pos4, nrm4)
+    ctx.map_build([0], I34[None], W)
+    ctx.set_queries_device(q4, n4)
+    Tj = shard.expmap(np.array([0.0005, -0.0003, 0.0008, 0.02, 0.01, -0.01]))
+    ctx.match(Tj, W)
+    ref = ctx.match_download()
+    S0, e0 = ctx.linearize_matched(Tj, 0.1)
+    ctx.profile(True)
+    ctx.profile_reset()
+    ctx.match(Tj, W, counts=False)
+    S1, e1 = ctx.linearize_matched(Tj, 0.1)
+    S2, e2 = ctx.linearize_matched(Tj, 0.1)  # the match is still deferred: fused again, same sums
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    assert prof["match_linearize"]["launches"] == 2 and prof["match"]["launches"] == 0
+    assert prof["linearize"]["launches"] == 0
+    assert np.all(np.abs(S1 - S0) <= 1e-10 * np.abs(S0).max()) and abs(e1 - e0) <= 1e-10 * e0
+    assert np.array_equal(S1, S2) and e1 == e2
+    got = ctx.match_download()  # settles the deferred match
+    for k in ("pair", "d2", "pi", "ni"):
+        assert np.array_equal(got[k], ref[k]), k
+    # at another pose the deferred match is launched first, then linearized as stored
+    ctx.match(Tj, W, counts=False)
+    T2 = shard.expmap(np.array([0.0004, -0.0003, 0.0008, 0.02, 0.01, -0.01]))
+    S3, _ = ctx.linearize_matched(T2, 0.1)
+    ctx.match(Tj, W)
+    S4, _ = ctx.linearize_matched(T2, 0.1)
+    assert np.array_equal(S3, S4)
 
 
 def test_comm_single_rank_is_identity(fmx_mod, c5_map):
@@ -125,14 +164,17 @@ def test_comm_single_rank_is_identity(fmx_mod, c5_map):
         ctx.keypoints_add_device(0, pos4, nrm4)
         ctx.map_build([0], I34[None], W)
         ctx.set_queries_device(q4, n4)
+        ctx.match(I34, W, counts=False)
+        Sf, ef = ctx.linearize_matched(I34, 0.1)  # fused
         ctx.match(I34, W)
         S, e = ctx.linearize_matched(I34, 0.1)
         G, err = ctx.linearize(I34[None], I34[None], 0.1, False)
-        out.append((S, e, G, err))
+        out.append((S, e, G, err, Sf, ef))
         ctx.close()
-    (S0, e0, G0, r0), (S1, e1, G1, r1) = out
+    (S0, e0, G0, r0, F0, f0), (S1, e1, G1, r1, F1, f1) = out
     assert np.array_equal(S0, S1) and e0 == e1
     assert np.array_equal(G0, G1) and np.array_equal(r0, r1)
+    assert np.array_equal(F0, F1) and f0 == f1
 
 
 def _free_port():
