@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--prefill", type=int, default=90,
                     help="untimed scans registered before the warmup so the timed region runs with the "
                          "window in steady state (10 recent scans + keyscans), not while it fills")
+    ap.add_argument("--c5-dist", default="both", choices=["both", "local", "wholemap"],
+                    help="C5 query sets: the 240 m terrain scan, 2M distinct features across the whole map, or both")
+    ap.add_argument("--c5-comm", action="store_true",
+                    help="attach the RCCL communicator even on one rank (the exchange step's own overhead)")
     ap.add_argument("--c5-steps", type=int, default=5, help="sharded C5 registrations timed beside the C4 line")
     ap.add_argument("--c5-warmup", type=int, default=1)
     ap.add_argument("--no-c5", action="store_true", help="skip the sharded C5 measurement beside the C4 line")
@@ -193,15 +197,20 @@ def host_info():
     return {"host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": model}
 
 
-def cpu_baseline(scans_host, params, budget_s, single):
-    """Oracle register_scan on the host cores over the first scans of the same stream.
-    Threads: the job's CPU share — OMP_NUM_THREADS when the launcher sets it (the GPU
-    box allots 16 CPUs per GPU and exports 16), else every CPU in this process's
-    affinity mask (the reference's TBB default: all host cores)."""
+def cpu_threads():
+    """The job's CPU share: OMP_NUM_THREADS when the launcher sets it (the GPU box allots
+    16 CPUs per GPU, exports 16 and asks worker pools to stay within it: its other CPUs
+    belong to other jobs), else every CPU in this process's affinity mask (the
+    reference's TBB default: all host cores)."""
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or host_info()["affinity_cpus"]
+
+
+def cpu_baseline(scans_host, params, budget_s, single, threads):
+    """Oracle register_scan on `threads` host threads (a persistent pool at the
+    reference's TBB sites) over the first scans of the same stream."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O  # CPU baseline only (test infrastructure)
     hi = host_info()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or hi["affinity_cpus"]
     prm = O.default_params(params)
     prm.disable_smoothing = int(single)
     est = O.Estimator(prm, threads)
@@ -220,8 +229,9 @@ def cpu_baseline(scans_host, params, budget_s, single):
     per = float(np.median(steady))
     return dict(value=1.0 / per, unit="scans/s", cores=threads, kind="port",
                 sample=f"oracle register_scan ({'single-pose' if single else 'smoothing'} mode; C++ restatement, "
-                       f"std::thread at the reference's TBB sites (normals, match queries) and over the factors "
-                       f"of a linearization (GTSAM's TBB-parallel NonlinearFactorGraph::linearize)) over the first "
+                       f"a persistent {threads}-thread pool at the reference's TBB sites (normals, match queries) "
+                       f"and over the factors of a linearization (GTSAM's TBB-parallel "
+                       f"NonlinearFactorGraph::linearize)) over the first "
                        f"{len(times)} scans of the same synthetic stream; median of {len(steady)} steady-state "
                        f"scans = {per * 1e3:.1f} ms/scan",
                 ms_per_scan=per * 1e3, **hi), poses
@@ -270,6 +280,8 @@ def c5_setup(a, rank, world, local):
         uid = [fmx.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(uid[0], world, rank)
+    elif a.c5_comm:  # a one-rank communicator: the all-reduce + publish path without peers
+        ctx.comm_init(fmx.comm_unique_id(), 1, 0)
     ctx.keypoints_add_device(0, pos4, nrm4)
     I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
     ctx.map_build([0], I34[None], w)
@@ -361,7 +373,8 @@ def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmu
                                f"({C5_DISTS[dist_name]}); points sharded contiguously, map replicated; match + "
                                "single-pose 7x7 normal equations fused in one launch, all-reduced (RCCL, device "
                                "buffers, context stream) per ICP iteration", "points_per_scan": a.c5_queries,
-                   "query_distribution": dist_name, "parallelism": f"point shards x{world} + all_reduce"},
+                   "query_distribution": dist_name, "parallelism": f"point shards x{world} + all_reduce",
+                   "rccl_communicator": world > 1 or bool(a.c5_comm)},
         "pose_error": {"initial_m": round(e0t, 6), "initial_rad": round(e0r, 8), "final_m": round(et, 6),
                        "final_rad": round(er, 8)},
     }
@@ -416,10 +429,12 @@ def main():
     rank, world, local = dist_setup(a.gpus)
     if a.workload == "c5":
         torch.cuda.set_device(local)
-        res = run_c5(a, rank, world, local, a.steps, a.warmup)
+        dists = ("local", "wholemap") if a.c5_dist == "both" else (a.c5_dist,)
+        res = run_c5(a, rank, world, local, a.steps, a.warmup, dists=dists)
         if res is not None:
-            out = res["local"]
-            out["wholemap"] = res["wholemap"]
+            out = res[dists[0]]
+            if len(dists) > 1:
+                out["wholemap"] = res["wholemap"]
             print(json.dumps(out))
         if world > 1:
             import torch.distributed as dist
@@ -517,6 +532,8 @@ def main():
     st_mean = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]} if stats else {}
     kern_ms = {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()}
     kern_sum = sum(kern_ms.values())
+    side = {"map_build"} | ({"extract_rows", "closest", "fit", "compact"} if pipe else set())
+    main_ms = sum(v for k, v in kern_ms.items() if k not in side)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -544,9 +561,12 @@ def main():
         "roofline": roof,
         "kernels_ms_per_step": kern_ms,
         "profile_steps": psteps,
-        # device time per scan (profile pass, HIP events; the side-stream map build
-        # overlaps extraction and is counted in full) over the timed wall time per scan
-        "gpu_busy_frac": round(min(kern_sum / ms_per_step, 1.0), 4) if ms_per_step > 0 else None,
+        # the context (critical-path) stream's kernel time per scan (profile pass, HIP
+        # events; its kernels never overlap each other) over the timed wall time per
+        # scan; side-stream work (pipelined extraction, map build) is excluded.  The
+        # rocprofv3 trace's own figure: profiles/critical_path_c4.json (tools/critical_path.py)
+        "main_stream_busy_frac": round(min(main_ms / ms_per_step, 1.0), 4) if ms_per_step > 0 else None,
+        "all_streams_kernel_ms_per_step": round(kern_sum, 4),
         "host_round_trips_per_scan": round(st_mean.get("host_waits", 0.0), 2),
         "counters": st_mean,
         "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
@@ -558,12 +578,20 @@ def main():
     if c5 is not None:
         out["sharded_c5"] = c5
         out["sharded_c5_wholemap"] = c5_whole
+    cp = os.path.join(ROOT, "profiles", f"critical_path_{a.workload}.json")
+    if os.path.exists(cp):
+        with open(cp) as f:
+            out["critical_path_trace"] = json.load(f)
     if prev_aff is not None:
         os.sched_setaffinity(0, prev_aff)  # the CPU baseline's threads use every host core
     if not a.no_cpu_baseline and world == 1:
         host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
         del scans
-        out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s, single)
+        out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s, single, cpu_threads())
+        # one thread over the same scans: the pool's scaling (and a per-core figure)
+        one, _ = cpu_baseline(host[:12], params, a.cpu_sample_s / 2, single, 1)
+        out["cpu_baseline"]["single_thread"] = {"value": one["value"], "ms_per_scan": one["ms_per_scan"],
+                                                "sample": one["sample"]}
         out["ate"] = ate_block(host, opos, params, k0, local, single, pipe)
     print(json.dumps(out))
     if world > 1:

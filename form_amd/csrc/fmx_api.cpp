@@ -1594,7 +1594,7 @@ fmx_status fmx_last_stats(fmx_ctx* c, uint64_t* stats, int n) {
 }
 
 fmx_status fmx_match_work(fmx_ctx* c, double work[3]) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {  // the last launched match (a fused one counts too)
     match_counts_fetch(c);
     work[0] = (double)c->n_qpl + (double)c->n_qpt;
     work[1] = c->last_probes;

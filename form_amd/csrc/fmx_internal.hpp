@@ -368,6 +368,7 @@ struct fmx_ctx {
   fmx::DBuf<uint32_t> ticket;                     // its last-block ticket
   fmx::DBuf<uint32_t> fz_tickets;                 // fused match + linearization: per block-group tickets
   fmx::DBuf<uint32_t> mcnt, mticket;              // query-order match: per-pair counters + ticket
+  bool fz_work_pending = false;                   // fused launch's work counters copied, not yet summed
   fmx::DBuf<uint32_t> ins_blk, ins_off;           // per match block insert counts / offsets
   uint32_t ins_tot[2] = {0, 0};                   // insert totals of the last match
   uint32_t match_nb_pl = 0, match_nb = 0;         // blocks of the last match
@@ -578,7 +579,8 @@ inline uint32_t next_flag(fmx_ctx* c) {
   void run_insert(fmx_ctx* c, uint64_t scan, uint32_t* n_inserted);                                  \
   void match_counts_fetch(fmx_ctx* c, bool wait = true);                                             \
   void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* dst, \
-                           uint32_t* flag, uint32_t seq);
+                           uint32_t* flag, uint32_t seq);                                              \
+  void work_fetch(fmx_ctx* c);
 // Windows of at most this many map scans (pairs) use the tiled pair sort; wider ones a
 // per-match-block histogram whose scatter ranks within one wave, so they take the g8
 // build (32 queries per block) whatever the query count.

@@ -311,9 +311,9 @@ void run_match_linearize_total(fmx_ctx* c, const double* pose_j34, double max_di
   } else {
     wait_flag(c, c->h_flag.p, seq);
   }
-  if (c->counts_pending && c->prof.on) {  // the work counters of this launch (byte model)
+  if (c->fz_work_pending) {  // profiling: the work counters of this launch (byte model)
     stream_wait(c);
-    match_counts_fetch(c, false);
+    gl::work_fetch(c);
   }
   std::memcpy(out, c->h_G.p, 29 * sizeof(double));
 }

@@ -599,15 +599,12 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 }
 
 // VoxelMap::find_closest (map.tpp:70-91) of one query by a group of G lanes (lane g of
-// the group), bounded by the incoming best (a.bound, or +inf).  Returns false when the
-// query was abandoned as heavy: a cell walk of more than `cap` records (group-uniform);
-// the caller then searches it again with a whole wave.
+// the group), bounded by the incoming best (a.bound, or +inf).
 template <int G, bool DENSE>
-__device__ __forceinline__ bool nn_search(const MatchArgs& a, const MapView& M, const double (&wq)[3], int g,
-                                          uint32_t* hd, uint32_t cap, double& best, uint32_t& best_rid,
-                                          uint32_t& best_i, uint32_t& n_probe, uint32_t& n_cand) {
+__device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, const double (&wq)[3], int g,
+                                          uint32_t* hd, double& best, uint32_t& best_rid, uint32_t& best_i,
+                                          uint32_t& n_probe, uint32_t& n_cand) {
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
-  bool heavy = false;
   // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
   // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
   // the record's build order (= insertion order inside a voxel, map.tpp:41-52)
@@ -779,10 +776,6 @@ __device__ __forceinline__ bool nn_search(const MatchArgs& a, const MapView& M, 
         for (int o = 1; o < G; o <<= 1) tot += __shfl_xor(tot, o, G);
       }
       if (tot == 0) continue;
-      if (tot > cap) {  // a heavy walk: the whole query goes to a wave of its own
-        heavy = true;
-        return;
-      }
       int k = __ffsll((unsigned long long)mask) - 1;
       uint32_t ks = sorted ? sub_beg(k) : 0u, ke = sorted ? hd[k] : tot, vbase = 0;  // (not sorted: never advances)
       auto locate = [&](uint32_t v) {  // v ascending per lane
@@ -840,10 +833,10 @@ __device__ __forceinline__ bool nn_search(const MatchArgs& a, const MapView& M, 
   // (records split over the lanes), re-checking each bound against the shared best.
   // One loop over the passes, so the cell walk is emitted once.
   const int npass = a.rings >= 2 ? 4 : 3;
-  for (int ip = 0; ip < npass && !heavy; ++ip) {
+  for (int ip = 0; ip < npass; ++ip) {
     const int s_begin = ip == 0 ? 0 : (ip == 1 ? 1 : (ip == 2 ? 7 : 27));
     const int s_end = ip == 0 ? 1 : (ip == 1 ? 7 : (ip == 2 ? 27 : 125));
-    for (int s0 = s_begin; s0 < s_end && !heavy; s0 += G) {  // one shift per lane per chunk
+    for (int s0 = s_begin; s0 < s_end; s0 += G) {  // one shift per lane per chunk
       uint32_t vf = 0, vc = 0;
       bool vd = false;
       double vlb = INFINITY;
@@ -883,26 +876,14 @@ __device__ __forceinline__ bool nn_search(const MatchArgs& a, const MapView& M, 
         const int sl = s0 + l;
         scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2],
                   srank(c_shift[sl][0], c_shift[sl][1], c_shift[sl][2]));
-        if (heavy) break;
       }
     }
   }
-  return !heavy;
 }
 
 // DENSE = false: the map has no dense cell (known from the build's pinned info word),
 // so the sub-cell walk is compiled out (fewer registers, more waves in flight).
 //
-// Heavy queries (DENSE): a query whose search reaches a cell walk of more than
-// kHeavyCap records (a dense ground cell near the sensor: ~500 candidates) would hold
-// its whole block for ~40 us at kGroup lanes and set the launch's span.  Its group
-// abandons it, and once the wave's other queries are done the whole wave (64 lanes,
-// 8x the loads in flight) searches it again from the start; its result, pair count
-// and insert flag stay in this block, so the bookkeeping below is unchanged.
-#ifndef FMX_HEAVY_CAP
-#define FMX_HEAVY_CAP 0  // 0: off (measured slower, DESIGN.md: heavy queries cluster in whole waves)
-#endif
-constexpr uint32_t kHeavyCap = FMX_HEAVY_CAP;
 
 #include "factor_rows.hpp"
 
@@ -1011,7 +992,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   if (threadIdx.x == 0) s_ins = 0;
   __syncthreads();
   const uint32_t t_begin = (uint32_t)wall_clock64();
-  uint32_t n_probe = 0, n_cand = 0, heavy_cand = 0;
+  uint32_t n_probe = 0, n_cand = 0;
   auto world_query = [&](uint32_t q, double (&wq)[3]) {
     const float4 lq = planar ? q_pl[q] : q_pt[q];
     d_xform(Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
@@ -1046,37 +1027,14 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (ins) atomicAdd(&s_ins, 1u);
     if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
   };
-  bool heavy = false;
   double best = a.bound;
   uint32_t best_i = 0xFFFFFFFFu;
   if (qi < nq) {
     double wq[3];
     world_query(qi, wq);
     uint32_t best_rid = 0xFFFFFFFFu;
-    heavy = !nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0],
-                                       DENSE && kHeavyCap ? kHeavyCap : 0xFFFFFFFFu, best, best_rid, best_i,
-                                       n_probe, n_cand);
-  }
-  if constexpr (DENSE && kGroup < kWave && kHeavyCap > 0) {
-    // the wave's abandoned queries, one at a time, 64 lanes each; the result goes back
-    // to the query's own group leader (lane l)
-    uint64_t hv = __ballot(heavy && g == 0);
-    const uint32_t c0 = n_cand;
-    while (hv) {
-      const int l = __ffsll((unsigned long long)hv) - 1;
-      hv &= hv - 1;
-      const uint32_t gi = (threadIdx.x / kWave) * (kWave / kGroup) + l / kGroup;  // query slot in the block
-      double wq[3];
-      world_query(qb + gi, wq);
-      double hb = a.bound;
-      uint32_t hr = 0xFFFFFFFFu, hi = 0xFFFFFFFFu;
-      nn_search<kWave, DENSE>(a, M, wq, lane_id(), s_hdr[gi], 0xFFFFFFFFu, hb, hr, hi, n_probe, n_cand);
-      if (lane_id() == l) {
-        best = hb;
-        best_i = hi;
-      }
-    }
-    heavy_cand = wave_sum(n_cand - c0);  // the heavy queries' candidates (diagnostics)
+    nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, n_probe,
+                             n_cand);
   }
   // work counters for the algorithmic-byte model and the match diagnostics (one plain
   // store per block, summed on the host): probes, candidate records, the largest
@@ -1087,7 +1045,6 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   for (int o = 1; o < kGroup; o <<= 1) qc += __shfl_xor(qc, o, 64);
 #pragma unroll
   for (int o = kGroup; o < kWave; o <<= 1) qc = max(qc, (uint32_t)__shfl_xor(qc, o, 64));
-  qc = max(qc, heavy_cand);
   const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
   if (lane_id() == 0) {
     s_work[0][threadIdx.x / kWave] = wp;
@@ -1898,13 +1855,27 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   (void)a;
   throw StatusError(FMX_E_STATE, "fused match + linearization needs the one-lane-per-query build");
 #endif
-  c->work_copied = c->prof.on;
-  if (c->prof.on) {  // per-block work counters (byte model of the next launch)
+  if (c->prof.on) {  // per-block work counters (byte model of the next launch), read by work_fetch
     c->h_work.ensure(kWorkWords * (size_t)nb + 8);
     FMX_HIP(hipMemcpyAsync(c->h_work.p, c->work.p, kWorkWords * (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost,
                            st));
-    c->counts_pending = true;  // the counters are read with the next counts fetch
+    c->fz_work_pending = true;
   }
+}
+
+// The work counters of the last fused launch (copied while profiling): sums for the
+// byte model and the match diagnostics.  The caller has waited for the stream.
+void work_fetch(fmx_ctx* c) {
+  if (!c->fz_work_pending) return;
+  double tp = 0, tc = 0;
+  for (uint32_t b = 0; b < c->work_blocks; ++b) {
+    tp += c->h_work.p[kWorkWords * b];
+    tc += c->h_work.p[kWorkWords * b + 1];
+  }
+  match_diag_add(c->h_work.p, c->work_blocks);
+  c->last_probes = tp;
+  c->last_cands = tc;
+  c->fz_work_pending = false;
 }
 
 // Consume the asynchronously copied match counts (caller has synchronized or will).

@@ -49,17 +49,23 @@ def _near_features(pos4, nrm4, qw):
     return np.ascontiguousarray(feats)
 
 
-def test_c5_match_full_map_matches_oracle(fmx_mod, oracle, c5_map):
+@pytest.mark.parametrize("dist", ["local", "wholemap"])
+def test_c5_match_full_map_matches_oracle(fmx_mod, oracle, c5_map, dist):
+    """The bench's two C5 query sets: a 240 m terrain scan (samples with replacement)
+    and distinct features drawn across the whole 50M-voxel map (up to ~4 km away, so
+    the rotation of the ICP iterate is scaled down as in the bench)."""
     pos4, nrm4 = c5_map
     n_map = pos4.shape[0]
     assert n_map == SIDE * SIDE > 50_000_000 - 100_000
-    Tt = shard.c5_offset()
-    q4, n4 = shard.make_queries(pos4, nrm4, 65536, Tt, 0.03, 77)
+    rs = 1.0 if dist == "local" else shard.C5_WHOLEMAP_ROT_SCALE
+    Tt = shard.c5_offset(rs)
+    make = shard.make_queries if dist == "local" else shard.make_queries_wholemap
+    q4, n4 = make(pos4, nrm4, 65536, Tt, 0.03, 77)
     ctx = _ctx(fmx_mod, n_map)
     ctx.keypoints_add_device(0, pos4, nrm4)
     ctx.map_build([0], I34[None], W)
     ctx.set_queries_device(q4, n4)
-    Tj = shard.expmap(np.array([0.0005, -0.0003, 0.0008, 0.02, 0.01, -0.01]))  # an ICP iterate
+    Tj = shard.expmap(np.array([0.0005 * rs, -0.0003 * rs, 0.0008 * rs, 0.02, 0.01, -0.01]))  # an ICP iterate
     cpl, _ = ctx.match(Tj, W)
     got = ctx.match_download()
     Q = np.concatenate([q4[:, :3].cpu().numpy(), n4[:, :3].cpu().numpy()], 1)
@@ -149,6 +155,33 @@ def test_fused_match_linearize(fmx_mod, oracle, c5_map):
     ctx.match(Tj, W)
     S4, _ = ctx.linearize_matched(T2, 0.1)
     assert np.array_equal(S3, S4)
+
+
+def test_fused_first_match_with_profiling(fmx_mod, c5_map):
+    """A fresh context whose first match is the deferred one, consumed fused while
+    profiling (the bench's C5 loop): the work counters of the fused launch are read
+    (byte model) and the system equals the two-step path's of a second context."""
+    pos4, nrm4 = c5_map
+    q4, n4 = shard.make_queries(pos4, nrm4, 200000, shard.c5_offset(), 0.03, 82)
+    out = []
+    for fused in (True, False):
+        ctx = _ctx(fmx_mod, pos4.shape[0])
+        ctx.keypoints_add_device(0, pos4, nrm4)
+        ctx.map_build([0], I34[None], W)
+        ctx.set_queries_device(q4, n4)
+        ctx.profile(True)
+        ctx.profile_reset()
+        ctx.match(I34, W, counts=not fused)
+        out.append(ctx.linearize_matched(I34, 0.1))
+        ctx.sync()
+        prof = ctx.profile_read()
+        work = ctx.match_work()
+        assert prof["match_linearize" if fused else "match"]["launches"] == 1
+        ctx.profile(False)
+        ctx.close()
+        assert work["candidates"] > 0 and work["probes"] > 0
+    (S0, e0), (S1, e1) = out
+    assert np.all(np.abs(S0 - S1) <= 1e-10 * np.abs(S1).max()) and abs(e0 - e1) <= 1e-10 * e1
 
 
 def test_comm_single_rank_is_identity(fmx_mod, c5_map):

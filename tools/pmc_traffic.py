@@ -30,6 +30,8 @@ from collections import defaultdict
 
 # fmx kernel symbol fragment -> bench.py profile id
 KMAP = {
+    "k_match<false, true>": "match_linearize",  # C5: match + single-pose linearization fused
+    "k_match<true, true>": "match_linearize",
     "k_match": "match",
     "k_extract_rows": "extract_rows",
     "k_normals": "fit",  # find_closest + compute_normal, fused (C <= 2048)
@@ -49,7 +51,7 @@ KMAP = {
 
 
 # kernels whose HBM reads are dominated by random 64-B lines (1 x FETCH_SIZE)
-GATHER = {"match"}
+GATHER = {"match", "match_linearize"}
 
 
 def kernel_id(name: str):
