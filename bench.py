@@ -62,6 +62,9 @@ def parse():
                     help="extra steps, after the timed ones, with per-kernel HIP-event timing (roofline); "
                          "default = --steps.  The timed region itself runs without event overhead.")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", default="2,4",
+                    help="also time S independent register_scan streams sharing each GPU (one context and one "
+                         "host thread each; a serving figure beside the single-stream headline); '' = skip")
     ap.add_argument("--mode", default="smooth", choices=["smooth", "single"],
                     help="ConstraintManager mode: smooth = the reference default (window smoother), "
                          "single = the disable_smoothing ablation (single-pose LM)")
@@ -245,6 +248,43 @@ def register(ctx, scans, k, pipeline):
     ctx.register_scan(scans[k])
 
 
+def concurrent_streams(S, new_ctx, scans, start, steps, pipeline, single, aff):
+    """S independent estimators on this GPU, each registering the same scans [start,
+    start + steps) from its own host thread (ctypes drops the GIL inside each fmx
+    call), after an untimed prefill of [0, start).  Returns aggregate and per-stream
+    scans/s (time = the slowest stream's)."""
+    import threading
+    ctxs = [new_ctx(single) for _ in range(S)]
+    for c in ctxs:
+        for k in range(start):
+            register(c, scans, k, pipeline)
+        c.sync()
+    cpus = sorted(aff) if aff else []
+    ready = threading.Barrier(S + 1)
+    times = [0.0] * S
+
+    def run(i):
+        if cpus:
+            os.sched_setaffinity(0, {cpus[(4 * i + 1) % len(cpus)]})  # this thread only (Linux)
+        ready.wait()
+        t0 = time.perf_counter()
+        for k in range(start, start + steps):
+            register(ctxs[i], scans, k, pipeline)
+        ctxs[i].sync()
+        times[i] = time.perf_counter() - t0
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(S)]
+    for t in th:
+        t.start()
+    ready.wait()
+    for t in th:
+        t.join()
+    for c in ctxs:
+        c.close()
+    tm = max(times)
+    return {"streams": S, "scans_per_s": round(S * steps / tm, 3), "per_stream_scans_per_s": round(steps / tm, 3)}
+
+
 def ate_block(scans_host, oracle_poses, params, k0, device, single, pipeline):
     """ATE of the GPU path and of the CPU oracle path over the same scans against the
     synthetic ground truth (the newer_college ATE is unavailable
@@ -315,18 +355,10 @@ def c5_register(ctx, w, max_iters=30, thr=1e-4):
     (this rank's shard) -> the shard's single-pose 7x7 normal equations, all-reduced
     over the ranks on the device (RCCL) -> the identical Gauss-Newton step on every
     rank, from the identity to convergence (form.cpp:83-88's 1e-4 threshold on the
-    increment).  fmx_match without counts + fmx_linearize_matched at the same pose run
-    as ONE fused launch (no per-query results).  Returns (pose, ICP iterations)."""
-    from form_amd import shard
-    T = np.hstack([np.eye(3), np.zeros((3, 1))])
-    for it in range(max_iters):
-        ctx.match(T, w, counts=False)  # deferred: fused with the linearization below
-        S, _ = ctx.linearize_matched(T, 0.1)
-        dx = shard.gauss_newton_step(S)
-        T = shard.compose(T, shard.expmap(dx))
-        if np.linalg.norm(dx) < thr:
-            return T, it + 1
-    return T, max_iters
+    increment).  The loop runs inside libfmx (fmx_register_points): one fused match +
+    linearization launch and one completion-word wait per iteration, no Python in
+    between.  Returns (pose, ICP iterations)."""
+    return ctx.register_points(np.hstack([np.eye(3), np.zeros((3, 1))]), w, 0.1, max_iters, thr)
 
 
 def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmup, profile):
@@ -435,7 +467,7 @@ def main():
             out = res[dists[0]]
             if len(dists) > 1:
                 out["wholemap"] = res["wholemap"]
-            print(json.dumps(out))
+            print(json.dumps(out), flush=True)
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
@@ -510,6 +542,9 @@ def main():
     work = ctx.match_work()
     ctx.profile(False)
     ctx.close()
+    multi = {}
+    for S in [int(x) for x in a.streams.split(",") if x.strip()]:
+        multi[str(S)] = concurrent_streams(S, new_ctx, scans, pre + a.warmup, a.steps, pipe, single, prev_aff)
     t_max = max_over_ranks(t_local, world, local)
     scans_total = sum_over_ranks(float(a.steps), world, local)
     # the sharded C5 registration beside the replica line: every rank takes part
@@ -571,6 +606,11 @@ def main():
         "counters": st_mean,
         "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
     }
+    if multi:
+        # S independent streams on one GPU (per rank), each its own context, stream and
+        # host thread: aggregate scans/s and the per-stream rate.  Not the headline (a
+        # single stream's rate bounds one robot's odometry); what one MI355X serves.
+        out["concurrent_streams"] = multi
     if ablation is not None:
         out["ablation"] = ablation
     if sequential is not None:
@@ -593,7 +633,7 @@ def main():
         out["cpu_baseline"]["single_thread"] = {"value": one["value"], "ms_per_scan": one["ms_per_scan"],
                                                 "sample": one["sample"]}
         out["ate"] = ate_block(host, opos, params, k0, local, single, pipe)
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -1485,6 +1485,50 @@ fmx_status fmx_linearize_matched(fmx_ctx* c, const double pose_j[12], double sig
   });
 }
 
+fmx_status fmx_register_points(fmx_ctx* c, const double pose_init[12], double max_dist, double sigma,
+                               uint32_t max_iters, double threshold, double pose_out[12], uint32_t* iters) {
+  return guard<false>(c, [&] {
+    c->lazy.pending = false;  // replaced by this loop's matches
+    if (!c->have_map) throw StatusError(FMX_E_STATE, "fmx_map_build first");
+    if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
+    if (!pose_init || !pose_out) throw StatusError(FMX_E_INVAL, "null pose");
+    if (!(max_dist > 0) || !(sigma > 0) || !(threshold >= 0)) throw StatusError(FMX_E_INVAL, "bad max_dist / sigma");
+    const bool fused = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) == 1 && !no_fused();
+    Pose T;
+    std::memcpy(T.m, pose_init, sizeof(T.m));
+    uint32_t it = 0;
+    double S[29];
+    while (it < max_iters) {
+      // Matcher::match at T + the summed single-pose system (all-reduced when sharded)
+      if (fused) {
+        run_match_linearize_total(c, T.m, max_dist, sigma, S);
+        c->lazy.pending = true;  // the last match stays available (launched on demand)
+        std::memcpy(c->lazy.pose, T.m, sizeof(T.m));
+        c->lazy.max_dist = max_dist;
+      } else {
+        run_match(c, T.m, max_dist, c->P.min_dist_map, false);
+        run_linearize_total(c, T.m, sigma, S);
+      }
+      ++it;
+      // Gauss-Newton on X(j): H dx = g from the packed 7 x 7 [H_j b]^T [H_j b]
+      double H[6][6], g[6], dx[6];
+      for (int r = 0; r < 7; ++r)
+        for (int q = r; q < 7; ++q) {
+          const double v = S[r * 7 - r * (r - 1) / 2 + (q - r)];
+          if (q < 6) H[r][q] = H[q][r] = v;
+          else if (r < 6) g[r] = v;
+        }
+      if (!chol_solve6(H, g, dx)) throw StatusError(FMX_E_STATE, "singular normal equations (too few matches)");
+      T = compose(T, expmap(dx));
+      double n2 = 0.0;
+      for (double x : dx) n2 += x * x;
+      if (std::sqrt(n2) < threshold) break;  // form.cpp:83-88
+    }
+    std::memcpy(pose_out, T.m, sizeof(T.m));
+    if (iters) *iters = it;
+  });
+}
+
 fmx_status fmx_comm_unique_id(uint8_t id[128]) {
   if (!id) return FMX_E_INVAL;
   try {

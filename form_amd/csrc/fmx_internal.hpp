@@ -1,6 +1,8 @@
 // fmx_internal.hpp — context layout and kernel-launcher interfaces of libfmx.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 
 #include <algorithm>
@@ -32,8 +34,8 @@ struct StatusError : std::runtime_error {
       throw ::fmx::HipError(std::string(#call) + ": " + hipGetErrorString(e_));              \
   } while (0)
 
-inline uint64_t& dbuf_reallocs() {  // diagnostic (FMX_HOST_TIMING prints it)
-  static uint64_t n = 0;
+inline std::atomic<uint64_t>& dbuf_reallocs() {  // diagnostic (FMX_HOST_TIMING prints it); contexts may
+  static std::atomic<uint64_t> n{0};              // live on several host threads
   return n;
 }
 // Growable device buffer (grows only; contents are not preserved across growth).
@@ -432,7 +434,7 @@ struct HostTiming {
     for (int i = 0; i < 16; ++i)
       if (n[i]) fprintf(stderr, "host %-14s %10.1f us total %8llu calls %8.2f us/call\n", names[i], t[i] * 1e6,
                         (unsigned long long)n[i], t[i] * 1e6 / n[i]);
-    fprintf(stderr, "host device-buffer reallocations %llu\n", (unsigned long long)dbuf_reallocs());
+    fprintf(stderr, "host device-buffer reallocations %llu\n", (unsigned long long)dbuf_reallocs().load());
   }
 };
 inline HostTiming& host_timing() {

@@ -82,7 +82,7 @@ EXPORTED = [
     "fmx_current_pose",
     "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
     "fmx_profile_name", "fmx_profile_read", "fmx_sync", "fmx_comm_unique_id", "fmx_comm_init",
-    "fmx_map_download",
+    "fmx_map_download", "fmx_register_points",
 ]
 
 
@@ -311,6 +311,18 @@ class Context:
         out = np.zeros(29)
         self._chk(self._L.fmx_linearize_matched(self.h, _p(pose), C.c_double(sigma), _p(out)))
         return out[:28].copy(), float(out[28])
+
+    def register_points(self, pose_init34, max_dist: float, sigma: float = 0.1, max_iters: int = 30,
+                        threshold: float = 1e-4):
+        """fmx_register_points: Gauss-Newton ICP of the query set against the built map
+        (match + summed 7x7 + solve per iteration, all in libfmx).  Returns (pose 3x4,
+        iterations)."""
+        T0 = np.ascontiguousarray(pose_init34, np.float64).reshape(12)
+        T = np.zeros(12)
+        it = C.c_uint32(0)
+        self._chk(self._L.fmx_register_points(self.h, _p(T0), C.c_double(max_dist), C.c_double(sigma),
+                                              C.c_uint32(max_iters), C.c_double(threshold), _p(T), C.byref(it)))
+        return T.reshape(3, 4), int(it.value)
 
     # ---------------------------------------------------------------- multi-GPU
     def comm_init(self, unique_id: bytes, nranks: int, rank: int):

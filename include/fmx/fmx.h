@@ -176,6 +176,18 @@ fmx_status fmx_error(fmx_ctx* ctx, const double* poses_i34, const double* poses_
  * packed upper 7 x 7, out[28]: the error 0.5 ||r/sigma||^2. */
 fmx_status fmx_linearize_matched(fmx_ctx* ctx, const double pose_j34[12], double sigma, double out[29]);
 
+/* Point-set registration against the built map in the single-pose formulation (the
+ * 2M-point C5 configuration): from pose_init, iterate
+ *   Matcher::match at X (matcher.hpp:67-112) -> the summed 7 x 7 [H_j b]^T [H_j b]
+ *   (gtsam.hpp:67-86, 144-170; all-reduced over the communicator's ranks, below) ->
+ *   Gauss-Newton step H dx = g -> X <- X Exp(dx)
+ * until ||dx|| < threshold (form.cpp:83-88's break) or max_iters iterations.  The whole
+ * loop runs in libfmx (on large query sets each iteration is one fused launch); every
+ * rank of a communicator computes the identical iterate.  pose_out: the result, *iters
+ * (may be NULL): the iterations run.  FMX_E_STATE if a system is singular. */
+fmx_status fmx_register_points(fmx_ctx* ctx, const double pose_init34[12], double max_dist, double sigma,
+                               uint32_t max_iters, double threshold, double pose_out34[12], uint32_t* iters);
+
 /* ---------------- multi-GPU: the sharded C5 path -----------
  * One rank per GPU, each with the same voxel map and a contiguous shard of the
  * queries.  fmx_comm_unique_id on one rank; the caller shares the 128 bytes (e.g. a

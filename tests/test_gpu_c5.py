@@ -118,6 +118,37 @@ def test_c5_registration_converges(fmx_mod, c5_map):
     assert et < 0.02 * e0t and er < 0.02 * e0r, (et, er, e0t, e0r)
 
 
+def test_register_points_equals_python_loop(fmx_mod, c5_map):
+    """fmx_register_points (the ICP loop inside libfmx, bench.py's C5 step) follows the
+    same iterates as the loop driven from Python over fmx_match + fmx_linearize_matched
+    (its 6 x 6 solve is a Cholesky instead of numpy's LU: iterates agree to 1e-9), on
+    the fused (large query set) and the materialized (small set) paths."""
+    pos4, nrm4 = c5_map
+    Tt = shard.c5_offset()
+    for n in (300000, 50000):
+        q4, n4 = shard.make_queries(pos4, nrm4, n, Tt, 0.03, 83)
+        ctx = _ctx(fmx_mod, pos4.shape[0])
+        ctx.keypoints_add_device(0, pos4, nrm4)
+        ctx.map_build([0], I34[None], W)
+        ctx.set_queries_device(q4, n4)
+        T = I34.copy()
+        for it in range(30):
+            ctx.match(T, W, counts=False)
+            S, _ = ctx.linearize_matched(T, 0.1)
+            dx = shard.gauss_newton_step(S)
+            T = shard.compose(T, shard.expmap(dx))
+            if np.linalg.norm(dx) < 1e-4:
+                break
+        T2, iters = ctx.register_points(I34, W, 0.1, 30, 1e-4)
+        assert iters == it + 1, (n, iters, it + 1)
+        assert np.abs(T2 - T).max() < 1e-9, (n, np.abs(T2 - T).max())
+        et, _ = shard.pose_error(T2, Tt)
+        assert et < 0.001
+        got = ctx.match_download()  # the last iterate's match is still available
+        assert (got["pair"] >= 0).sum() > 0.9 * n
+        ctx.close()
+
+
 def test_fused_match_linearize(fmx_mod, oracle, c5_map):
     """fmx_match without counts on a large query set is deferred; fmx_linearize_matched
     at the same pose then runs match + linearization in one launch (no per-query
