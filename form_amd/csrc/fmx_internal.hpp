@@ -450,7 +450,6 @@ struct MatchDiag {
   uint64_t launches = 0;
   double span = 0, p50 = 0, p90 = 0, p99 = 0, pmax = 0, f50 = 0, f90 = 0, f99 = 0, mq_all = 0, mq_slow = 0;
   uint64_t mq_hist[8] = {0};
-  double split[4] = {0, 0, 0, 0};  // FMX_MATCH_SPLIT builds: pass-0, walk-1, pass>=1 candidates, all
   ~MatchDiag() {
     if (!on || !launches) return;
     const double n = (double)launches;
@@ -462,9 +461,6 @@ struct MatchDiag {
     fprintf(stderr, "match diag: block max-query-cands histogram <16 <32 <64 <128 <256 <512 <1024 >=1024:");
     for (uint64_t h : mq_hist) fprintf(stderr, " %llu", (unsigned long long)h);
     fprintf(stderr, "\n");
-    if (split[0] + split[1] + split[2] > 0)
-      fprintf(stderr, "match diag: candidates: pass 0 %.1f%%, walk 1 %.1f%%, passes >= 1 %.1f%%\n",
-              100 * split[0] / split[3], 100 * split[1] / split[3], 100 * split[2] / split[3]);
   }
 };
 inline MatchDiag& match_diag() {
@@ -504,12 +500,6 @@ inline void match_diag_add(const uint32_t* w, uint32_t nb) {
   d.f90 += pct(fin, 0.9);
   d.f99 += pct(fin, 0.99);
   d.mq_all += mq / nb;
-  for (uint32_t b = 0; b < nb; ++b) {
-    d.split[0] += w[8 * b + 3];
-    d.split[1] += w[8 * b + 6];
-    d.split[2] += w[8 * b + 7];
-    d.split[3] += w[8 * b + 1];
-  }
   const size_t ns = std::max<size_t>(1, nb / 100);
   double ms = 0;
   for (size_t i = nb - ns; i < nb; ++i) ms += by[i].second;
