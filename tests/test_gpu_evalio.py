@@ -129,3 +129,32 @@ def test_form_planar_ablation(fmx_mod, oracle):
         To, _, _ = oest.register_scan(s.numpy())
         assert np.abs(f.pose()[:3] - To).max() < 1e-6, k
     assert len(f.map()["point"]) == 0
+
+
+def test_map_download_edge_cases(fmx_mod):
+    """fmx_map_download before any registered scan is a state error; a buffer smaller
+    than the map is a size error; the size query needs no buffers."""
+    import ctypes as C
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p)))
+    with pytest.raises(fmx_mod.FmxError) as e:
+        ctx.map_download(0.1)
+    assert e.value.status == 5  # FMX_E_STATE
+    world = synth.World()
+    for k in range(3):
+        ctx.register_scan(synth.make_scan("tiny", k, world=world)[0].to("cuda:0"))
+    L = fmx_mod.lib()
+    npl, npt = C.c_uint32(0), C.c_uint32(0)
+    assert L.fmx_map_download(ctx.h, C.c_double(0.1), None, None, C.byref(npl), None, None, C.byref(npt)) == 0
+    assert npl.value > 0 and npt.value > 0
+    small = np.zeros(6 * (npl.value - 1))
+    cap, cap2 = C.c_uint32(npl.value - 1), C.c_uint32(npt.value)
+    pt = np.zeros(3 * npt.value)
+    st = L.fmx_map_download(ctx.h, C.c_double(0.1), small.ctypes.data_as(C.c_void_p), None, C.byref(cap),
+                            pt.ctypes.data_as(C.c_void_p), None, C.byref(cap2))
+    assert st == 2  # FMX_E_SIZE
+    assert L.fmx_map_download(ctx.h, C.c_double(0.0), None, None, C.byref(npl), None, None, C.byref(npt)) == 1
+    m = ctx.map_download(0.1)
+    assert len(m["planar"][0]) == npl.value and len(m["point"][0]) == npt.value
+    ctx.close()
