@@ -543,7 +543,7 @@ def main():
     ctx.profile(False)
     ctx.close()
     multi = {}
-    for S in [int(x) for x in a.streams.split(",") if x.strip()]:
+    for S in ([int(x) for x in a.streams.split(",") if x.strip()] if world == 1 else []):  # a per-GPU figure
         multi[str(S)] = concurrent_streams(S, new_ctx, scans, pre + a.warmup, a.steps, pipe, single, prev_aff)
     t_max = max_over_ranks(t_local, world, local)
     scans_total = sum_over_ranks(float(a.steps), world, local)

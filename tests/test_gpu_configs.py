@@ -125,3 +125,29 @@ def test_register_stream_c2_full_window(fmx_mod, oracle):
     """32 C2 scans (64 x 1024), smoothing mode, window full."""
     maxd, stats = _stream(fmx_mod, oracle, "c2", 32, pipelined=True)
     assert stats["sequential"]["map_scans"] >= 10
+
+
+@pytest.mark.parametrize("single", [False, True])
+def test_register_stream_with_blank_and_sparse_scans(fmx_mod, oracle, single):
+    """A sensor blackout (an all-zero scan: every point fails the range check, so no
+    feature and no match: the LM keeps the prediction) and a scan with half its points
+    dropped, inside a C2 stream: both paths handle them alike and recover."""
+    geo = synth.GEOMETRIES["c2"]
+    p = synth.default_params(geo)
+    world = synth.World()
+    prm = oracle.default_params(p) if not single else _single(oracle, p)
+    oest = oracle.Estimator(prm)
+    ctx = _ctx(fmx_mod, p, disable_smoothing=single)
+    g = torch.Generator().manual_seed(5)
+    for k in range(16):
+        s, _, _ = synth.make_scan("c2", k, world=world)
+        if k == 6:
+            s = torch.zeros_like(s)
+        elif k == 9:
+            s = torch.where((torch.rand(s.shape[0], generator=g) < 0.5)[:, None], torch.zeros_like(s), s)
+        ctx.register_scan(s.to("cuda:0"))
+        To, _, _ = oest.register_scan(s.numpy())
+        d = float(np.abs(ctx.current_pose() - To).max())
+        assert d < 1e-6, (k, d)
+        if k == 6:
+            assert ctx.last_stats()["matched_planar"] + ctx.last_stats()["matched_point"] == 0
