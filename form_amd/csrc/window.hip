@@ -39,7 +39,8 @@ namespace {
 
 constexpr int kWinWaves = kPlaneChunk / kWave;  // waves per block: one chunk, one 64-row step per wave
 // (128-row chunks measured slower, 0.22 vs 0.19 ms per scan; a one-wave block, 64 rows,
-// is not a supported configuration: its C4 stream diverged, profiles/r3_ab_c4_window_rows.txt)
+// is not a supported configuration: its C4 stream came out different — 2.4x the probes
+// and candidates per match query, not a parity-tested build; profiles/r3_ab_c4_window_rows.txt)
 static_assert(kPlaneChunk == kPointChunk && kPlaneChunk % kWave == 0 && kWinWaves >= 2 && kWinWaves <= 16,
               "window chunking");
 constexpr int kFinBatch = 16;   // chunk partials in flight per thread in the pair finisher
