@@ -598,6 +598,17 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
   else return (ballot >> ((lane_id() / G) * G)) & ((1ull << G) - 1);
 }
 
+#ifndef FMX_COMPACT_SHIFTS
+#define FMX_COMPACT_SHIFTS 1  // one-lane-per-query ring-1 search from a per-lane work list (A/B switch)
+#endif
+// The ring-1 shifts (c_shift[0..26], the reference's voxel_shifts order, map.tpp:54-68)
+// as bit masks over the shift index: bit s of kShiftXP is set when shift s has dx = +1,
+// of kShiftXN when dx = -1, and so on — a lane decodes ITS shift without a table load.
+constexpr uint32_t kShiftXP = 0x781982u, kShiftXN = 0x7806604u, kShiftYP = 0x1998288u, kShiftYN = 0x6660510u,
+                   kShiftZP = 0x2aaa820u, kShiftZN = 0x5555040u;
+__device__ __forceinline__ int shift_axis(uint32_t pos, uint32_t neg, int s) {
+  return (int)((pos >> s) & 1u) - (int)((neg >> s) & 1u);
+}
 // VoxelMap::find_closest (map.tpp:70-91) of one query by a group of G lanes (lane g of
 // the group), bounded by the incoming best (a.bound, or +inf).
 template <int G, bool DENSE>
@@ -833,7 +844,14 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
   // (records split over the lanes), re-checking each bound against the shared best.
   // One loop over the passes, so the cell walk is emitted once.
   const int npass = a.rings >= 2 ? 4 : 3;
-  for (int ip = 0; ip < npass; ++ip) {
+  // One lane per query, plain cells, one ring (the large-set build, C5): after the own
+  // cell, each lane walks ITS OWN list of the ring-1 cells whose bound admits them, one
+  // cell per step, instead of the wave stepping through all 26 shifts (probing a shift
+  // whenever any of its 64 queries needs it).  The wave then takes as many dependent
+  // probe + record rounds as its busiest query, not as the union of its queries' cells.
+  constexpr bool kCompact = G == 1 && !DENSE && FMX_COMPACT_SHIFTS;
+  const bool compact = kCompact && a.rings == 1;
+  for (int ip = 0; ip < (compact ? 1 : npass); ++ip) {
     const int s_begin = ip == 0 ? 0 : (ip == 1 ? 1 : (ip == 2 ? 7 : 27));
     const int s_end = ip == 0 ? 1 : (ip == 1 ? 7 : (ip == 2 ? 27 : 125));
     for (int s0 = s_begin; s0 < s_end; s0 += G) {  // one shift per lane per chunk
@@ -876,6 +894,59 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         const int sl = s0 + l;
         scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2],
                   srank(c_shift[sl][0], c_shift[sl][1], c_shift[sl][2]));
+      }
+    }
+  }
+  if constexpr (kCompact) {
+    if (compact && inr) {
+      // the query's squared distance (1e-9 slack, as shift_lb) to its cell's low / high
+      // face per axis, rounded down to fp32; a shift's bound is the sum of its axes'
+      // terms.  The test against best allows for the fp32 sum's rounding (threshold
+      // rounded up, x (1 + 2^-20)), so a cell is skipped only when shift_lb would skip
+      // it: the winner is unchanged.
+      float fl[3], fh[3];
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        const int ba = ax == 0 ? bx : (ax == 1 ? by : bz);
+        const double lo = fmax(wq[ax] - ba * a.w - 1e-9, 0.0), hi = fmax((ba + 1) * a.w - wq[ax] - 1e-9, 0.0);
+        fl[ax] = __double2float_rd(lo * lo);
+        fh[ax] = __double2float_rd(hi * hi);
+      }
+      auto term = [&](int ax, int d) { return d > 0 ? fh[ax] : (d < 0 ? fl[ax] : 0.0f); };
+      auto thresh = [&]() { return __double2float_ru(best) * (1.0f + 0x1p-20f); };
+      uint32_t todo = 0;
+      {
+        const float bt = thresh();
+#pragma unroll
+        for (int s = 1; s < 27; ++s) {
+          const int dx = shift_axis(kShiftXP, kShiftXN, s), dy = shift_axis(kShiftYP, kShiftYN, s),
+                    dz = shift_axis(kShiftZP, kShiftZN, s);
+          if ((term(0, dx) + term(1, dy)) + term(2, dz) <= bt) todo |= 1u << s;
+        }
+      }
+      // faces (1..6) pop before edges (7..18) and corners (19..26): increasing bound
+      while (todo) {
+        const int s = __ffs(todo) - 1;
+        todo &= todo - 1;
+        const int dx = shift_axis(kShiftXP, kShiftXN, s), dy = shift_axis(kShiftYP, kShiftYN, s),
+                  dz = shift_axis(kShiftZP, kShiftZN, s);
+        if ((term(0, dx) + term(1, dy)) + term(2, dz) > thresh()) continue;  // best has moved
+        uint32_t vf = 0, vc = 0;
+        bool vd = false;
+        probe(dx, dy, dz, vf, vc, vd);
+        const uint32_t rk = (uint32_t)s << 27;  // one ring: the reference rank is the shift index
+        if (vc <= (uint32_t)kSmallCell) {
+          double4 pr[kSmallCell];
+#pragma unroll
+          for (int u = 0; u < kSmallCell; ++u)
+            if (u < (int)vc) pr[u] = M.pos[vf + u];
+#pragma unroll
+          for (int u = 0; u < kSmallCell; ++u)
+            if (u < (int)vc) fold(pr[u], vf + u, rk);
+          n_cand += vc;
+        } else {
+          scan_cell(vf, vc, false, bx + dx, by + dy, bz + dz, rk);
+        }
       }
     }
   }
