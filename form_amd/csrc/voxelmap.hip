@@ -601,6 +601,9 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_COMPACT_SHIFTS
 #define FMX_COMPACT_SHIFTS 1  // one-lane-per-query ring-1 search from a per-lane work list (A/B switch)
 #endif
+#ifndef FMX_PROBE_TOGETHER
+#define FMX_PROBE_TOGETHER 1  // brick key and cell range in flight together (A/B switch)
+#endif
 // The ring-1 shifts (c_shift[0..26], the reference's voxel_shifts order, map.tpp:54-68)
 // as bit masks over the shift index: bit s of kShiftXP is set when shift s has dx = +1,
 // of kShiftXN when dx = -1, and so on — a lane decodes ITS shift without a table load.
@@ -625,13 +628,14 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
               dz = ((bz + sz) >> sh) - (bz >> sh);
     return (uint32_t)c_refrank[(dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)] << 27;
   };
+  // the tie rank of shift s: on an unsubdivided map the shift IS the reference voxel
+  // shift, whose rank is its index (c_shift[0..26] = voxel_shifts, map.tpp:54-68)
+  auto srank_s = [&](int s) -> uint32_t {
+    return sh == 0 && s < 27 ? (uint32_t)s << 27 : srank(c_shift[s][0], c_shift[s][1], c_shift[s][2]);
+  };
   // one bucket read per probe: key, the cell's two boundaries and its dense bit in
   // flight together; a bucket of another build epoch ends the chain (empty)
-  auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count, bool& dense) {
-    const int X = bx + sx, Y = by + sy, Z = bz + sz;
-    const unsigned long long key = brick_key(X, Y, Z, M.epoch);
-    const uint32_t ci = brick_cell(X, Y, Z);
-    uint64_t h = mix64(key) & M.mask;
+  auto walk = [&](unsigned long long key, uint32_t ci, uint64_t h, uint32_t& first, uint32_t& count, bool& dense) {
     first = 0;
     count = 0;
     dense = false;
@@ -640,6 +644,14 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       const Brick* b = M.bricks + h;
       const unsigned long long k = b->key;
       const uint32_t b0 = b->beg[ci], b1 = b->beg[ci + 1], dm = b->dense;
+      // one lane per query: the cell's range is read with the key, not after its
+      // compare (the compiler sinks these loads into the hit branch: a second dependent
+      // round; C5 -2..4 %).  The 8-lane build keeps the sunk loads (its registers are
+      // tighter: C4 match +3 % with them hoisted).
+      if constexpr (G == 1 && FMX_PROBE_TOGETHER) {
+        asm volatile("" ::"v"(b0), "v"(b1));
+        if constexpr (DENSE) asm volatile("" ::"v"(dm));
+      }
       if (k == key) {
         first = b0;
         count = b1 - b0;
@@ -649,6 +661,11 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       if (key_epoch(k) != M.epoch) return;
       h = (h + 1) & M.mask;
     }
+  };
+  auto probe = [&](int sx, int sy, int sz, uint32_t& first, uint32_t& count, bool& dense) {
+    const int X = bx + sx, Y = by + sy, Z = bz + sz;
+    const unsigned long long key = brick_key(X, Y, Z, M.epoch);
+    walk(key, brick_cell(X, Y, Z), mix64(key) & M.mask, first, count, dense);
   };
   // a record is one double4: world position + its build order in .w (exact in a
   // double), so a candidate test is one 32-B load
@@ -871,7 +888,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       // the argmin on (d^2, tie key) does not depend on the folding order
       const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
       if (small) {
-        const uint32_t rk = srank(c_shift[s][0], c_shift[s][1], c_shift[s][2]);
+        const uint32_t rk = srank_s(s);
         double4 pr[kSmallCell];
 #pragma unroll
         for (int u = 0; u < kSmallCell; ++u)
@@ -892,8 +909,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         const uint32_t first = __shfl(vf, l, G);
         const bool dn = __shfl((int)vd, l, G) != 0;
         const int sl = s0 + l;
-        scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2],
-                  srank(c_shift[sl][0], c_shift[sl][1], c_shift[sl][2]));
+        scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2], srank_s(sl));
       }
     }
   }
