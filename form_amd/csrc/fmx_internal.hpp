@@ -450,9 +450,13 @@ struct MatchDiag {
   uint64_t launches = 0;
   double span = 0, p50 = 0, p90 = 0, p99 = 0, pmax = 0, f50 = 0, f90 = 0, f99 = 0, mq_all = 0, mq_slow = 0;
   uint64_t mq_hist[8] = {0};
+  double walk_rounds = 0, walk_steps = 0, walk_listed = 0, waves = 0;  // FMX_DIAG_WALK builds
   ~MatchDiag() {
     if (!on || !launches) return;
     const double n = (double)launches;
+    if (walk_listed > 0)
+      fprintf(stderr, "match diag: ring-1 list walk: %.2f rounds per wave, %.3f steps and %.3f listed cells per query\n",
+              walk_rounds / waves, walk_steps / (waves * 64), walk_listed / (waves * 64));
     fprintf(stderr,
             "match diag: %llu launches; span %.1f us; block dur p50 %.1f p90 %.1f p99 %.1f max %.1f us; "
             "blocks done at 50/90/99%%: %.1f %.1f %.1f us; max query cands per block: mean %.1f, slowest 1%% %.1f\n",
@@ -467,7 +471,8 @@ inline MatchDiag& match_diag() {
   static MatchDiag d;
   return d;
 }
-// w: kWorkWords (8) words per block: probes, cands, max query cands, 0, t_begin, t_end, 0, 0
+// w: kWorkWords (8) words per block: probes, cands, max query cands, walk rounds, t_begin, t_end,
+// walk steps, listed cells (the walk words: FMX_DIAG_WALK builds, else 0)
 inline void match_diag_add(const uint32_t* w, uint32_t nb) {
   MatchDiag& d = match_diag();
   if (!d.on || nb == 0) return;
@@ -481,6 +486,10 @@ inline void match_diag_add(const uint32_t* w, uint32_t nb) {
     dur[b] = (double)(int32_t)(w[8 * b + 5] - w[8 * b + 4]) * 0.01;  // 100 MHz -> us
     fin[b] = (double)(int32_t)(w[8 * b + 5] - t0) * 0.01;
     by.push_back({dur[b], w[8 * b + 2]});
+    d.walk_rounds += w[8 * b + 3];
+    d.walk_steps += w[8 * b + 6];
+    d.walk_listed += w[8 * b + 7];
+    d.waves += 4;  // waves per match block (256 threads)
     mq += w[8 * b + 2];
     int h = 0;
     for (uint32_t v = w[8 * b + 2]; v >= 16 && h < 7; v >>= 1) ++h;

@@ -604,20 +604,32 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_PROBE_TOGETHER
 #define FMX_PROBE_TOGETHER 1  // brick key and cell range in flight together (A/B switch)
 #endif
-// The ring-1 shifts (c_shift[0..26], the reference's voxel_shifts order, map.tpp:54-68)
-// as bit masks over the shift index: bit s of kShiftXP is set when shift s has dx = +1,
-// of kShiftXN when dx = -1, and so on — a lane decodes ITS shift without a table load.
-constexpr uint32_t kShiftXP = 0x781982u, kShiftXN = 0x7806604u, kShiftYP = 0x1998288u, kShiftYN = 0x6660510u,
-                   kShiftZP = 0x2aaa820u, kShiftZN = 0x5555040u;
-__device__ __forceinline__ int shift_axis(uint32_t pos, uint32_t neg, int s) {
-  return (int)((pos >> s) & 1u) - (int)((neg >> s) & 1u);
+// The 26 ring-1 cells relative to a query's octant, nearest first: component i along
+// the query's i-th nearest axis is +1 (toward its near face), -1 (far face) or 0.
+// Cells 0..6 are the near faces, edges and corner; 7..25 hold a far side.  Bit k of
+// kRel0P is set when cell k's component 0 is +1, of kRel0N when it is -1, and so on:
+// a lane decodes ITS cell without a table load.
+constexpr uint32_t kRel0P = 0x581455u, kRel0N = 0x3a32880u, kRel1P = 0xa84866u, kRel1N = 0x3558500u,
+                   kRel2P = 0x130a078u, kRel2N = 0x2ce5200u;
+constexpr int kRelNear = 7;
+__device__ __forceinline__ int shift_axis(uint32_t pos, uint32_t neg, int k) {
+  return (int)((pos >> k) & 1u) - (int)((neg >> k) & 1u);
+}
+// index of ring-1 shift (dx, dy, dz) != 0 in c_shift / the reference's voxel_shifts
+// (map.tpp:54-68): faces 1..6, edges 7..18 (xy, xz, yz), corners 19..26
+__device__ __forceinline__ int ring1_index(int dx, int dy, int dz) {
+  const int nz = (dx != 0) + (dy != 0) + (dz != 0);
+  if (nz == 1) return dx != 0 ? 1 + (dx < 0) : (dy != 0 ? 3 + (dy < 0) : 5 + (dz < 0));
+  if (nz == 2)
+    return dz == 0 ? 7 + 2 * (dx < 0) + (dy < 0) : (dy == 0 ? 11 + 2 * (dx < 0) + (dz < 0) : 15 + 2 * (dy < 0) + (dz < 0));
+  return 19 + 4 * (dx < 0) + 2 * (dy < 0) + (dz < 0);
 }
 // VoxelMap::find_closest (map.tpp:70-91) of one query by a group of G lanes (lane g of
 // the group), bounded by the incoming best (a.bound, or +inf).
 template <int G, bool DENSE>
 __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, const double (&wq)[3], int g,
                                           uint32_t* hd, double& best, uint32_t& best_rid, uint32_t& best_i,
-                                          uint32_t& n_probe, uint32_t& n_cand) {
+                                          uint32_t& n_probe, uint32_t& n_cand, uint32_t& n_iter, uint32_t& n_list) {
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
   // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
   // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
@@ -915,42 +927,95 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
   }
   if constexpr (kCompact) {
     if (compact && inr) {
-      // the query's squared distance (1e-9 slack, as shift_lb) to its cell's low / high
-      // face per axis, rounded down to fp32; a shift's bound is the sum of its axes'
-      // terms.  The test against best allows for the fp32 sum's rounding (threshold
-      // rounded up, x (1 + 2^-20)), so a cell is skipped only when shift_lb would skip
-      // it: the winner is unchanged.
-      float fl[3], fh[3];
+      // Per axis: the query's squared distance (1e-9 slack, as shift_lb) to its cell's
+      // near and far face, rounded down to fp32, and the near side's sign; the axes
+      // sorted by near distance.  The 26 ring-1 cells are listed RELATIVE to that
+      // frame, nearest first (kRel*: the near faces, edges and corner of the query's
+      // octant, then every cell with a far side, whose bound is at least the smallest
+      // far term >= (w/2)^2).  A shift's bound is the sum of its axes' terms; the test
+      // against best allows for the fp32 sum's rounding (threshold rounded up,
+      // x (1 + 2^-20)), so a cell is skipped only when shift_lb would skip it: the
+      // winner is unchanged (the argmin on (d^2, tie) does not depend on visit order).
+      // nr / fr: near / far terms in sorted order; cd: per sorted slot i, bits 3i..3i+1
+      // the grid axis and bit 3i+2 set when the near face is the low one
+      float nr[3], fr[3];
+      uint32_t cd[3];
 #pragma unroll
-      for (int ax = 0; ax < 3; ++ax) {
-        const int ba = ax == 0 ? bx : (ax == 1 ? by : bz);
-        const double lo = fmax(wq[ax] - ba * a.w - 1e-9, 0.0), hi = fmax((ba + 1) * a.w - wq[ax] - 1e-9, 0.0);
-        fl[ax] = __double2float_rd(lo * lo);
-        fh[ax] = __double2float_rd(hi * hi);
+      for (int k = 0; k < 3; ++k) {
+        const int ba = k == 0 ? bx : (k == 1 ? by : bz);
+        const double lo = fmax(wq[k] - ba * a.w - 1e-9, 0.0), hi = fmax((ba + 1) * a.w - wq[k] - 1e-9, 0.0);
+        const float l2 = __double2float_rd(lo * lo), h2 = __double2float_rd(hi * hi);
+        nr[k] = fminf(l2, h2);
+        fr[k] = fmaxf(l2, h2);
+        cd[k] = (uint32_t)k | (h2 <= l2 ? 0u : 4u);
       }
-      auto term = [&](int ax, int d) { return d > 0 ? fh[ax] : (d < 0 ? fl[ax] : 0.0f); };
-      auto thresh = [&]() { return __double2float_ru(best) * (1.0f + 0x1p-20f); };
-      uint32_t todo = 0;
-      {
-        const float bt = thresh();
-#pragma unroll
-        for (int s = 1; s < 27; ++s) {
-          const int dx = shift_axis(kShiftXP, kShiftXN, s), dy = shift_axis(kShiftYP, kShiftYN, s),
-                    dz = shift_axis(kShiftZP, kShiftZN, s);
-          if ((term(0, dx) + term(1, dy)) + term(2, dz) <= bt) todo |= 1u << s;
+      auto cswap = [&](int i, int j) {  // sort the axes by near term (3-element network)
+        if (nr[j] < nr[i]) {
+          float t = nr[i]; nr[i] = nr[j]; nr[j] = t;
+          t = fr[i]; fr[i] = fr[j]; fr[j] = t;
+          const uint32_t u = cd[i]; cd[i] = cd[j]; cd[j] = u;
         }
-      }
-      // faces (1..6) pop before edges (7..18) and corners (19..26): increasing bound
-      while (todo) {
-        const int s = __ffs(todo) - 1;
-        todo &= todo - 1;
-        const int dx = shift_axis(kShiftXP, kShiftXN, s), dy = shift_axis(kShiftYP, kShiftYN, s),
-                  dz = shift_axis(kShiftZP, kShiftZN, s);
-        if ((term(0, dx) + term(1, dy)) + term(2, dz) > thresh()) continue;  // best has moved
+      };
+      cswap(0, 1);
+      cswap(1, 2);
+      cswap(0, 1);
+      const uint32_t code = cd[0] | cd[1] << 3 | cd[2] << 6;
+      auto term = [&](int i, int r) { return r > 0 ? nr[i] : (r < 0 ? fr[i] : 0.0f); };
+      auto thresh = [&]() { return __double2float_ru(best) * (1.0f + 0x1p-20f); };
+      auto list = [&](int k0, int k1) {  // the cells k0..k1-1 admitted by the current best
+        const float bt = thresh();
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 26; ++k)
+          if (k >= k0 && k < k1 &&
+              (term(0, shift_axis(kRel0P, kRel0N, k)) + term(1, shift_axis(kRel1P, kRel1N, k))) +
+                      term(2, shift_axis(kRel2P, kRel2N, k)) <= bt)
+            m |= 1u << k;
+        return m;
+      };
+      uint32_t todo = list(0, kRelNear);
+      n_list += __popc(todo);
+      bool far_listed = false;
+      for (;;) {
+        // this lane's next admitted cell (bounds re-checked against the current best)
+        int k = -1;
+        for (;;) {
+          if (!todo) {
+            if (far_listed || thresh() < fminf(fminf(fr[0], fr[1]), fr[2])) break;  // no far-side cell can win
+            far_listed = true;
+            todo = list(kRelNear, 26);
+            n_list += __popc(todo);
+            continue;
+          }
+          const int kk = __ffs(todo) - 1;
+          todo &= todo - 1;
+          const int r0 = shift_axis(kRel0P, kRel0N, kk), r1 = shift_axis(kRel1P, kRel1N, kk),
+                    r2 = shift_axis(kRel2P, kRel2N, kk);
+          if ((term(0, r0) + term(1, r1)) + term(2, r2) <= thresh()) {
+            k = kk;
+            break;
+          }
+        }
+        if (k < 0) break;
+        ++n_iter;
+        // back to grid axes
+        int d[3] = {0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const uint32_t c = code >> (3 * i);
+          const int r = shift_axis(i == 0 ? kRel0P : (i == 1 ? kRel1P : kRel2P),
+                                   i == 0 ? kRel0N : (i == 1 ? kRel1N : kRel2N), k);
+          const int q = (c & 4u) ? -r : r;
+          const uint32_t a3 = c & 3u;
+          d[0] += a3 == 0 ? q : 0;
+          d[1] += a3 == 1 ? q : 0;
+          d[2] += a3 == 2 ? q : 0;
+        }
+        const int dx = d[0], dy = d[1], dz = d[2];
         uint32_t vf = 0, vc = 0;
         bool vd = false;
         probe(dx, dy, dz, vf, vc, vd);
-        const uint32_t rk = (uint32_t)s << 27;  // one ring: the reference rank is the shift index
+        const uint32_t rk = (uint32_t)ring1_index(dx, dy, dz) << 27;  // one ring: the rank is the shift index
         if (vc <= (uint32_t)kSmallCell) {
           double4 pr[kSmallCell];
 #pragma unroll
@@ -1079,7 +1144,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   if (threadIdx.x == 0) s_ins = 0;
   __syncthreads();
   const uint32_t t_begin = (uint32_t)wall_clock64();
-  uint32_t n_probe = 0, n_cand = 0;
+  uint32_t n_probe = 0, n_cand = 0, n_iter = 0, n_list = 0;  // (walk counts: FMX_DIAG_WALK builds only)
   auto world_query = [&](uint32_t q, double (&wq)[3]) {
     const float4 lq = planar ? q_pl[q] : q_pt[q];
     d_xform(Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
@@ -1121,7 +1186,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     world_query(qi, wq);
     uint32_t best_rid = 0xFFFFFFFFu;
     nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, n_probe,
-                             n_cand);
+                             n_cand, n_iter, n_list);
   }
   // work counters for the algorithmic-byte model and the match diagnostics (one plain
   // store per block, summed on the host): probes, candidate records, the largest
@@ -1138,6 +1203,20 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     s_work[1][threadIdx.x / kWave] = wc;
     s_work[2][threadIdx.x / kWave] = qc;
   }
+#ifdef FMX_DIAG_WALK  // per block: sum over waves of the wave's walk rounds, lanes' walk steps, listed cells
+  __shared__ uint32_t s_walk[3][kMatchThreads / kWave];
+  {
+    uint32_t wr = n_iter;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) wr = max(wr, (uint32_t)__shfl_xor(wr, o, 64));
+    const uint32_t wi = wave_sum(n_iter), wl = wave_sum(n_list);
+    if (lane_id() == 0) {
+      s_walk[0][threadIdx.x / kWave] = wr;
+      s_walk[1][threadIdx.x / kWave] = wi;
+      s_walk[2][threadIdx.x / kWave] = wl;
+    }
+  }
+#endif
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t tp = 0, tc = 0, mq = 0;
@@ -1147,9 +1226,18 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
       mq = max(mq, s_work[2][i]);
     }
     uint4* w4 = reinterpret_cast<uint4*>(work) + 2 * blockIdx.x;
-    w4[0] = make_uint4(tp, tc, mq, 0u);
-    w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), 0u, 0u);
+    uint32_t d0 = 0, d1 = 0, d2 = 0;
+#ifdef FMX_DIAG_WALK
+    for (int i = 0; i < kMatchThreads / kWave; ++i) {
+      d0 += s_walk[0][i];
+      d1 += s_walk[1][i];
+      d2 += s_walk[2][i];
+    }
+#endif
+    w4[0] = make_uint4(tp, tc, mq, d0);
+    w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), d1, d2);
   }
+
   if constexpr (!FUSED) {
     if (qi < nq && g == 0) emit(qi, best, best_i);
   } else {
@@ -1178,6 +1266,9 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     double H[12], av[7];
 #pragma unroll
     for (int i = 0; i < 12; ++i) H[i] = 0.0;
+#ifdef FMX_DIAG_NOEPI  // diagnostic build: no rows (instruction-count split of the kernel)
+    accs[0][0] = acc_q ? 1e-300 * (pi[0] + ni[0] + Ti[0]) : 0.0;
+#else
     if (planar) {  // block-uniform: a block holds one feature type
       double r = 0.0;
       if (acc_q) plane_row<1>(Ti, Tj, pi, ni, pj, r, H);
@@ -1198,6 +1289,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         fz_stage_mfma(rows, av, acc_q, accs);
       }
     }
+#endif
     const f64x4 acc = accs[0] + accs[1];
     {
       const int col = lane_id() & 15;
@@ -1243,7 +1335,11 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (!s_flast) return;
     const double tot = fz_sum_partials(fz.gpart, ngrp, s_q);
     if (tid < 28) {
+#ifdef FMX_DIAG_NOEPI  // keep the diagnostic build's system solvable
+      host_store(fz.out + tid, tot + (tid == 0 || tid == 7 || tid == 13 || tid == 18 || tid == 22 || tid == 25 ? 1.0 : 0.0));
+#else
       host_store(fz.out + tid, tot);
+#endif
       if (tid == 27) host_store(fz.out + 28, 0.5 * tot);  // error = 0.5 ||r / sigma||^2
     }
     if (tid == 0) {
