@@ -34,6 +34,7 @@ int match_group_for(uint64_t nq, uint32_t K) {
   return nq >= (uint64_t)(FMX_MATCH_LARGE_MIN) && K <= kMatchTileMaxPairs ? 1 : 8;
 }
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w, hipStream_t st) {
+  ++c->warm_gen;  // a new map: no warm start from an earlier match
   g8::run_map_build(c, scans, poses34, w, st);  // the same build in both variants
 }
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
@@ -291,6 +292,7 @@ void set_queries_device(fmx_ctx* c, uint64_t scan, const float* plp, const float
   c->n_sel = npl;
   c->q_scan = scan;
   c->have_queries = true;
+  ++c->warm_gen;  // a new query set: no warm start from an earlier match
   c->have_match = false;
   c->have_qo = false;
 }
@@ -317,6 +319,7 @@ void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const
   c->n_sel = npl;
   c->q_scan = scan;
   c->have_queries = true;
+  ++c->warm_gen;  // a new query set: no warm start from an earlier match
   c->have_match = false;
   c->have_qo = false;
 }
@@ -344,6 +347,7 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
   run_extract(c, d, (int)R, (int)C, out, while_waiting);
   c->q_scan = scan;
   c->have_queries = true;
+  ++c->warm_gen;  // a new query set: no warm start from an earlier match
   c->have_match = false;
   c->have_qo = false;
 }
@@ -412,6 +416,7 @@ bool pf_take(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, uint64_t scan,
   ++c->pf_used;
   c->q_scan = scan;
   c->have_queries = true;
+  ++c->warm_gen;  // a new query set: no warm start from an earlier match
   c->have_match = false;
   c->have_qo = false;
   return true;
@@ -1253,6 +1258,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->blk_lo.release(); c->blk_hi.release(); c->h_work.release();
   c->work.release(); c->pair_base.release();
   c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();
+  c->m_rec.release();
   c->hist.release(); c->hist_off.release(); c->thist.release(); c->c_pl.release(); c->c_pt.release(); c->pair_counts.release();
   c->chunk_range.release(); c->chunks.release(); c->n_chunks.release();
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();

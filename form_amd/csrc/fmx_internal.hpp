@@ -335,6 +335,13 @@ struct fmx_ctx {
   fmx::DBuf<double4> m_pi, m_ni;
   fmx::DBuf<uint8_t> m_ins;
   fmx::DBuf<uint32_t> hist, hist_off;
+  // Warm start: every match writes its NN record per query (m_rec, not part of a
+  // MatchSet: each launch reads and rewrites it in place, in stream order).  A later
+  // match on the same map and query set starts each query's search bounded by that
+  // record's distance at the new pose (any record of the map is a valid bound).
+  fmx::DBuf<uint32_t> m_rec;
+  uint64_t warm_gen = 1;      // bumped by every map build and query-set change
+  uint64_t warm_rec_gen = 0;  // warm_gen when m_rec was last written (0: never)
   fmx::DBuf<uint32_t> thist;  // tiled pair sort: per-(type, pair, tile) counts, self-resetting
   bool have_match = false;
 
@@ -451,9 +458,15 @@ struct MatchDiag {
   double span = 0, p50 = 0, p90 = 0, p99 = 0, pmax = 0, f50 = 0, f90 = 0, f99 = 0, mq_all = 0, mq_slow = 0;
   uint64_t mq_hist[8] = {0};
   double walk_rounds = 0, walk_steps = 0, walk_listed = 0, waves = 0;  // FMX_DIAG_WALK builds
+  double ph50[4] = {0, 0, 0, 0}, ph99[4] = {0, 0, 0, 0};              // FMX_DIAG_PHASE builds
   ~MatchDiag() {
     if (!on || !launches) return;
     const double n = (double)launches;
+#ifdef FMX_DIAG_PHASE
+    fprintf(stderr, "match diag: phase ends after block start (p50 / p99 over blocks, us): query %.1f / %.1f, own cell "
+                    "%.1f / %.1f, faces %.1f / %.1f, edges+corners %.1f / %.1f\n",
+            ph50[0] / n, ph99[0] / n, ph50[1] / n, ph99[1] / n, ph50[2] / n, ph99[2] / n, ph50[3] / n, ph99[3] / n);
+#endif
     if (walk_listed > 0)
       fprintf(stderr, "match diag: ring-1 list walk: %.2f rounds per wave, %.3f steps and %.3f listed cells per query\n",
               walk_rounds / waves, walk_steps / (waves * 64), walk_listed / (waves * 64));
@@ -482,13 +495,25 @@ inline void match_diag_add(const uint32_t* w, uint32_t nb) {
   std::vector<double> dur(nb), fin(nb);
   std::vector<std::pair<double, uint32_t>> by;
   double mq = 0;
+#ifdef FMX_DIAG_PHASE
+  for (int k = 0; k < 4; ++k) {
+    std::vector<double> v(nb);
+    for (uint32_t b = 0; b < nb; ++b) v[b] = ((w[8 * b + 3 + 3 * (k / 2)] >> (16 * (k & 1))) & 0xFFFFu) * 0.01;
+    std::sort(v.begin(), v.end());
+    d.ph50[k] += v[nb / 2];
+    d.ph99[k] += v[std::min<size_t>(nb - 1, (size_t)(0.99 * nb))];
+  }
+#else
+  for (uint32_t b = 0; b < nb; ++b) {
+    d.walk_rounds += w[8 * b + 3];
+    d.walk_steps += w[8 * b + 6];
+    d.walk_listed += w[8 * b + 7];
+  }
+#endif
   for (uint32_t b = 0; b < nb; ++b) {
     dur[b] = (double)(int32_t)(w[8 * b + 5] - w[8 * b + 4]) * 0.01;  // 100 MHz -> us
     fin[b] = (double)(int32_t)(w[8 * b + 5] - t0) * 0.01;
     by.push_back({dur[b], w[8 * b + 2]});
-    d.walk_rounds += w[8 * b + 3];
-    d.walk_steps += w[8 * b + 6];
-    d.walk_listed += w[8 * b + 7];
     d.waves += 4;  // waves per match block (256 threads)
     mq += w[8 * b + 2];
     int h = 0;

@@ -464,6 +464,13 @@ struct MatchArgs {
   int sorted;  // 1: pair histogram for the pair sort; 0: per-pair counts only
   int tiles;   // sorted: 1 = per-(pair, tile) counts scanned by the last block (k_pair_scatter_t)
   uint32_t ntl_pl, ntl_pt;  // tiles (kTileBlocks match blocks each) per type
+  // warm start (fmx_ctx::m_rec): the NN record per query of an earlier match on the same
+  // map and query set (null: cold), this launch's NN records (null: not kept), and the
+  // largest warm distance^2 that may bound the search (a record that close to the query
+  // lies inside the searched cells, so it is a legal candidate)
+  const uint32_t* warm;
+  uint32_t* rec;
+  double warm_lim;
 };
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
@@ -629,7 +636,8 @@ __device__ __forceinline__ int ring1_index(int dx, int dy, int dz) {
 template <int G, bool DENSE>
 __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, const double (&wq)[3], int g,
                                           uint32_t* hd, double& best, uint32_t& best_rid, uint32_t& best_i,
-                                          uint32_t& n_probe, uint32_t& n_cand, uint32_t& n_iter, uint32_t& n_list) {
+                                          uint32_t& n_probe, uint32_t& n_cand, uint32_t& n_iter, uint32_t& n_list,
+                                          double warm_b = INFINITY, uint32_t* phase = nullptr) {
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
   // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
   // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
@@ -895,6 +903,10 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           vlb = lb;
         }
       }
+      // the warm bound joins once the own cell's probe is in flight (the probe does not
+      // wait for the warm record's load): a record at distance^2 warm_b exists, so no
+      // cell, sub-cell or record farther than that can win — the argmin is unchanged
+      if (ip == 0) best = fmin(best, warm_b);
       // small cells (<= kSmallCell records): the lane that probed one folds its
       // records itself, every lane's loads in flight together, one group min after;
       // the argmin on (d^2, tie key) does not depend on the folding order
@@ -924,6 +936,9 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2], srank_s(sl));
       }
     }
+#ifdef FMX_DIAG_PHASE  // wall clock at the end of each pass (own cell, faces, edges + corners)
+    if (phase && ip < 3) phase[ip] = (uint32_t)wall_clock64();
+#endif
   }
   if constexpr (kCompact) {
     if (compact && inr) {
@@ -1176,17 +1191,45 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (planar) m_ni[q] = ni;
     const bool ins = !found || best > a.min_d2;
     m_ins[gq] = ins ? 1 : 0;
+    if (a.rec) a.rec[gq] = best_i;  // the next match's warm start
     if (ins) atomicAdd(&s_ins, 1u);
     if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
   };
   double best = a.bound;
   uint32_t best_i = 0xFFFFFFFFu;
+#ifdef FMX_DIAG_PHASE
+  uint32_t phase[4] = {t_begin, t_begin, t_begin, t_begin};  // query loaded, passes 0..2 done
+#else
+  uint32_t* phase = nullptr;
+#endif
   if (qi < nq) {
     double wq[3];
     world_query(qi, wq);
+#ifdef FMX_DIAG_PHASE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    phase[0] = (uint32_t)wall_clock64();
+#endif
     uint32_t best_rid = 0xFFFFFFFFu;
+    // warm start: the earlier match's NN record of this query, at the new pose (the same
+    // (dx^2 + dz^2) + dy^2 as fold); it bounds the search, it is not taken as the result
+    double warm_b = INFINITY;
+    if (a.warm) {
+      const uint32_t r = a.warm[planar ? qi : a.nq_pl + qi];
+      if (r != 0xFFFFFFFFu) {
+        const double4 p = M.pos[r];
+        const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
+        const double d2 = (dx * dx + dz * dz) + dy * dy;
+        if (d2 <= a.warm_lim) warm_b = d2;
+      }
+    }
     nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, n_probe,
-                             n_cand, n_iter, n_list);
+                             n_cand, n_iter, n_list, warm_b,
+#ifdef FMX_DIAG_PHASE
+                             phase + 1
+#else
+                             phase
+#endif
+    );
   }
   // work counters for the algorithmic-byte model and the match diagnostics (one plain
   // store per block, summed on the host): probes, candidate records, the largest
@@ -1203,6 +1246,13 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     s_work[1][threadIdx.x / kWave] = wc;
     s_work[2][threadIdx.x / kWave] = qc;
   }
+#ifdef FMX_DIAG_PHASE  // per block: the latest wave's end of each phase (ticks after the block's start)
+  __shared__ uint32_t s_ph[4];
+  if (threadIdx.x < 4) s_ph[threadIdx.x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) atomicMax(&s_ph[k], phase[k] - t_begin);
+#endif
 #ifdef FMX_DIAG_WALK  // per block: sum over waves of the wave's walk rounds, lanes' walk steps, listed cells
   __shared__ uint32_t s_walk[3][kMatchThreads / kWave];
   {
@@ -1233,6 +1283,10 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
       d1 += s_walk[1][i];
       d2 += s_walk[2][i];
     }
+#endif
+#ifdef FMX_DIAG_PHASE
+    d0 = min(s_ph[0], 0xFFFFu) | min(s_ph[1], 0xFFFFu) << 16;
+    d1 = min(s_ph[2], 0xFFFFu) | min(s_ph[3], 0xFFFFu) << 16;
 #endif
     w4[0] = make_uint4(tp, tc, mq, d0);
     w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), d1, d2);
@@ -1843,6 +1897,12 @@ void run_pair_scatter(fmx_ctx* c) {
   FMX_HIP(hipGetLastError());
 }
 
+// FMX_NO_WARM: every match cold (A/B switch; results are identical either way)
+static bool no_warm() {
+  static const bool v = std::getenv("FMX_NO_WARM") != nullptr;
+  return v;
+}
+
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
   hipStream_t st = c->match_stream ? c->match_stream : c->stream;
@@ -1859,6 +1919,17 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   if (obs > reach * reach && c->cell_m > 1)
     throw StatusError(FMX_E_INVAL, "max_dist / min_dist_map exceed the voxel width of a subdivided map");
   a.bound = obs <= reach * reach ? obs : INFINITY;
+  // warm start from the last match on this map and query set (m_rec, stream order); an
+  // unbounded search (a.bound = inf) takes a warm record only well inside the reach
+  a.warm_lim = std::isfinite(a.bound) ? a.bound : 0.99 * reach * reach;
+  {
+    const uint32_t* before = c->m_rec.p;
+    c->m_rec.ensure((size_t)c->n_qpl + c->n_qpt + 1);
+    const bool warm = c->warm_rec_gen == c->warm_gen && c->m_rec.p == before && !no_warm();
+    a.warm = warm ? c->m_rec.p : nullptr;
+    a.rec = c->m_rec.p;
+    c->warm_rec_gen = c->warm_gen;
+  }
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
@@ -1986,6 +2057,9 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
     throw StatusError(FMX_E_INVAL, "max_dist exceeds the voxel width of a subdivided map");
   // only acceptance is observable here: the search is bounded by max_dist alone
   a.bound = a.max_d2 <= reach * reach ? a.max_d2 : INFINITY;
+  a.warm = nullptr;  // (no per-query results: no warm start kept)
+  a.rec = nullptr;
+  a.warm_lim = 0.0;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
