@@ -447,6 +447,15 @@ __device__ __constant__ int c_shift[125][3] = {
     {-2, 2, -2}, {-2, 2, 2}, {2, -2, -2}, {2, -2, 2}, {2, 2, -2}, {2, 2, 2},
 };
 
+// Component ax of shift s.  Ring 1 (s < 27) is decoded from bit masks (bit s of kShP[ax]
+// set: +1, of kShN[ax]: -1) — pure ALU: a lane-indexed c_shift load is a dependent
+// memory round of its own in every probe step; ring 2 reads the table.
+constexpr uint32_t kShP[3] = {0x781982u, 0x1998288u, 0x2aaa820u}, kShN[3] = {0x7806604u, 0x6660510u, 0x5555040u};
+__device__ __forceinline__ int shift_c(int s, int ax) {
+  if (s < 27) return (int)((kShP[ax] >> s) & 1u) - (int)((kShN[ax] >> s) & 1u);
+  return c_shift[s][ax];
+}
+
 // rank of each reference voxel shift (dx, dy, dz) in {-1, 0, 1}^3 in the reference's
 // order (map.tpp:54-68), indexed (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)
 __device__ __constant__ uint8_t c_refrank[27] = {
@@ -608,6 +617,9 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_COMPACT_SHIFTS
 #define FMX_COMPACT_SHIFTS 1  // one-lane-per-query ring-1 search from a per-lane work list (A/B switch)
 #endif
+#ifndef FMX_RING_LIST
+#define FMX_RING_LIST 1  // neighbour shifts admitted once and probed G per round (A/B switch)
+#endif
 #ifndef FMX_PROBE_TOGETHER
 #define FMX_PROBE_TOGETHER 1  // brick key and cell range in flight together (A/B switch)
 #endif
@@ -651,7 +663,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
   // the tie rank of shift s: on an unsubdivided map the shift IS the reference voxel
   // shift, whose rank is its index (c_shift[0..26] = voxel_shifts, map.tpp:54-68)
   auto srank_s = [&](int s) -> uint32_t {
-    return sh == 0 && s < 27 ? (uint32_t)s << 27 : srank(c_shift[s][0], c_shift[s][1], c_shift[s][2]);
+    return sh == 0 && s < 27 ? (uint32_t)s << 27 : srank(shift_c(s, 0), shift_c(s, 1), shift_c(s, 2));
   };
   // one bucket read per probe: key, the cell's two boundaries and its dense bit in
   // flight together; a bucket of another build epoch ends the chain (empty)
@@ -864,7 +876,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     for (int ax = 0; ax < 3; ++ax) {
       // distance from the query to its cell's face on the side of the shift (recomputed
       // here rather than kept live: registers)
-      const int sa = c_shift[s][ax];
+      const int sa = shift_c(s, ax);
       const int ba = ax == 0 ? bx : (ax == 1 ? by : bz);
       const double hi = (ba + 1) * a.w - wq[ax], lo = wq[ax] - ba * a.w;
       const double e = sa > 0 ? hi + (sa - 1) * a.w : (sa < 0 ? lo + (-sa - 1) * a.w : 0.0);
@@ -888,58 +900,112 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
   // probe + record rounds as its busiest query, not as the union of its queries' cells.
   constexpr bool kCompact = G == 1 && !DENSE && FMX_COMPACT_SHIFTS;
   const bool compact = kCompact && a.rings == 1;
+  // One step of the search: lane g bounds and probes shift s (s < 0: none); the cells
+  // of at most kSmallCell records are folded by their probing lane, the larger ones
+  // walked by the whole group, each bound re-checked against the shared best.
+  auto visit = [&](int s, bool own) {
+    uint32_t vf = 0, vc = 0;
+    bool vd = false;
+    double vlb = INFINITY;
+    if (inr && s >= 0) {
+      const double lb = shift_lb(s);
+      if (lb <= best) {  // else conservative: no point inside can win
+        probe(shift_c(s, 0), shift_c(s, 1), shift_c(s, 2), vf, vc, vd);
+        vlb = lb;
+      }
+    }
+    // the warm bound joins once the own cell's probe is in flight (the probe does not
+    // wait for the warm record's load): a record at distance^2 warm_b exists, so no
+    // cell, sub-cell or record farther than that can win — the argmin is unchanged
+    if (own) best = fmin(best, warm_b);
+    // small cells (<= kSmallCell records): the lane that probed one folds its
+    // records itself, every lane's loads in flight together, one group min after;
+    // the argmin on (d^2, tie key) does not depend on the folding order
+    const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
+    if (small) {
+      const uint32_t rk = srank_s(s);
+      double4 pr[kSmallCell];
+#pragma unroll
+      for (int u = 0; u < kSmallCell; ++u)
+        if (u < (int)vc) pr[u] = M.pos[vf + u];
+#pragma unroll
+      for (int u = 0; u < kSmallCell; ++u)
+        if (u < (int)vc) fold(pr[u], vf + u, rk);
+      n_cand += vc;
+    }
+    if (group_bits<G>(__ballot(small))) group_min();
+    uint64_t live = group_bits<G>(__ballot(vc > (uint32_t)kSmallCell));  // larger cells: walked by the group
+    while (live) {
+      const int l = __ffsll((unsigned long long)live) - 1;
+      live &= live - 1;
+      const double lb = __shfl(vlb, l, G);
+      if (lb > best) continue;  // best is group-uniform here
+      const uint32_t cnt = __shfl(vc, l, G);
+      const uint32_t first = __shfl(vf, l, G);
+      const bool dn = __shfl((int)vd, l, G) != 0;
+      const int sl = __shfl(s, l, G);
+      scan_cell(first, cnt, dn, bx + shift_c(sl, 0), by + shift_c(sl, 1), bz + shift_c(sl, 2), srank_s(sl));
+    }
+  };
+#if FMX_RING_LIST
+  // The query's own cell first (shift 0, visited first by the reference too), then
+  // every other shift whose lower bound admits it against the best so far — ring 1
+  // (and ring 2 on a map of half-width cells), listed once per group as a bit mask and
+  // taken G at a time in shift order (nearer rings first), each re-bounded when taken.
+  // A group's admitted cells are thus probed G per dependent round instead of one pass
+  // per ring class (faces, then edges + corners, then ring 2), each a round of its own.
+  visit(g == 0 ? 0 : -1, true);
+#ifdef FMX_DIAG_PHASE
+  if (phase) phase[0] = (uint32_t)wall_clock64();
+#endif
+  if (!compact) {
+    const int nsh = a.rings >= 2 ? 124 : 26;
+    uint64_t m0 = 0, m1 = 0;  // admitted shifts: bit s - 1
+    for (int u = 0; u * G < nsh; ++u) {
+      const int s = 1 + u * G + g;
+      const bool ad = inr && s <= nsh && shift_lb(s) <= best;
+      const uint64_t b = group_bits<G>(__ballot(ad));
+      const int bit = u * G;
+      if (bit < 64) m0 |= b << bit;
+      else m1 |= b << (bit - 64);
+    }
+#ifdef FMX_DIAG_PHASE
+    if (phase) phase[1] = (uint32_t)wall_clock64();
+#endif
+    while (m0 | m1) {
+      int mine = -1;  // this lane's shift of the round: the g-th admitted one left
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        if (!(m0 | m1)) break;
+        int bit;
+        if (m0) {
+          bit = __ffsll((unsigned long long)m0) - 1;
+          m0 &= m0 - 1;
+        } else {
+          bit = 64 + __ffsll((unsigned long long)m1) - 1;
+          m1 &= m1 - 1;
+        }
+        if (k == g) mine = bit + 1;
+      }
+      visit(mine, false);
+    }
+  }
+#ifdef FMX_DIAG_PHASE
+  if (phase) phase[2] = (uint32_t)wall_clock64();
+#endif
+#else
+  // The cells in passes of increasing lower bound — the query's own cell (shift 0,
+  // visited first by the reference too), ring-1 faces (shifts 1..6), ring-1 edges +
+  // corners (7..26), then ring 2 (27..124) when the map uses half-width cells — each
+  // pass pruned against the best found so far; in a pass a lane bounds and probes its
+  // shifts in parallel (visit).
   for (int ip = 0; ip < (compact ? 1 : npass); ++ip) {
     const int s_begin = ip == 0 ? 0 : (ip == 1 ? 1 : (ip == 2 ? 7 : 27));
     const int s_end = ip == 0 ? 1 : (ip == 1 ? 7 : (ip == 2 ? 27 : 125));
-    for (int s0 = s_begin; s0 < s_end; s0 += G) {  // one shift per lane per chunk
-      uint32_t vf = 0, vc = 0;
-      bool vd = false;
-      double vlb = INFINITY;
-      const int s = s0 + g;
-      if (inr && s < s_end) {
-        const double lb = shift_lb(s);
-        if (lb <= best) {  // else conservative: no point inside can win
-          probe(c_shift[s][0], c_shift[s][1], c_shift[s][2], vf, vc, vd);
-          vlb = lb;
-        }
-      }
-      // the warm bound joins once the own cell's probe is in flight (the probe does not
-      // wait for the warm record's load): a record at distance^2 warm_b exists, so no
-      // cell, sub-cell or record farther than that can win — the argmin is unchanged
-      if (ip == 0) best = fmin(best, warm_b);
-      // small cells (<= kSmallCell records): the lane that probed one folds its
-      // records itself, every lane's loads in flight together, one group min after;
-      // the argmin on (d^2, tie key) does not depend on the folding order
-      const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
-      if (small) {
-        const uint32_t rk = srank_s(s);
-        double4 pr[kSmallCell];
-#pragma unroll
-        for (int u = 0; u < kSmallCell; ++u)
-          if (u < (int)vc) pr[u] = M.pos[vf + u];
-#pragma unroll
-        for (int u = 0; u < kSmallCell; ++u)
-          if (u < (int)vc) fold(pr[u], vf + u, rk);
-        n_cand += vc;
-      }
-      if (group_bits<G>(__ballot(small))) group_min();
-      uint64_t live = group_bits<G>(__ballot(vc > (uint32_t)kSmallCell));  // larger cells: walked by the group
-      while (live) {
-        const int l = __ffsll((unsigned long long)live) - 1;
-        live &= live - 1;
-        const double lb = __shfl(vlb, l, G);
-        if (lb > best) continue;  // best is group-uniform here
-        const uint32_t cnt = __shfl(vc, l, G);
-        const uint32_t first = __shfl(vf, l, G);
-        const bool dn = __shfl((int)vd, l, G) != 0;
-        const int sl = s0 + l;
-        scan_cell(first, cnt, dn, bx + c_shift[sl][0], by + c_shift[sl][1], bz + c_shift[sl][2], srank_s(sl));
-      }
-    }
-#ifdef FMX_DIAG_PHASE  // wall clock at the end of each pass (own cell, faces, edges + corners)
-    if (phase && ip < 3) phase[ip] = (uint32_t)wall_clock64();
-#endif
+    for (int s0 = s_begin; s0 < s_end; s0 += G)  // one shift per lane per chunk
+      visit(s0 + g < s_end ? s0 + g : -1, ip == 0);
   }
+#endif
   if constexpr (kCompact) {
     if (compact && inr) {
       // Per axis: the query's squared distance (1e-9 slack, as shift_lb) to its cell's
