@@ -617,8 +617,14 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_COMPACT_SHIFTS
 #define FMX_COMPACT_SHIFTS 1  // one-lane-per-query ring-1 search from a per-lane work list (A/B switch)
 #endif
-#ifndef FMX_RING_LIST
-#define FMX_RING_LIST 1  // neighbour shifts admitted once and probed G per round (A/B switch)
+#ifndef FMX_WARM_START
+#define FMX_WARM_START 1  // bound each search by the previous match's record (compile-time A/B switch)
+#endif
+#ifndef FMX_RING_LIST  // neighbour shifts admitted once and probed G per round (A/B switch): the
+// 8-lane build (C4: same time as the ring-class passes); the one-lane build keeps the
+// passes (its plain variant walks per-lane lists instead, and the list code costs it
+// 8 spilled VGPRs)
+#define FMX_RING_LIST (FMX_MATCH_GROUP != 1)
 #endif
 #ifndef FMX_PROBE_TOGETHER
 #define FMX_PROBE_TOGETHER 1  // brick key and cell range in flight together (A/B switch)
@@ -1279,7 +1285,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     // warm start: the earlier match's NN record of this query, at the new pose (the same
     // (dx^2 + dz^2) + dy^2 as fold); it bounds the search, it is not taken as the result
     double warm_b = INFINITY;
-    if (a.warm) {
+    if (FMX_WARM_START && a.warm) {
       const uint32_t r = a.warm[planar ? qi : a.nq_pl + qi];
       if (r != 0xFFFFFFFFu) {
         const double4 p = M.pos[r];
@@ -2123,7 +2129,10 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
     throw StatusError(FMX_E_INVAL, "max_dist exceeds the voxel width of a subdivided map");
   // only acceptance is observable here: the search is bounded by max_dist alone
   a.bound = a.max_d2 <= reach * reach ? a.max_d2 : INFINITY;
-  a.warm = nullptr;  // (no per-query results: no warm start kept)
+  // no warm start here: measured (profiles/r3_ab_c5_warm_*.txt) the C5 searches barely
+  // prune further (probes per query 1.724 either way), and keeping 4 B per query cost
+  // the HBM-bound whole-map set 2-3 % (0.75 -> 0.77 ms per registration)
+  a.warm = nullptr;
   a.rec = nullptr;
   a.warm_lim = 0.0;
   a.nq_pl = c->n_qpl;
