@@ -322,11 +322,14 @@ __global__ __launch_bounds__(kAllocThreads) void k_map_alloc(BuildArgs a) {
   }
 }
 
-// .w of a record: build order (k_match tie-break) in the low 32 bits, the segment above
-// them (exact in a double: < 2^53), so the match epilogue needs no seg[] lookup
+// .w of a record: the BITS of a u64 (never a value: only loaded, stored and moved) —
+// build order (k_match tie-break) in the low 32, the segment above them, so the match
+// epilogue needs no seg[] lookup and a candidate's tie key costs no f64 -> u64
+// conversion (~8 VALU per candidate when .w held the value)
 __device__ __forceinline__ double rec_tag(uint32_t rec, uint32_t seg) {
-  return (double)rec + 4294967296.0 * (double)seg;
+  return __longlong_as_double((long long)((unsigned long long)seg << 32 | rec));
 }
+__device__ __forceinline__ unsigned long long tag_bits(double w) { return (unsigned long long)__double_as_longlong(w); }
 
 __global__ __launch_bounds__(256) void k_map_scatter(BuildArgs a) {
   const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
@@ -617,6 +620,9 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_COMPACT_SHIFTS
 #define FMX_COMPACT_SHIFTS 1  // one-lane-per-query ring-1 search from a per-lane work list (A/B switch)
 #endif
+#ifndef FMX_F32_BOUNDS
+#define FMX_F32_BOUNDS 1  // cell lower bounds in fp32 from the query's in-cell offset (A/B switch)
+#endif
 #ifndef FMX_WARM_START
 #define FMX_WARM_START 1  // bound each search by the previous match's record (compile-time A/B switch)
 #endif
@@ -705,12 +711,12 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     const unsigned long long key = brick_key(X, Y, Z, M.epoch);
     walk(key, brick_cell(X, Y, Z), mix64(key) & M.mask, first, count, dense);
   };
-  // a record is one double4: world position + its build order in .w (exact in a
-  // double), so a candidate test is one 32-B load
+  // a record is one double4: world position + its build order in .w (rec_tag), so a
+  // candidate test is one 32-B load
   auto fold = [&](const double4& p, uint32_t i, uint32_t rk) {
     const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
     const double d2 = (dx * dx + dz * dz) + dy * dy;
-    const uint32_t tk = rk | ((uint32_t)(unsigned long long)p.w & 0x07FFFFFFu);  // build order: low bits
+    const uint32_t tk = rk | ((uint32_t)tag_bits(p.w) & 0x07FFFFFFu);  // build order: low bits
     if (d2 <= best && (d2 < best || tk < best_rid)) {
       best = d2;
       best_rid = tk;
@@ -759,8 +765,27 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
   // query's own sub-cell first, then every other sub-cell whose box lower bound does
   // not exceed the best so far, each group-walked (lane g holds sub-cells g, g + G, ...
   // for the bounds; the header copy in LDS `hd` is shared by the group).
-  const double sw = a.w / kSubPerAxis;
-  auto scan_cell = [&](uint32_t first, uint32_t count, bool dense, int X, int Y, int Z, uint32_t rk) {
+  // Lower bounds (cell and sub-cell pruning) in fp32 from the query's offset inside its
+  // own cell, qo (the double subtraction wq - b * w, then one rounding): every bound is
+  // a distance to a plane of the cell grid, shortened by a slack of 1e-6 w — well over
+  // the fp32 error of qo and of the bound's few operations (< 1e-6 relative of w) — so a
+  // bound never exceeds the true distance^2 and pruning never drops the winner.  fp64
+  // bounds cost ~3x the VALU issue slots of these (C4 k_match is ~60 % VALU-busy per
+  // SIMD at 4 waves).
+  const float wf = (float)a.w, swf = wf * (1.0f / kSubPerAxis), slk = 1e-6f * wf;
+  float qo[3] = {0.0f, 0.0f, 0.0f};
+  if (FMX_F32_BOUNDS || DENSE) {
+    qo[0] = (float)(wq[0] - bx * a.w);
+    qo[1] = (float)(wq[1] - by * a.w);
+    qo[2] = (float)(wq[2] - bz * a.w);
+  }
+  // Records of one cell, walked by the whole group (group-uniform arguments).  A
+  // dense cell (k_map_dense) starts with a header of its 64 sub-cell ends: the
+  // query's own sub-cell first, then every other sub-cell whose box lower bound does
+  // not exceed the best so far, each group-walked (lane g holds sub-cells g, g + G, ...
+  // for the bounds; the header copy in LDS `hd` is shared by the group).  sx, sy, sz:
+  // the cell's shift from the query's cell.
+  auto scan_cell = [&](uint32_t first, uint32_t count, bool dense, int sx, int sy, int sz, uint32_t rk) {
     if constexpr (!DENSE) {  // no dense cell in the map: the cell's records, split over the lanes
       constexpr int D = FMX_MATCH_DEPTH_PLAIN;
       const uint32_t end = first + count;
@@ -780,25 +805,27 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     constexpr int kPer = kSubCells / G;  // sub-cells per lane
     const uint32_t* hdr = reinterpret_cast<const uint32_t*>(M.pos + first);
     const uint32_t base = dense ? first + kHdr : first;
-    const bool sorted = DENSE && dense && hdr[0] != kUnsorted;
-    // per sub-cell lower bound (1e-9 slack over the fp rounding of the sub-cell index)
-    auto axis_lb = [&](double q, int C, int i) {
-      const double lo = C * a.w + i * sw, hi = lo + sw;
-      const double d = q < lo ? lo - q : (q > hi ? q - hi : 0.0);
-      const double m = fmax(d - 1e-9, 0.0);
+    // the query's offset from this cell's origin, per axis
+    const float ox = qo[0] - sx * wf, oy = qo[1] - sy * wf, oz = qo[2] - sz * wf;
+    // per sub-cell lower bound: distance^2 to the sub-cell's box (fp32, slack as above)
+    auto axis_lb = [&](float q, int i) {
+      const float lo = i * swf, hi = lo + swf;
+      const float d = fmaxf(fmaxf(lo - q, q - hi), 0.0f);
+      const float m = fmaxf(d - slk, 0.0f);
       return m * m;
     };
     auto sub_lb = [&](int sub) {
-      return axis_lb(wq[0], X, sub % kSubPerAxis) + axis_lb(wq[1], Y, (sub / kSubPerAxis) % kSubPerAxis) +
-             axis_lb(wq[2], Z, sub / (kSubPerAxis * kSubPerAxis));
+      return (double)(axis_lb(ox, sub % kSubPerAxis) + axis_lb(oy, (sub / kSubPerAxis) % kSubPerAxis) +
+                      axis_lb(oz, sub / (kSubPerAxis * kSubPerAxis)));
     };
     auto sub_beg = [&](int sub) { return sub == 0 ? 0u : hd[sub - 1]; };
-    // A sorted dense cell's sub-cell ranges in hd[] (LDS; coalesced copy: lane g
-    // copies entries [g * kPer, (g + 1) * kPer)); any other cell is one range.  The
-    // s_waitcnt + memory clobbers order the copy after the previous cell's reads and
-    // before the other lanes' reads.
-    if (sorted) {
-      if (g == 0) n_probe += kHdr * 32 / 64;  // the header's 64-B lines (byte model)
+    // A dense cell's header in hd[] (LDS; coalesced copy: lane g copies entries
+    // [g * kPer, (g + 1) * kPer)), read in the same round as its sorted marker (entry 0):
+    // a sorted cell's sub-cell ranges; any other cell is one range.  The s_waitcnt +
+    // memory clobbers order the copy after the previous cell's reads and before the
+    // other lanes' reads.
+    bool sorted = false;
+    if (DENSE && dense) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if constexpr (kPer >= 4) {
 #pragma unroll
@@ -809,9 +836,15 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         for (int u = 0; u < kPer; ++u) hd[g * kPer + u] = hdr[g * kPer + u];
       }
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      sorted = hd[0] != kUnsorted;
+      if (sorted && g == 0) n_probe += kHdr * 32 / 64;  // the header's 64-B lines (byte model)
     }
-    const int qs = sub_axis(wq[0], X * a.w, sw) + kSubPerAxis * sub_axis(wq[1], Y * a.w, sw) +
-                   kSubPerAxis * kSubPerAxis * sub_axis(wq[2], Z * a.w, sw);
+    // the query's (nearest) sub-cell: only the visiting order depends on it
+    auto sub_of = [&](float q) {
+      const int i = (int)floorf(q * (kSubPerAxis / wf));
+      return i < 0 ? 0 : (i > kSubPerAxis - 1 ? kSubPerAxis - 1 : i);
+    };
+    const int qs = sub_of(ox) + kSubPerAxis * sub_of(oy) + kSubPerAxis * kSubPerAxis * sub_of(oz);
     // Walk 0: the whole cell, or (sorted) the query's own / nearest sub-cell.  Walk 1
     // (sorted only): every other sub-cell whose box can still hold a closer record.
     // A walk is ONE virtual range — the chosen ranges' records concatenated in
@@ -875,13 +908,12 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     }
   };
   const bool inr = key_in_range(bx, by, bz);
-  // lower bound on d^2 from the query to any point of the cell at shift s
+#if !FMX_F32_BOUNDS
+  // lower bound on d^2 from the query to any point of the cell at shift s (fp64)
   auto shift_lb = [&](int s) {
     double lb = 0.0;
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
-      // distance from the query to its cell's face on the side of the shift (recomputed
-      // here rather than kept live: registers)
       const int sa = shift_c(s, ax);
       const int ba = ax == 0 ? bx : (ax == 1 ? by : bz);
       const double hi = (ba + 1) * a.w - wq[ax], lo = wq[ax] - ba * a.w;
@@ -891,6 +923,22 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     }
     return lb;
   };
+#else
+  // lower bound on d^2 from the query to any point of the cell at shift s (fp32 from
+  // qo, slack as above)
+  auto shift_lb = [&](int s) {
+    float lb = 0.0f;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      const int sa = shift_c(s, ax);
+      const float lo = qo[ax], hi = wf - qo[ax];
+      const float e = sa > 0 ? hi + (sa - 1) * wf : (sa < 0 ? lo + (-sa - 1) * wf : 0.0f);
+      const float m = fmaxf(e - slk, 0.0f);
+      lb += m * m;
+    }
+    return (double)lb;
+  };
+#endif
   // The cells in passes of increasing lower bound — the query's own cell (shift 0,
   // visited first by the reference too), ring-1 faces (shifts 1..6), ring-1 edges +
   // corners (7..26), then ring 2 (27..124) when the map uses half-width cells — each
@@ -950,7 +998,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       const uint32_t first = __shfl(vf, l, G);
       const bool dn = __shfl((int)vd, l, G) != 0;
       const int sl = __shfl(s, l, G);
-      scan_cell(first, cnt, dn, bx + shift_c(sl, 0), by + shift_c(sl, 1), bz + shift_c(sl, 2), srank_s(sl));
+      scan_cell(first, cnt, dn, shift_c(sl, 0), shift_c(sl, 1), shift_c(sl, 2), srank_s(sl));
     }
   };
 #if FMX_RING_LIST
@@ -1014,14 +1062,14 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
 #endif
   if constexpr (kCompact) {
     if (compact && inr) {
-      // Per axis: the query's squared distance (1e-9 slack, as shift_lb) to its cell's
+      // Per axis: the query's squared distance (1e-9 slack) to its cell's
       // near and far face, rounded down to fp32, and the near side's sign; the axes
       // sorted by near distance.  The 26 ring-1 cells are listed RELATIVE to that
       // frame, nearest first (kRel*: the near faces, edges and corner of the query's
       // octant, then every cell with a far side, whose bound is at least the smallest
       // far term >= (w/2)^2).  A shift's bound is the sum of its axes' terms; the test
       // against best allows for the fp32 sum's rounding (threshold rounded up,
-      // x (1 + 2^-20)), so a cell is skipped only when shift_lb would skip it: the
+      // x (1 + 2^-20)), so a cell is skipped only when its true bound exceeds the best: the
       // winner is unchanged (the argmin on (d^2, tie) does not depend on visit order).
       // nr / fr: near / far terms in sorted order; cd: per sorted slot i, bits 3i..3i+1
       // the grid axis and bit 3i+2 set when the near face is the low one
@@ -1113,7 +1161,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
             if (u < (int)vc) fold(pr[u], vf + u, rk);
           n_cand += vc;
         } else {
-          scan_cell(vf, vc, false, bx + dx, by + dy, bz + dz, rk);
+          scan_cell(vf, vc, false, dx, dy, dz, rk);
         }
       }
     }
@@ -1245,7 +1293,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (found) {
       const double4 p = M.pos[best_i];
       const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);  // in flight with p
-      const uint32_t sg = (uint32_t)((unsigned long long)p.w >> 32);     // the record's segment
+      const uint32_t sg = (uint32_t)(tag_bits(p.w) >> 32);     // the record's segment
       const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
       double o[3];
       d_xform(Ti, p.x, p.y, p.z, o);
@@ -1375,7 +1423,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (acc_q) {
       const double4 p = M.pos[best_i];
       const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);
-      const uint32_t sg = (uint32_t)((unsigned long long)p.w >> 32);
+      const uint32_t sg = (uint32_t)(tag_bits(p.w) >> 32);
       const double* Tinv = inv_poses + 12 * sg;  // matcher.hpp:95
       d_xform(Tinv, p.x, p.y, p.z, pi);
       if (planar) d_rot(Tinv, n.x, n.y, n.z, ni);
