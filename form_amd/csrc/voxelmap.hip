@@ -660,6 +660,7 @@ __device__ __forceinline__ int ring1_index(int dx, int dy, int dz) {
 template <int G, bool DENSE>
 __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, const double (&wq)[3], int g,
                                           uint32_t* hd, double& best, uint32_t& best_rid, uint32_t& best_i,
+                                          uint32_t& best_sg,
                                           uint32_t& n_probe, uint32_t& n_cand, uint32_t& n_iter, uint32_t& n_list,
                                           double warm_b = INFINITY, uint32_t* phase = nullptr) {
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
@@ -716,49 +717,73 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
   auto fold = [&](const double4& p, uint32_t i, uint32_t rk) {
     const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
     const double d2 = (dx * dx + dz * dz) + dy * dy;
-    const uint32_t tk = rk | ((uint32_t)tag_bits(p.w) & 0x07FFFFFFu);  // build order: low bits
+    const unsigned long long t = tag_bits(p.w);
+    const uint32_t tk = rk | ((uint32_t)t & 0x07FFFFFFu);  // build order: low bits
     if (d2 <= best && (d2 < best || tk < best_rid)) {
       best = d2;
       best_rid = tk;
       best_i = i;
+      best_sg = (uint32_t)(t >> 32);  // the record's segment, for the epilogue's pose loads
     }
   };
-  // argmin over (d^2, tie key) across the group's lanes: DPP moves (VALU latency, no LDS
-  // crossbar) inside a row — [row_mirror l <-> 15-l,] row_half_mirror l <-> 7-l, quad
-  // xor 2, quad xor 1 — after ds_bpermute exchanges across rows for a whole wave
-  auto take = [&](double ob, uint32_t orid, uint32_t oi) {
-    if (oi != 0xFFFFFFFFu && (best_i == 0xFFFFFFFFu || ob < best || (ob == best && orid < best_rid))) {
-      best = ob;
-      best_rid = orid;
-      best_i = oi;
-    }
-  };
+  // The same argmin in three reductions instead of one over (d^2, tie, index) moves:
+  // min d^2 (fp64 min), then the least tie key among the lanes holding that d^2, then
+  // the index among the lanes holding both (every such lane holds the same record: a
+  // record's (d^2, tie key) is unique; its segment rides along).  A lane without a
+  // candidate holds the bound it
+  // started from and tie / index ~0, so it never displaces one (~26 VALU per call
+  // instead of ~42: C4 k_match is VALU-limited).
   auto group_min = [&]() {
-    auto step = [&](auto ctrl_tag) {
-      constexpr int CTRL = decltype(ctrl_tag)::value;
-      const long long bb = __double_as_longlong(best);
-      const int blo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)bb, CTRL, 0xF, 0xF, false);
-      const int bhi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(bb >> 32), CTRL, 0xF, 0xF, false);
-      const double ob = __longlong_as_double((long long)(((unsigned long long)(uint32_t)bhi << 32) | (uint32_t)blo));
-      const uint32_t orid = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_rid, CTRL, 0xF, 0xF, false);
-      const uint32_t oi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best_i, CTRL, 0xF, 0xF, false);
-      take(ob, orid, oi);
-    };
-    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 64,
-                  "group reduction assumes 1-, 2-, 4-, 8-, 16- or 64-lane groups");
-    if constexpr (G == 64) {
-#pragma unroll
-      for (int o = 32; o >= 16; o >>= 1) {
-        const double ob = __shfl_xor(best, o, 64);
-        const uint32_t orid = (uint32_t)__shfl_xor((int)best_rid, o, 64);
-        const uint32_t oi = (uint32_t)__shfl_xor((int)best_i, o, 64);
-        take(ob, orid, oi);
-      }
+    if constexpr (G == 1) return;
+    else if constexpr (G > 16) {
+      double m = best;
+      for (int o = 1; o < G; o <<= 1) m = fmin(m, __shfl_xor(m, o, G));
+      uint32_t r = best == m ? best_rid : 0xFFFFFFFFu;
+      for (int o = 1; o < G; o <<= 1) r = min(r, (uint32_t)__shfl_xor((int)r, o, G));
+      const bool win = best == m && best_rid == r;
+      uint32_t i = win ? best_i : 0xFFFFFFFFu, sg = win ? best_sg : 0xFFFFFFFFu;
+      for (int o = 1; o < G; o <<= 1) i = min(i, (uint32_t)__shfl_xor((int)i, o, G));
+      for (int o = 1; o < G; o <<= 1) sg = min(sg, (uint32_t)__shfl_xor((int)sg, o, G));
+      best = m;
+      best_rid = r;
+      best_i = i;
+      best_sg = sg;
+    } else {
+      auto dmin = [&](auto ctrl_tag) {
+        constexpr int CTRL = decltype(ctrl_tag)::value;
+        const long long bb = __double_as_longlong(best);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)bb, CTRL, 0xF, 0xF, false);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(bb >> 32), CTRL, 0xF, 0xF, false);
+        best = fmin(best, __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo)));
+      };
+      auto umin = [&](uint32_t& v, auto ctrl_tag) {
+        constexpr int CTRL = decltype(ctrl_tag)::value;
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false));
+      };
+      const double mine = best;
+      if constexpr (G >= 16) dmin(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
+      if constexpr (G >= 8) dmin(std::integral_constant<int, 0x141>{});   // row_half_mirror
+      if constexpr (G >= 4) dmin(std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]
+      if constexpr (G >= 2) dmin(std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]
+      uint32_t r = mine == best ? best_rid : 0xFFFFFFFFu;
+      if constexpr (G >= 16) umin(r, std::integral_constant<int, 0x140>{});
+      if constexpr (G >= 8) umin(r, std::integral_constant<int, 0x141>{});
+      if constexpr (G >= 4) umin(r, std::integral_constant<int, 0x4E>{});
+      if constexpr (G >= 2) umin(r, std::integral_constant<int, 0xB1>{});
+      const bool win = mine == best && best_rid == r;
+      uint32_t i = win ? best_i : 0xFFFFFFFFu, sg = win ? best_sg : 0xFFFFFFFFu;
+      if constexpr (G >= 16) umin(i, std::integral_constant<int, 0x140>{});
+      if constexpr (G >= 8) umin(i, std::integral_constant<int, 0x141>{});
+      if constexpr (G >= 4) umin(i, std::integral_constant<int, 0x4E>{});
+      if constexpr (G >= 2) umin(i, std::integral_constant<int, 0xB1>{});
+      if constexpr (G >= 16) umin(sg, std::integral_constant<int, 0x140>{});
+      if constexpr (G >= 8) umin(sg, std::integral_constant<int, 0x141>{});
+      if constexpr (G >= 4) umin(sg, std::integral_constant<int, 0x4E>{});
+      if constexpr (G >= 2) umin(sg, std::integral_constant<int, 0xB1>{});
+      best_rid = r;
+      best_i = i;
+      best_sg = sg;
     }
-    if constexpr (G >= 16) step(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
-    if constexpr (G >= 8) step(std::integral_constant<int, 0x141>{});   // row_half_mirror
-    if constexpr (G >= 4) step(std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]
-    if constexpr (G >= 2) step(std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]
   };
   // Records of one cell, walked by the whole group (group-uniform arguments).  A
   // dense cell (k_map_dense) starts with a header of its 64 sub-cell ends: the
@@ -1286,14 +1311,15 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   };
   // the query's result (one lane): the match moved back to its scan's frame
   // (matcher.hpp:92-96), acceptance (:103-105), insert decision (map.tpp:160-163)
-  auto emit = [&](uint32_t q, double best, uint32_t best_i) {
+  auto emit = [&](uint32_t q, double best, uint32_t best_i, uint32_t sg) {
     const bool found = best_i != 0xFFFFFFFFu;
     int32_t pair = -1;
     double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
     if (found) {
+      // the record, its normal and its segment's inverse pose in flight together (the
+      // segment came with the argmin)
       const double4 p = M.pos[best_i];
-      const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);  // in flight with p
-      const uint32_t sg = (uint32_t)(tag_bits(p.w) >> 32);     // the record's segment
+      const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);
       const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
       double o[3];
       d_xform(Ti, p.x, p.y, p.z, o);
@@ -1316,7 +1342,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
   };
   double best = a.bound;
-  uint32_t best_i = 0xFFFFFFFFu;
+  uint32_t best_i = 0xFFFFFFFFu, best_sg = 0;
 #ifdef FMX_DIAG_PHASE
   uint32_t phase[4] = {t_begin, t_begin, t_begin, t_begin};  // query loaded, passes 0..2 done
 #else
@@ -1342,7 +1368,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         if (d2 <= a.warm_lim) warm_b = d2;
       }
     }
-    nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, n_probe,
+    nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, best_sg, n_probe,
                              n_cand, n_iter, n_list, warm_b,
 #ifdef FMX_DIAG_PHASE
                              phase + 1
@@ -1413,7 +1439,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   }
 
   if constexpr (!FUSED) {
-    if (qi < nq && g == 0) emit(qi, best, best_i);
+    if (qi < nq && g == 0) emit(qi, best, best_i, best_sg);
   } else {
     static_assert(kGroup == 1, "the fused match + linearization runs one lane per query");
     // this lane's accepted match in its map scan's frame, then its row(s)
@@ -1423,7 +1449,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (acc_q) {
       const double4 p = M.pos[best_i];
       const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);
-      const uint32_t sg = (uint32_t)(tag_bits(p.w) >> 32);
+      const uint32_t sg = best_sg;  // (with the argmin: the pose loads need not wait for p)
       const double* Tinv = inv_poses + 12 * sg;  // matcher.hpp:95
       d_xform(Tinv, p.x, p.y, p.z, pi);
       if (planar) d_rot(Tinv, n.x, n.y, n.z, ni);

@@ -27,6 +27,11 @@ for k, v in d["kernels"].items():
           "busy-cycles %.0f" % c.get("SQ_BUSY_CYCLES", 0))
 EOF
 }
-run c5_local --workload c5 --c5-dist local --steps 4 --warmup 2 --no-cpu-baseline
-run c5_wholemap --workload c5 --c5-dist wholemap --steps 4 --warmup 2 --no-cpu-baseline
-run c4 --workload c4 --steps 10 --warmup 5 --no-cpu-baseline --no-c5 --no-ablation --streams ""
+# WORKLOADS: which runs (default all three)
+for w in ${WORKLOADS:-c5_local c5_wholemap c4}; do
+  case $w in
+    c5_local) run c5_local --workload c5 --c5-dist local --steps 4 --warmup 2 --no-cpu-baseline ;;
+    c5_wholemap) run c5_wholemap --workload c5 --c5-dist wholemap --steps 4 --warmup 2 --no-cpu-baseline ;;
+    c4) run c4 --workload c4 --steps 10 --warmup 5 --no-cpu-baseline --no-c5 --no-ablation --streams "" ;;
+  esac
+done
