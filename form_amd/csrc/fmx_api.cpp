@@ -1258,7 +1258,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->blk_lo.release(); c->blk_hi.release(); c->h_work.release();
   c->work.release(); c->pair_base.release();
   c->m_pair.release(); c->m_d2.release(); c->m_pi.release(); c->m_ni.release(); c->m_ins.release();
-  c->m_rec.release();
+  c->m_rec.release(); c->m_cell.release();
   c->hist.release(); c->hist_off.release(); c->thist.release(); c->c_pl.release(); c->c_pt.release(); c->pair_counts.release();
   c->chunk_range.release(); c->chunks.release(); c->n_chunks.release();
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();

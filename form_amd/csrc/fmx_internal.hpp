@@ -340,6 +340,7 @@ struct fmx_ctx {
   // match on the same map and query set starts each query's search bounded by that
   // record's distance at the new pose (any record of the map is a valid bound).
   fmx::DBuf<uint32_t> m_rec;
+  fmx::DBuf<uint4> m_cell;    // per query: its own cell as the last match found it (same scheme)
   uint64_t warm_gen = 1;      // bumped by every map build and query-set change
   uint64_t warm_rec_gen = 0;  // warm_gen when m_rec was last written (0: never)
   fmx::DBuf<uint32_t> thist;  // tiled pair sort: per-(type, pair, tile) counts, self-resetting

@@ -483,6 +483,9 @@ struct MatchArgs {
   const uint32_t* warm;
   uint32_t* rec;
   double warm_lim;
+  // per query, its own cell as the last match found it (packed cell coordinates, record
+  // range, dense bit; fmx_ctx::m_cell): read when `warm` is set, rewritten with rec
+  uint4* cell;
 };
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
@@ -662,7 +665,8 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
                                           uint32_t* hd, double& best, uint32_t& best_rid, uint32_t& best_i,
                                           uint32_t& best_sg,
                                           uint32_t& n_probe, uint32_t& n_cand, uint32_t& n_iter, uint32_t& n_list,
-                                          double warm_b = INFINITY, uint32_t* phase = nullptr) {
+                                          double warm_b = INFINITY, uint32_t* phase = nullptr,
+                                          uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u}, uint4* oc_out = nullptr) {
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
   // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
   // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
@@ -933,6 +937,10 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     }
   };
   const bool inr = key_in_range(bx, by, bz);
+  // the own cell's identity for the per-query cell cache: 21 bits per coordinate (in
+  // range: |coordinate| < 2^18), bit 63 clear (set: no entry)
+  const uint2 own_key = make_uint2((uint32_t)(bx & 0x1FFFFF) | (uint32_t)(by & 0x7FF) << 21,
+                                   (uint32_t)((by >> 11) & 0x3FF) | (uint32_t)(bz & 0x1FFFFF) << 10);
 #if !FMX_F32_BOUNDS
   // lower bound on d^2 from the query to any point of the cell at shift s (fp64)
   auto shift_lb = [&](int s) {
@@ -989,9 +997,19 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     if (inr && s >= 0) {
       const double lb = shift_lb(s);
       if (lb <= best) {  // else conservative: no point inside can win
-        probe(shift_c(s, 0), shift_c(s, 1), shift_c(s, 2), vf, vc, vd);
+        if (own && s == 0 && ocv.x == own_key.x && ocv.y == own_key.y) {
+          // warm: the own cell as the last match on this map found it (no bucket read)
+          vf = ocv.z;
+          vc = ocv.w & 0x7FFFFFFFu;
+          vd = (ocv.w >> 31) != 0;
+        } else {
+          probe(shift_c(s, 0), shift_c(s, 1), shift_c(s, 2), vf, vc, vd);
+          if (own && s == 0 && oc_out) *oc_out = uint4{own_key.x, own_key.y, vf, vc | (vd ? 0x80000000u : 0u)};
+        }
         vlb = lb;
       }
+    } else if (own && s == 0 && oc_out) {
+      *oc_out = uint4{0u, 0x80000000u, 0u, 0u};  // no entry
     }
     // the warm bound joins once the own cell's probe is in flight (the probe does not
     // wait for the warm record's load): a record at distance^2 warm_b exists, so no
@@ -1359,8 +1377,11 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     // warm start: the earlier match's NN record of this query, at the new pose (the same
     // (dx^2 + dz^2) + dy^2 as fold); it bounds the search, it is not taken as the result
     double warm_b = INFINITY;
+    const uint32_t gq = planar ? qi : a.nq_pl + qi;
+    uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u};
+    if (FMX_WARM_START && a.warm && a.cell) ocv = a.cell[gq];
     if (FMX_WARM_START && a.warm) {
-      const uint32_t r = a.warm[planar ? qi : a.nq_pl + qi];
+      const uint32_t r = a.warm[gq];
       if (r != 0xFFFFFFFFu) {
         const double4 p = M.pos[r];
         const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
@@ -1371,11 +1392,11 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, best_sg, n_probe,
                              n_cand, n_iter, n_list, warm_b,
 #ifdef FMX_DIAG_PHASE
-                             phase + 1
+                             phase + 1,
 #else
-                             phase
+                             phase,
 #endif
-    );
+                             ocv, FMX_WARM_START && a.cell && g == 0 ? a.cell + gq : nullptr);
   }
   // work counters for the algorithmic-byte model and the match diagnostics (one plain
   // store per block, summed on the host): probes, candidate records, the largest
@@ -2043,9 +2064,14 @@ void run_pair_scatter(fmx_ctx* c) {
   FMX_HIP(hipGetLastError());
 }
 
-// FMX_NO_WARM: every match cold (A/B switch; results are identical either way)
+// FMX_NO_WARM: every match cold; FMX_NO_CELL_CACHE: warm matches probe their own cell
+// again (A/B switches; results are identical either way)
 static bool no_warm() {
   static const bool v = std::getenv("FMX_NO_WARM") != nullptr;
+  return v;
+}
+static bool no_cell_cache() {
+  static const bool v = std::getenv("FMX_NO_CELL_CACHE") != nullptr;
   return v;
 }
 
@@ -2072,8 +2098,11 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     const uint32_t* before = c->m_rec.p;
     c->m_rec.ensure((size_t)c->n_qpl + c->n_qpt + 1);
     const bool warm = c->warm_rec_gen == c->warm_gen && c->m_rec.p == before && !no_warm();
-    a.warm = warm ? c->m_rec.p : nullptr;
+    const uint4* cbefore = c->m_cell.p;
+    c->m_cell.ensure((size_t)c->n_qpl + c->n_qpt + 1);
+    a.warm = warm && c->m_cell.p == cbefore ? c->m_rec.p : nullptr;
     a.rec = c->m_rec.p;
+    a.cell = no_cell_cache() ? nullptr : c->m_cell.p;
     c->warm_rec_gen = c->warm_gen;
   }
   a.nq_pl = c->n_qpl;
@@ -2208,6 +2237,7 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   // the HBM-bound whole-map set 2-3 % (0.75 -> 0.77 ms per registration)
   a.warm = nullptr;
   a.rec = nullptr;
+  a.cell = nullptr;
   a.warm_lim = 0.0;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
