@@ -536,6 +536,32 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* ws, ui
   return off + incl - v;
 }
 
+// Exclusive scan of n values of the last block's tail, get(i) -> value, put(i, offset):
+// each thread takes a contiguous run of kRun entries per pass, all its reads issued
+// before the scan (one dependent round per pass instead of one per 256 entries); carry
+// is added to every offset; returns carry + the total.
+template <int kRun, class Get, class Put>
+__device__ __forceinline__ uint32_t block_scan_runs(uint32_t n, uint32_t carry, Get get, Put put, uint32_t* ws) {
+  for (uint32_t s0 = 0; s0 < n; s0 += kMatchThreads * kRun) {
+    const uint32_t b = s0 + threadIdx.x * kRun;
+    uint32_t v[kRun];
+#pragma unroll
+    for (int u = 0; u < kRun; ++u) v[u] = b + u < n ? get(b + u) : 0u;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int u = 0; u < kRun; ++u) sum += v[u];
+    uint32_t tot;
+    uint32_t ex = carry + block_excl_scan(sum, ws, tot);
+#pragma unroll
+    for (int u = 0; u < kRun; ++u) {
+      if (b + u < n) put(b + u, ex);
+      ex += v[u];
+    }
+    carry += tot;
+  }
+  return carry;
+}
+
 // The match kernel's last block, tiled sort: scan the (type, pair, tile) counts
 // (read and reset), then what k_pair_base does: per-pair counts and first rows, host
 // copy of the counts, the linearize chunk table.  K <= kTileMaxPairs.
@@ -549,18 +575,14 @@ __device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist,
     const uint32_t ntl = t ? a.ntl_pt : a.ntl_pl;
     const size_t base = t ? (size_t)K * a.ntl_pl : 0;
     const uint32_t n = (uint32_t)K * ntl;
-    uint32_t carry = 0;
-    for (uint32_t s0 = 0; s0 < n; s0 += kMatchThreads) {
-      const uint32_t i = s0 + threadIdx.x;
-      const uint32_t v = i < n ? __hip_atomic_exchange(thist + base + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      uint32_t tot;
-      const uint32_t ex = block_excl_scan(v, ws, tot);
-      if (i < n) {
-        so.hist_off[base + i] = carry + ex;
-        if (i % ntl == 0) s_pb[t][i / ntl] = carry + ex;
-      }
-      carry += tot;
-    }
+    const uint32_t carry = block_scan_runs<4>(
+        n, 0u,
+        [&](uint32_t i) { return __hip_atomic_exchange(thist + base + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); },
+        [&](uint32_t i, uint32_t o) {
+          so.hist_off[base + i] = o;
+          if (i % ntl == 0) s_pb[t][i / ntl] = o;
+        },
+        ws);
     for (int k = threadIdx.x; k < K; k += kMatchThreads)
       if (ntl == 0) s_pb[t][k] = 0;
     if (threadIdx.x == 0) s_pb[t][K] = carry;
@@ -1609,30 +1631,12 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
       host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   __shared__ uint32_t ws[kMatchThreads / kWave];
-  __shared__ uint32_t carry;
   for (int tt = 0; tt < 2; ++tt) {  // planar blocks [0, nb_pl), point blocks [nb_pl, nb)
-    const uint32_t b0 = tt == 0 ? 0u : a.nb_pl, b1 = tt == 0 ? a.nb_pl : a.nb_pl + a.nb_pt;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t s0 = b0; s0 < b1; s0 += kMatchThreads) {
-      const uint32_t b = s0 + threadIdx.x;
-      const uint32_t val =
-          b < b1 ? __hip_atomic_load(ins_blk + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      const uint32_t incl = wave_incl_scan(val);
-      const int w = threadIdx.x / kWave;
-      if (lane_id() == 63) ws[w] = incl;
-      __syncthreads();
-      uint32_t off = 0, tot = 0;
-      for (int i = 0; i < kMatchThreads / kWave; ++i) {
-        if (i < w) off += ws[i];
-        tot += ws[i];
-      }
-      if (b < b1) ins_off[b] = carry + off + incl - val;
-      __syncthreads();
-      if (threadIdx.x == 0) carry += tot;
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, carry);
+    const uint32_t b0 = tt == 0 ? 0u : a.nb_pl, n = tt == 0 ? a.nb_pl : a.nb_pt;
+    const uint32_t tot = block_scan_runs<8>(
+        n, 0u, [&](uint32_t i) { return __hip_atomic_load(ins_blk + b0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); },
+        [&](uint32_t i, uint32_t o) { ins_off[b0 + i] = o; }, ws);
+    if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, tot);
   }
   if (a.sorted && a.tiles) pair_sort_tail(a, thist, so, host_counts);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
