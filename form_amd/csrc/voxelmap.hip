@@ -1804,8 +1804,17 @@ __global__ __launch_bounds__(kTileQ) void k_pair_scatter_t(uint32_t nq_pl, uint3
   const uint32_t nq = planar ? nq_pl : nq_pt;
   const int w = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < (kTileQ / kWave) * K; i += kTileQ) s_cnt[i / K][i % K] = 0;
+  // every load up front: the row's fields with its pair, then the (pair, tile) offset as
+  // soon as the pair is in; the ranking and the per-wave scan run while they fly
+  const size_t gq = planar ? qi : nq_pl + qi;
+  const bool in = qi < nq;
+  const int32_t pair = in ? m_pair[gq] : -1;
+  const double4 pi = in ? m_pi[gq] : make_double4(0, 0, 0, 0);
+  const double4 ni = in && planar ? m_ni[qi] : make_double4(0, 0, 0, 0);
+  const float4 pj = in ? (planar ? q_pl[qi] : q_pt[qi]) : make_float4(0, 0, 0, 0);
+  const size_t hb = planar ? (size_t)max(pair, 0) * ntl_pl + tile : (size_t)K * ntl_pl + (size_t)max(pair, 0) * ntl_pt + tile;
+  const uint32_t hoff = pair >= 0 ? hist_off[hb] : 0u;
   __syncthreads();
-  const int32_t pair = qi < nq ? m_pair[planar ? qi : nq_pl + qi] : -1;
   uint32_t rank = 0;
   bool todo = pair >= 0;
   while (__ballot(todo)) {
@@ -1830,19 +1839,13 @@ __global__ __launch_bounds__(kTileQ) void k_pair_scatter_t(uint32_t nq_pl, uint3
   }
   __syncthreads();
   if (pair < 0) return;
-  const size_t hb = planar ? (size_t)pair * ntl_pl + tile : (size_t)K * ntl_pl + (size_t)pair * ntl_pt + tile;
-  const uint32_t dst = hist_off[hb] + s_cnt[w][pair] + rank;
-  const size_t gq = planar ? qi : nq_pl + qi;
-  const double4 pi = m_pi[gq];
+  const uint32_t dst = hoff + s_cnt[w][pair] + rank;
   if (planar) {
-    const double4 ni = m_ni[qi];
-    const float4 pj = q_pl[qi];
     c_pl[0 * ld_pl + dst] = pi.x; c_pl[1 * ld_pl + dst] = pi.y; c_pl[2 * ld_pl + dst] = pi.z;
     c_pl[3 * ld_pl + dst] = ni.x; c_pl[4 * ld_pl + dst] = ni.y; c_pl[5 * ld_pl + dst] = ni.z;
     c_pl[6 * ld_pl + dst] = (double)pj.x; c_pl[7 * ld_pl + dst] = (double)pj.y;
     c_pl[8 * ld_pl + dst] = (double)pj.z;
   } else {
-    const float4 pj = q_pt[qi];
     c_pt[0 * ld_pt + dst] = pi.x; c_pt[1 * ld_pt + dst] = pi.y; c_pt[2 * ld_pt + dst] = pi.z;
     c_pt[3 * ld_pt + dst] = (double)pj.x; c_pt[4 * ld_pt + dst] = (double)pj.y;
     c_pt[5 * ld_pt + dst] = (double)pj.z;
