@@ -132,15 +132,21 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
   const int w = threadIdx.x / kWave, lane = lane_id(), tid = threadIdx.x;
   const uint32_t ch = blockIdx.x;
   const uint32_t nch = a.n_chunks ? *a.n_chunks : a.n_chunks_host;
+  // the chunk descriptor in the same round as the count (a device count: ch < grid <=
+  // the table's capacity, an entry past the count is read and never used; a host count:
+  // only entries below it)
+  Chunk d{};
+  if (a.n_chunks || ch < a.n_chunks_host) d = a.chunks[ch];
   if (nch == 0) {  // nothing to linearize: publish at once
     if (blockIdx.x == 0 && tid == 0) publish_flag(a.flag, a.seq);
     return;
   }
   if (ch >= nch) return;
   WSTAMP(0);
-  const Chunk d = a.chunks[ch];
   const uint32_t type = d.type & 0xFFu;
   const int slot = (int)d.pair;
+  // the pair's chunk range, in flight with the rows (used after the block sum)
+  const uint32_t cb = a.chunk_range[slot], ce = a.chunk_range[slot + 1];
   int pi, pj;
   if (a.implicit_j >= 0) {
     pi = slot;
@@ -220,7 +226,6 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
 #pragma unroll
     for (int i = 1; i < kWinWaves; ++i) bsum += s_g[i][tid];
   }
-  const uint32_t cb = a.chunk_range[slot], ce = a.chunk_range[slot + 1];
   if (ce - cb > 1) {
     if (tid < 91) agent_store(a.partials + (size_t)ch * kWinLd + tid, bsum);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
