@@ -124,6 +124,66 @@ def test_match_matches_oracle(fmx_mod, oracle, config, subdiv, rot, trans):
         assert np.array_equal((cpl if t == 0 else cpt), counts)
 
 
+@pytest.mark.parametrize("config,subdiv", [("c2", 1), ("c2", 2), ("c3", 1)])
+def test_warm_matches_match_oracle(fmx_mod, oracle, config, subdiv):
+    """Matches after the first on the same map and query set start warm: each search is
+    bounded by the previous match's record at the new pose, and the query's own cell
+    comes from a per-query cache when the query stayed in it.  A sequence of poses that
+    moves queries across cell boundaries (far, then nearer, then back far), a map rebuilt
+    from other scans and a new query set (both must drop the warm state) — every match
+    bit-exact to the oracle."""
+    feats = stream_features(oracle, config, 7)
+    p = feats[0]["params"]
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p),
+                                                  voxel_subdivision=subdiv))
+    w = 0.8
+    for k in range(6):
+        ctx.keypoints_add(k, feats[k]["planar"], feats[k]["point"])
+
+    def build(scans):
+        scans = list(scans)
+        omaps = [oracle.VoxelMap(w, 0), oracle.VoxelMap(w, 1)]
+        for k in scans:
+            omaps[0].add_scan(k, feats[k]["pose"], feats[k]["planar"])
+            omaps[1].add_scan(k, feats[k]["pose"], feats[k]["point"])
+        ctx.map_build(scans, np.stack([feats[k]["pose"] for k in scans]), w)
+        return omaps, np.array(scans, np.uint64)
+
+    def check(built, q, Tj):
+        omaps, scan_of = built  # pair index -> scan id
+        cpl, cpt = ctx.match(Tj, w)
+        got = ctx.match_download()
+        npl = len(q["planar"])
+        for t, (om, Q) in enumerate(zip(omaps, (q["planar"], q["point"]))):
+            ref = om.match(Q, Tj)
+            sl = slice(0, npl) if t == 0 else slice(npl, None)
+            acc_ref = ref["found"] & (ref["d2"] < w * w)
+            pair = got["pair"][sl]
+            assert np.array_equal(pair >= 0, acc_ref)
+            assert np.array_equal(scan_of[pair[acc_ref]], ref["scan"][acc_ref])
+            assert np.array_equal(got["d2"][sl][acc_ref], ref["d2"][acc_ref])
+            assert np.array_equal(got["pi"][sl][acc_ref], ref["pi"][acc_ref])
+            if t == 0:
+                assert np.array_equal(got["ni"][acc_ref], ref["ni"][acc_ref])
+            assert np.array_equal(got["d2"][sl] > 0.01, ~ref["found"] | (ref["d2"] > 0.01))
+            idx = np.searchsorted(scan_of, ref["scan"][acc_ref])  # (scan lists ascending)
+            assert np.array_equal(cpl if t == 0 else cpt, np.bincount(idx, minlength=len(scan_of)))
+
+    rng = np.random.default_rng(11)
+    built = build(range(5))
+    q = feats[5]
+    ctx.set_queries(q["planar"], q["point"], 5)
+    for rot, trans in [(0.02, 0.35), (0.005, 0.03), (0.001, 0.004), (0.0, 0.0), (0.02, 0.35), (0.03, 0.5)]:
+        check(built, q, perturb(q["pose"], rng, rot, trans) if rot else q["pose"])
+    built = build([1, 3, 4])  # a new map: the warm state of the old one must not be used
+    for rot, trans in [(0.005, 0.03), (0.001, 0.004)]:
+        check(built, q, perturb(q["pose"], rng, rot, trans))
+    q = feats[6]  # a new query set
+    ctx.set_queries(q["planar"], q["point"], 6)
+    for rot, trans in [(0.005, 0.03), (0.02, 0.35)]:
+        check(built, q, perturb(q["pose"], rng, rot, trans))
+
+
 def test_match_large_query_set_matches_oracle(fmx_mod, oracle):
     """>= 128k queries: run_match takes the large-set build (fmx::gl, one lane per
     query and 256 queries per block: the C5 path); same bit-exact contract as the 8-lane
