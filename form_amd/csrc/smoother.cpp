@@ -8,12 +8,25 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#ifdef FMX_LM_PROF
+#ifdef FMX_LM_PROF  // diagnostic build: host LM phase times (printed at exit)
 #include <chrono>
-namespace fmxh { double g_lm_prof[4]; }
+#include <cstdio>
+namespace fmxh {
+double g_lm_prof[6];
+uint64_t g_lm_n[6];
+static const char* kLmProfNames[6] = {"H copy + chol_solve", "trial run (launch .. lin_end)", "accept test",
+                                      "after lin_end: add_pair", "iterate prologue", "trial poses"};
+struct LmProfPrint {
+  ~LmProfPrint() {
+    for (int i = 0; i < 6; ++i)
+      if (g_lm_n[i]) fprintf(stderr, "lm %-32s %10.1f us total %8llu calls %8.2f us/call\n", kLmProfNames[i],
+                             g_lm_prof[i] * 1e6, (unsigned long long)g_lm_n[i], g_lm_prof[i] * 1e6 / g_lm_n[i]);
+  }
+} g_lm_print;
+}  // namespace fmxh
 static double lmnow() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 #define LMP_BEGIN(i) const double _lmp##i = lmnow()
-#define LMP_END(i) fmxh::g_lm_prof[i] += lmnow() - _lmp##i
+#define LMP_END(i) (fmxh::g_lm_prof[i] += lmnow() - _lmp##i, ++fmxh::g_lm_n[i])
 #else
 #define LMP_BEGIN(i)
 #define LMP_END(i)
@@ -512,10 +525,12 @@ struct Assembler {
       g.lin_end(G.data());
       ++lins;
     }
+    LMP_BEGIN(3);
     for (size_t p = 0; p < g.pairs.size(); ++p) {
       S.add_pair(g.pairs[p].first, g.pairs[p].second, &G[p * kPairG]);
       err += G[p * kPairG + 91];
     }
+    LMP_END(3);
     return err;
   }
 };
@@ -541,20 +556,23 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
   std::vector<double> gg(D), Hd((size_t)D * D), dx(D);
   auto iterate = [&]() {
     // H is the leading D x D block of S.A (row stride D + 1), read in place
+    LMP_BEGIN(4);
     for (int r = 0; r < D; ++r) gg[r] = S.at(r, D);
     const double cc = S.at(D, D), oldLin = 0.5 * cc;
+    LMP_END(4);
     for (;;) {
+      LMP_BEGIN(0);
       for (int r = 0; r < D; ++r) {
         std::memcpy(&Hd[(size_t)r * D], &S.A[(size_t)r * (D + 1)], D * sizeof(double));
         Hd[(size_t)r * D + r] += lambda;
       }
-      LMP_BEGIN(0);
       const bool ok = chol_solve(Hd, gg.data(), dx.data(), D);
       LMP_END(0);
       bool success = false, stop = false;
       std::vector<Pose> xn;
       double nerr = err;
       if (ok) {
+        LMP_BEGIN(2);
         double dHd = 0, dg = 0;
         for (int r = 0; r < D; ++r) {
           const double h = dot(&S.A[(size_t)r * (D + 1)], dx.data(), D);
@@ -562,9 +580,12 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
           dg += dx[r] * gg[r];
         }
         const double newLin = 0.5 * (dHd - 2 * dg + cc), linChange = oldLin - newLin;
+        LMP_END(2);
         if (linChange >= 0) {
+          LMP_BEGIN(5);
           xn.resize(R.x.size());
           for (size_t k = 0; k < R.x.size(); ++k) xn[k] = compose(R.x[k], expmap(&dx[6 * k]));
+          LMP_END(5);
           LMP_BEGIN(1);
           g.trial_lin_change = linChange;
           g.trial_err = err;
