@@ -1400,9 +1400,11 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     // (dx^2 + dz^2) + dy^2 as fold); it bounds the search, it is not taken as the result
     double warm_b = INFINITY;
     const uint32_t gq = planar ? qi : a.nq_pl + qi;
+    // (the fused launch keeps no warm state: compiled out there)
+    constexpr bool kWarm = FMX_WARM_START && !FUSED;
     uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u};
-    if (FMX_WARM_START && a.warm && a.cell) ocv = a.cell[gq];
-    if (FMX_WARM_START && a.warm) {
+    if (kWarm && a.warm && a.cell) ocv = a.cell[gq];
+    if (kWarm && a.warm) {
       const uint32_t r = a.warm[gq];
       if (r != 0xFFFFFFFFu) {
         const double4 p = M.pos[r];
@@ -1418,7 +1420,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
 #else
                              phase,
 #endif
-                             ocv, FMX_WARM_START && a.cell && g == 0 ? a.cell + gq : nullptr);
+                             ocv, kWarm && a.cell && g == 0 ? a.cell + gq : nullptr);
   }
   // work counters for the algorithmic-byte model and the match diagnostics (one plain
   // store per block, summed on the host): probes, candidate records, the largest
