@@ -453,6 +453,19 @@ def roofline(a, name, d, workload):
         hbm = traffic / (avg_ms * 1e-3) / 1e9
         roof["hbm_achieved"] = round(hbm, 3)
         roof["hbm_frac"] = round(hbm / HBM_PEAK_GBS, 6)
+    # where the kernel's waves spend their cycles (SQ wave-state PMC of the same kernel,
+    # tools/gpu_sqpmc.sh, committed per workload): far below the HBM roof, the match is
+    # a chain of dependent memory rounds with the VALU issue sharing the SIMD
+    sq = os.path.join(ROOT, "profiles", f"sq_wavestate_{workload}.json")
+    try:
+        c = json.load(open(sq))["kernels"][name]["counters_per_launch"]
+        wc = max(c["SQ_WAVE_CYCLES"], 1.0)
+        roof["wave_cycles"] = dict(valu_active=round(c["SQ_ACTIVE_INST_VALU"] / wc, 3),
+                                   memory_wait=round(c["SQ_WAIT_ANY"] / wc, 3),
+                                   issue_wait=round(c["SQ_WAIT_INST_ANY"] / wc, 3),
+                                   source=os.path.relpath(sq, ROOT))
+    except (OSError, KeyError, ValueError):
+        pass
     return roof
 
 
