@@ -505,7 +505,10 @@ constexpr int kMatchThreads = kQPB * kGroup;  // 256
 constexpr int kSmallCell = FMX_SMALL_CELL;  // neighbour cells with at most this many records: one lane folds them
 // Tiled pair sort: a tile = kTileBlocks match blocks of one type = 1024 queries, one
 // k_pair_scatter_t block; the match counts matches per (type, pair, tile).
-constexpr int kTileBlocks = 1024 / kQPB;
+#ifndef FMX_TILE_Q
+#define FMX_TILE_Q 1024  // queries per pair-scatter tile (A/B switch)
+#endif
+constexpr int kTileBlocks = FMX_TILE_Q / kQPB > 0 ? FMX_TILE_Q / kQPB : 1;
 constexpr int kTileQ = kTileBlocks * kQPB;  // 1024
 constexpr int kTileMaxPairs = (int)kMatchTileMaxPairs;  // LDS bound of the tiled path (wider windows: per-block path)
 constexpr int kWorkWords = 8;               // per-block match work / diagnostic words
