@@ -2167,8 +2167,11 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + one 64-B line per
   // hash probe (a brick; a dense cell's 256-B header counts as 4 probes) + 32 B per
   // candidate record tested (double4: position + build order/segment), using the
-  // probe/candidate counts of the previous launch (counted by the kernel).
-  const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + 64.0 * c->last_probes + 32.0 * c->last_cands;
+  // probe/candidate counts of the previous launch (counted by the kernel), + the warm
+  // state: NN record index and own-cell entry written (4 + 16 B), and on a warm launch
+  // also read, with the warm record itself (4 + 16 + 32 B).
+  const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + 64.0 * c->last_probes + 32.0 * c->last_cands +
+                       (a.rec ? 20.0 * nq : 0.0) + (a.warm ? 52.0 * nq : 0.0);
   // the sub-cell walk only when the map may hold dense cells: the build's pinned info
   // word (written by k_map_dense) says "none" for this very build (same epoch)
   bool dense = c->map.n[0] + c->map.n[1] > 0;
