@@ -171,6 +171,9 @@ void settle_match(fmx_ctx* c) {
   c->lazy.pending = false;
   run_match(c, c->lazy.pose, c->lazy.max_dist, c->P.min_dist_map, true, true);
 }
+// Entry points that discard the match results (a new query set, an extraction,
+// register_scan) drop a deferred match instead of launching it: nothing could read it.
+void drop_match(fmx_ctx* c) { c->lazy.pending = false; }
 
 // SETTLE: run a deferred fmx_match first — every entry point but fmx_match itself,
 // fmx_linearize_matched (which may consume it fused) and those that read no match
@@ -324,6 +327,112 @@ void set_queries(fmx_ctx* c, uint64_t scan, const float* pl, uint32_t npl, const
   c->have_qo = false;
 }
 
+// ---- host-resident scans (stage.hpp)
+// Helper threads of the staging copy (FMX_STAGE_THREADS, default 3; 0 = the calling
+// thread copies alone), chunk size (FMX_STAGE_CHUNK_KB, default 256) and the number of
+// DMAs a sequential scan is split into at most (FMX_STAGE_DMAS, default 4: each
+// hipMemcpyAsync call costs the host a few microseconds).
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+int stage_threads() {
+  static const int v = std::max(0, env_int("FMX_STAGE_THREADS", 3));
+  return v;
+}
+size_t stage_chunk() {
+  static const size_t v = (size_t)std::max(4, env_int("FMX_STAGE_CHUNK_KB", 256)) << 10;
+  return v;
+}
+uint32_t stage_dmas() {
+  static const uint32_t v = (uint32_t)std::max(1, env_int("FMX_STAGE_DMAS", 4));
+  return v;
+}
+// FMX_HOST_PAGEABLE (A/B diagnostic): the pre-round-4 path, one pageable hipMemcpyAsync
+bool host_pageable() {
+  static const bool v = std::getenv("FMX_HOST_PAGEABLE") != nullptr;
+  return v;
+}
+// Pinned staging buffers of `bytes` each (grown only; growing drains every stream and
+// staging request first, since DMAs may still read the old ones).
+void pinned_ensure(fmx_ctx* c, size_t bytes) {
+  if (bytes <= c->pin_cap) return;
+  c->stager.retire(&c->st_seq);
+  c->stager.retire(&c->st_pf[0]);
+  c->stager.retire(&c->st_pf[1]);
+  sync_all(c);
+  uint8_t** bufs[3] = {&c->pin_seq, &c->pin_pf[0], &c->pin_pf[1]};
+  for (uint8_t** b : bufs) {
+    if (*b) (void)hipHostFree(*b);
+    *b = nullptr;
+  }
+  c->pin_cap = 0;
+  c->ann_ptr = nullptr;  // a staged announcement lived in the old buffers
+  for (uint8_t** b : bufs) FMX_HIP(hipHostMalloc(reinterpret_cast<void**>(b), bytes, hipHostMallocDefault));
+  c->pin_cap = bytes;
+}
+// Start the staging copy of `bytes` host bytes into pinned `dst` (helpers, if any).
+void stage_submit(fmx_ctx* c, StageReq& r, const void* src, void* dst, size_t bytes) {
+  c->stager.retire(&r);
+  c->stager.start(stage_threads());
+  r.reset(src, dst, bytes, stage_chunk());
+  if (c->stager.threads() > 0) c->stager.submit(&r);
+}
+// Every chunk of r copied (this thread helps) and r released by the helpers.
+void stage_finish(fmx_ctx* c, StageReq& r) {
+  while (r.work_one()) {
+  }
+  while (!r.complete()) std::this_thread::yield();
+  c->stager.retire(&r);
+}
+// Page-locked host memory (hipHostMalloc / hipHostRegister, e.g. fmx_scan_buffer or a
+// pinned torch tensor): both ends of [p, p + bytes) are checked.  Such a scan is DMA'd
+// straight from the caller's memory, without a staging copy.
+bool host_pinned(const void* p, size_t bytes) {
+  if (!p || !bytes) return false;
+  for (const void* q : {p, static_cast<const void*>(static_cast<const uint8_t*>(p) + bytes - 1)}) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+// A host scan for the sequential path, into c->scan on the context stream: a pinned one
+// is DMA'd directly; a pageable one is staged by the helpers and this thread, each
+// completed quarter DMA'd right away.
+const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n) {
+  const size_t bytes = n * sizeof(float4);
+  c->scan.ensure(n);
+  if (host_pageable() || host_pinned(xyzw, bytes)) {
+    FMX_HIP(hipMemcpyAsync(c->scan.p, xyzw, bytes, hipMemcpyHostToDevice, c->stream));
+    return c->scan.p;
+  }
+  pinned_ensure(c, bytes);
+  // pin_seq's previous DMA was on the context stream ahead of an extraction whose totals
+  // the host waited for: it has completed
+  StageReq& r = c->st_seq;
+  stage_submit(c, r, xyzw, c->pin_seq, bytes);
+  uint8_t* dev = reinterpret_cast<uint8_t*>(c->scan.p);
+  const uint32_t step = std::max<uint32_t>(1, (r.nchunks + stage_dmas() - 1) / stage_dmas());
+  uint32_t issued = 0;
+  while (issued < r.nchunks) {
+    uint32_t ready = issued;
+    while (ready < r.nchunks && r.chunk_done(ready)) ++ready;
+    if (ready - issued >= step || ready == r.nchunks) {
+      const size_t a = (size_t)issued * r.chunk, b = std::min(bytes, (size_t)ready * r.chunk);
+      FMX_HIP(hipMemcpyAsync(dev + a, c->pin_seq + a, b - a, hipMemcpyHostToDevice, c->stream));
+      issued = ready;
+      continue;
+    }
+    if (!r.work_one()) std::this_thread::yield();  // help; then wait for the helpers' chunks
+  }
+  c->stager.retire(&r);
+  return c->scan.p;
+}
+
 void pf_drop(fmx_ctx* c);
 void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out,
                 const std::function<void()>& while_waiting = nullptr) {
@@ -340,9 +449,7 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
   if (on_dev) {
     d = reinterpret_cast<const float4*>(xyzw);
   } else {
-    c->scan.ensure(n);
-    FMX_HIP(hipMemcpyAsync(c->scan.p, xyzw, n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-    d = c->scan.p;
+    d = stage_host_scan(c, xyzw, n);
   }
   run_extract(c, d, (int)R, (int)C, out, while_waiting);
   c->q_scan = scan;
@@ -374,8 +481,16 @@ void pf_drop(fmx_ctx* c) {
 // extraction and its first match, which read the current set).  Its results are not
 // read until the register_scan of that scan (pf_take).  Placement measured: here or at
 // the start of the full LM (optimize(false)) is the same within the box-to-box noise.
-void pf_launch(fmx_ctx* c) {
+// A host-announced scan is launched once its staging copy has finished (force: wait for
+// it): register_scan offers the launch after every ICP match and before the full LM,
+// and forces it at its end.
+void pf_launch(fmx_ctx* c, bool force = true) {
   if (!c->ann_ptr || c->pf_launched) return;
+  if (c->ann_host && !c->ann_pinned) {
+    StageReq& r = c->st_pf[c->ann_slot];
+    if (!force && !r.complete()) return;
+    stage_finish(c, r);
+  }
   HostScope hs(14);
   const auto& E = c->P.extraction;
   const float4* d = reinterpret_cast<const float4*>(c->ann_ptr);
@@ -383,6 +498,12 @@ void pf_launch(fmx_ctx* c) {
   if (c->pf_seq == 0) c->h_pf.p[4] = 0;
   FMX_HIP(hipEventRecord(c->ev_pf_fork, c->stream));
   FMX_HIP(hipStreamWaitEvent(c->side2, c->ev_pf_fork, 0));
+  if (c->ann_host) {  // the staged copy -> the device (side2: behind the previous queued extraction's reads)
+    c->pf_scan.ensure(c->ann_n);
+    const void* src = c->ann_pinned ? static_cast<const void*>(c->ann_ptr) : c->pin_pf[c->ann_slot];
+    FMX_HIP(hipMemcpyAsync(c->pf_scan.p, src, c->ann_n * sizeof(float4), hipMemcpyHostToDevice, c->side2));
+    d = c->pf_scan.p;
+  }
   swap_query_set(c);
   try {
     const uint32_t seq = ++c->pf_seq;
@@ -397,6 +518,8 @@ void pf_launch(fmx_ctx* c) {
   c->pf_launched = true;
   c->pf_ptr = c->ann_ptr;
   c->pf_n = c->ann_n;
+  c->pf_host = c->ann_host;
+  c->pf_slot = c->ann_pinned ? -1 : c->ann_slot;
   c->ann_ptr = nullptr;
 }
 // register_scan(scan): true if `scan` is the one whose extraction was queued; its query
@@ -404,7 +527,7 @@ void pf_launch(fmx_ctx* c) {
 // collected.  Any other scan drops the queued extraction.
 bool pf_take(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, uint64_t scan, fmx_feature_counts* out) {
   if (!c->pf_launched) return false;
-  if (!on_dev || xyzw != c->pf_ptr || n != c->pf_n) {
+  if ((on_dev != 0) == c->pf_host || xyzw != c->pf_ptr || n != c->pf_n) {
     pf_drop(c);
     return false;
   }
@@ -718,7 +841,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     const Pose before = e.values.at(j);
     if (!use_spec_match(c, before.m)) run_match(c, before.m, P.max_dist_matching, P.min_dist_map, true);  // pair-major
     c->spec_valid = false;
-    if (it == 0) pf_launch(c);  // the announced next scan's extraction, behind this match
+    pf_launch(c, false);  // the announced next scan's extraction, behind this match (host: once staged)
     // get_graph(true): the current scan's K pairs (empty ones linearize to zero)
     g.pairs.clear();
     for (uint32_t k = 0; k < c->K; ++k) g.pairs.push_back({slot.at(c->map_scans[k]), slot.at(j)});
@@ -796,6 +919,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     map_scans.assign(sset.begin(), sset.end());
   }
   int spec_builds = 0;
+  pf_launch(c, false);  // a host-announced next scan staged by now
   // optimize(false): every stored pair's FeatureFactor (constraints.cpp:294-305)
   const std::vector<WinPair> prs = win_pairs(c);
   g.lins.clear();
@@ -1095,7 +1219,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       ++icp;
       const Pose before = e.values.at(j);
       run_match(c, before.m, P.max_dist_matching, P.min_dist_map, false);  // query order
-      if (it == 0) pf_launch(c);  // the announced next scan's extraction, behind this match
+      pf_launch(c, false);  // the announced next scan's extraction, behind this match (host: once staged)
       int li = 0;
       const Pose after = lm.optimize(before, &li);
       lm_it += li;
@@ -1124,6 +1248,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     lins = lm.linearizations;
   }
   delete hs_icp;
+  pf_launch(c, true);  // an announced host scan whose staging outlasted the ICP loop
   if (!inserted) {  // single-pose mode
     HostScope hs_tail(5);
     record_cons(c, e, j);
@@ -1245,6 +1370,12 @@ void fmx_destroy(fmx_ctx* c) {
   c->q_pl_pos.release(); c->q_pl_nrm.release(); c->q_pt_pos.release(); c->q_pl_idx.release(); c->q_pt_idx.release();
   c->nq_pl_pos.release(); c->nq_pl_nrm.release(); c->nq_pt_pos.release(); c->nq_pl_idx.release(); c->nq_pt_idx.release();
   c->n_planar_mask.release(); c->h_pf.release();
+  c->stager.stop();  // no helper touches the staging buffers after this
+  for (uint8_t* b : {c->pin_seq, c->pin_pf[0], c->pin_pf[1]})
+    if (b) (void)hipHostFree(b);
+  c->pf_scan.release();
+  for (auto& B : c->scanbuf)
+    if (B.p) (void)hipHostFree(B.p);
   for (int t = 0; t < 2; ++t) {
     c->pool[t].pos.release(); c->pool[t].nrm.release();
     c->segs[t].release(); c->h_segs[t].release();
@@ -1264,6 +1395,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
+  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release();
   {
     auto& S = c->spec;
     S.m_pair.release(); S.m_d2.release(); S.m_pi.release(); S.m_ni.release(); S.m_ins.release();
@@ -1291,7 +1423,10 @@ void fmx_destroy(fmx_ctx* c) {
 const char* fmx_last_error(const fmx_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 fmx_status fmx_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_dev, fmx_feature_counts* out) {
-  return guard(c, [&] { do_extract(c, xyzw, n, scan, on_dev, out); });
+  return guard<false>(c, [&] {
+    drop_match(c);
+    do_extract(c, xyzw, n, scan, on_dev, out);
+  });
 }
 
 fmx_status fmx_extract_download(fmx_ctx* c, float* planar, uint32_t* planar_index, float* point,
@@ -1327,8 +1462,9 @@ fmx_status fmx_extract_download(fmx_ctx* c, float* planar, uint32_t* planar_inde
 
 fmx_status fmx_set_queries(fmx_ctx* c, uint64_t scan, const float* planar, uint32_t npl, const float* point,
                            uint32_t npt) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
     if ((npl && !planar) || (npt && !point)) throw StatusError(FMX_E_INVAL, "null features");
+    drop_match(c);
     set_queries(c, scan, planar, npl, point, npt);
   });
 }
@@ -1355,8 +1491,9 @@ fmx_status fmx_keypoints_add_device(fmx_ctx* c, uint64_t scan, const float* plp,
 
 fmx_status fmx_set_queries_device(fmx_ctx* c, uint64_t scan, const float* plp, const float* pln, uint32_t npl,
                                   const float* ptp, uint32_t npt) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
     if ((npl && (!plp || !pln)) || (npt && !ptp)) throw StatusError(FMX_E_INVAL, "null features");
+    drop_match(c);
     set_queries_device(c, scan, plp, pln, npl, ptp, npt);
   });
 }
@@ -1382,6 +1519,8 @@ fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint3
     if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
     if (!(max_dist > 0)) throw StatusError(FMX_E_INVAL, "max_dist must be > 0");
     if (!pose_j) throw StatusError(FMX_E_INVAL, "null pose");
+    // validated here, not when a deferred match is launched (the error belongs to this call)
+    check_match_reach(c, max_dist, c->P.min_dist_map);
     // no count outputs on a large query set (the one-lane-per-query build): deferred,
     // so that fmx_linearize_matched at this pose can run fused with it
     const bool defer = !cpl && !cpt && match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) == 1 &&
@@ -1508,7 +1647,8 @@ fmx_status fmx_register_points(fmx_ctx* c, const double pose_init[12], double ma
       // Matcher::match at T + the summed single-pose system (all-reduced when sharded)
       if (fused) {
         run_match_linearize_total(c, T.m, max_dist, sigma, S);
-        c->lazy.pending = true;  // the last match stays available (launched on demand)
+        // the last match stays available (launched on demand) when run_match accepts it
+        c->lazy.pending = match_reach_ok(c, max_dist, c->P.min_dist_map);
         std::memcpy(c->lazy.pose, T.m, sizeof(T.m));
         c->lazy.max_dist = max_dist;
       } else {
@@ -1556,23 +1696,58 @@ fmx_status fmx_comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank
 }
 
 fmx_status fmx_next_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev) {
-  return guard(c, [&] {
+  return guard<false>(c, [&] {
     if (!xyzw) {  // withdraw the announcement
       c->ann_ptr = nullptr;
       return;
     }
     const auto& E = c->P.extraction;
-    if (!on_dev) throw StatusError(FMX_E_INVAL, "fmx_next_scan: pipelined extraction needs a device-resident scan");
     if (n != (size_t)E.num_rows * (size_t)E.num_columns)
       throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " +
                                         std::to_string((size_t)E.num_rows * E.num_columns) + " != " + std::to_string(n));
+    c->ann_pinned = !on_dev && host_pinned(xyzw, n * sizeof(float4));
+    if (!on_dev && !c->ann_pinned) {
+      // a pageable host scan: its staging copy into a pinned slot starts now, in the
+      // background (the helpers copy it while the caller's next register_scan runs)
+      pinned_ensure(c, n * sizeof(float4));
+      const int slot = c->ann_ptr && c->ann_host && !c->ann_pinned
+                           ? c->ann_slot ^ 1
+                           : (c->pf_launched && c->pf_host && c->pf_slot >= 0 ? c->pf_slot ^ 1 : 0);
+      // the slot's pinned bytes may still feed the DMA of a queued, not yet taken extraction
+      if (c->pf_launched && c->pf_host && c->pf_slot == slot) FMX_HIP(hipStreamSynchronize(c->side2));
+      stage_submit(c, c->st_pf[slot], xyzw, c->pin_pf[slot], n * sizeof(float4));
+      if (c->stager.threads() == 0) stage_finish(c, c->st_pf[slot]);
+      c->ann_slot = slot;
+    }
+    c->ann_host = !on_dev;
     c->ann_ptr = xyzw;
     c->ann_n = n;
   });
 }
 
+fmx_status fmx_scan_buffer(fmx_ctx* c, size_t n, float** out) {
+  return guard<false>(c, [&] {
+    if (!out || !n) throw StatusError(FMX_E_INVAL, "null output / zero points");
+    auto& B = c->scanbuf[c->scanbuf_next];
+    if (B.cap < n) {
+      // the buffer may feed a queued DMA (a registered or announced scan): drain first
+      sync_all(c);
+      if (B.p) (void)hipHostFree(B.p);
+      B.p = nullptr;
+      B.cap = 0;
+      FMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&B.p), n * sizeof(float4), hipHostMallocDefault));
+      B.cap = n;
+    }
+    c->scanbuf_next = (c->scanbuf_next + 1) % 3;
+    *out = reinterpret_cast<float*>(B.p);
+  });
+}
+
 fmx_status fmx_register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
-  return guard(c, [&] { register_scan(c, xyzw, n, on_dev, out); });
+  return guard<false>(c, [&] {
+    drop_match(c);
+    register_scan(c, xyzw, n, on_dev, out);
+  });
 }
 
 fmx_status fmx_current_pose(fmx_ctx* c, double pose[12]) {

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "fmx/fmx.h"
+#include "stage.hpp"
 
 namespace fmx {
 
@@ -311,6 +312,27 @@ struct fmx_ctx {
   hipEvent_t ev_pf = nullptr, ev_pf_fork = nullptr;
   uint64_t pf_used = 0, pf_dropped = 0;
 
+  // ---- host-resident scans (stage.hpp): the reference passes the scan as a host
+  // std::vector<PointXYZf> (form.hpp:82-83).  Copied into pinned memory by helper
+  // threads + the caller, then DMA'd: the sequential path DMAs each completed part at
+  // once; an announced host scan (fmx_next_scan) is copied in the background and DMA'd
+  // + extracted on side2 once its copy has finished.
+  fmx::Stager stager;
+  fmx::StageReq st_seq, st_pf[2];
+  uint8_t* pin_seq = nullptr;
+  uint8_t* pin_pf[2] = {nullptr, nullptr};
+  size_t pin_cap = 0;           // bytes of each pinned staging buffer
+  bool ann_host = false;        // the announced scan is host memory (staged in st_pf[ann_slot])
+  bool ann_pinned = false;      // ... page-locked: DMA'd from the caller's memory, no staging
+  int ann_slot = 0, pf_slot = 0;  // pf_slot -1: the queued extraction's DMA read caller memory
+  bool pf_host = false;         // the queued extraction's scan was host memory
+  fmx::DBuf<float4> pf_scan;    // device copy of a host-announced scan (side2 order)
+  struct ScanBuf {              // fmx_scan_buffer: pinned scan buffers handed to the caller
+    float4* p = nullptr;
+    size_t cap = 0;
+  } scanbuf[3];
+  int scanbuf_next = 0;
+
   // ---- window keypoint store + maps
   fmx::Pool pool[2];
   fmx::VoxMap map;  // both feature types
@@ -379,6 +401,9 @@ struct fmx_ctx {
   fmx::DBuf<uint32_t> fz_tickets;                 // fused match + linearization: per block-group tickets
   fmx::DBuf<uint32_t> mcnt, mticket;              // query-order match: per-pair counters + ticket
   bool fz_work_pending = false;                   // fused launch's work counters copied, not yet summed
+  fmx::DBuf<uint32_t> fz_work;                    // ... its own per-block work words (a settled match's
+  fmx::HBuf<uint32_t> fz_h_work;                  // work / h_work may still await match_counts_fetch)
+  uint32_t fz_work_blocks = 0;
   fmx::DBuf<uint32_t> ins_blk, ins_off;           // per match block insert counts / offsets
   uint32_t ins_tot[2] = {0, 0};                   // insert totals of the last match
   uint32_t match_nb_pl = 0, match_nb = 0;         // blocks of the last match
@@ -586,6 +611,18 @@ inline void wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq, hipS
     }
   }
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+// The search reach of a match (run_match, and fmx_match before it defers one): on a
+// subdivided map (cell_m > 1) the rings searched cover one reference voxel, so neither
+// the acceptance radius nor the insert threshold may exceed the voxel width.
+inline bool match_reach_ok(const fmx_ctx* c, double max_dist, double min_dist_map) {
+  const double obs = std::max(max_dist * max_dist, min_dist_map * min_dist_map);
+  const double reach = c->cell_m * c->cell_w;  // = the map's voxel width
+  return !(obs > reach * reach && c->cell_m > 1);
+}
+inline void check_match_reach(const fmx_ctx* c, double max_dist, double min_dist_map) {
+  if (!match_reach_ok(c, max_dist, min_dist_map))
+    throw StatusError(FMX_E_INVAL, "max_dist / min_dist_map exceed the voxel width of a subdivided map");
 }
 inline uint32_t next_flag(fmx_ctx* c) {
   if (!c->h_flag.p) {

@@ -2100,8 +2100,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   a.min_d2 = min_dist_map * min_dist_map;
   const double obs = std::max(a.max_d2, a.min_d2);
   const double reach = c->cell_m * c->cell_w;  // = the map's voxel width
-  if (obs > reach * reach && c->cell_m > 1)
-    throw StatusError(FMX_E_INVAL, "max_dist / min_dist_map exceed the voxel width of a subdivided map");
+  check_match_reach(c, max_dist, min_dist_map);
   a.bound = obs <= reach * reach ? obs : INFINITY;
   // warm start from the last match on this map and query set (m_rec, stream order); an
   // unbounded search (a.bound = inf) takes a warm record only well inside the reach
@@ -2263,8 +2262,10 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   a.tiles = 0;
   a.ntl_pl = a.ntl_pt = 0;
   const uint32_t nb = a.nb_pl + a.nb_pt;
-  c->work.ensure(kWorkWords * (size_t)nb + 8);
-  c->work_blocks = nb;
+  // work words of its own: a settled match's (work, h_work) may still be waiting for
+  // match_counts_fetch, which must not see this launch's counters
+  c->fz_work.ensure(kWorkWords * (size_t)nb + 8);
+  c->fz_work_blocks = nb;
   const uint32_t ngrp = (nb + kFzGroup - 1) / kFzGroup;
   c->bpart.ensure((size_t)(nb + ngrp + 1) * kFzLd);
   ensure_zeroed(c->ticket, 1, st);
@@ -2296,7 +2297,7 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
     auto kern = dense ? k_match<true, true> : k_match<false, true>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(kMatchThreads),
                        std::max<int>(a.K, 1) * sizeof(uint32_t), st, a, view(0), view(1), c->q_pl_pos.p,
-                       c->q_pt_pos.p, c->map_inv_p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, c->work.p,
+                       c->q_pt_pos.p, c->map_inv_p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, c->fz_work.p,
                        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, so, fz);
     FMX_HIP(hipGetLastError());
   }
@@ -2307,9 +2308,9 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   throw StatusError(FMX_E_STATE, "fused match + linearization needs the one-lane-per-query build");
 #endif
   if (c->prof.on) {  // per-block work counters (byte model of the next launch), read by work_fetch
-    c->h_work.ensure(kWorkWords * (size_t)nb + 8);
-    FMX_HIP(hipMemcpyAsync(c->h_work.p, c->work.p, kWorkWords * (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           st));
+    c->fz_h_work.ensure(kWorkWords * (size_t)nb + 8);
+    FMX_HIP(hipMemcpyAsync(c->fz_h_work.p, c->fz_work.p, kWorkWords * (size_t)nb * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, st));
     c->fz_work_pending = true;
   }
 }
@@ -2319,11 +2320,11 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
 void work_fetch(fmx_ctx* c) {
   if (!c->fz_work_pending) return;
   double tp = 0, tc = 0;
-  for (uint32_t b = 0; b < c->work_blocks; ++b) {
-    tp += c->h_work.p[kWorkWords * b];
-    tc += c->h_work.p[kWorkWords * b + 1];
+  for (uint32_t b = 0; b < c->fz_work_blocks; ++b) {
+    tp += c->fz_h_work.p[kWorkWords * b];
+    tc += c->fz_h_work.p[kWorkWords * b + 1];
   }
-  match_diag_add(c->h_work.p, c->work_blocks);
+  match_diag_add(c->fz_h_work.p, c->fz_work_blocks);
   c->last_probes = tp;
   c->last_cands = tc;
   c->fz_work_pending = false;

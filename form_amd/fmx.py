@@ -82,7 +82,7 @@ EXPORTED = [
     "fmx_current_pose",
     "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
     "fmx_profile_name", "fmx_profile_read", "fmx_sync", "fmx_comm_unique_id", "fmx_comm_init",
-    "fmx_map_download", "fmx_register_points",
+    "fmx_map_download", "fmx_register_points", "fmx_scan_buffer",
 ]
 
 
@@ -340,17 +340,29 @@ class Context:
         self.n_planar, self.n_point = c.planar, c.point
         return c.planar, c.point
 
+    def scan_buffer(self, n: int | None = None) -> np.ndarray:
+        """fmx_scan_buffer: a context-owned page-locked (n, 4) float32 buffer (default:
+        rows * cols points) to assemble a scan in; registered or announced as a host scan
+        it is DMA'd without a staging copy.  Buffers rotate over three: the array
+        returned here aliases the one returned by the third next call."""
+        e = self.params.extraction
+        n = n or e.num_rows * e.num_columns
+        p = C.c_void_p()
+        self._chk(self._L.fmx_scan_buffer(self.h, C.c_size_t(n), C.byref(p)))
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n, 4))
+
     def next_scan(self, scan):
         """fmx_next_scan: announce the scan that follows the one the next register_scan
-        receives (a contiguous (N, 4) float32 CUDA tensor, left unchanged until its own
-        register_scan); that call extracts it while registering.  None withdraws."""
+        receives — a contiguous (N, 4) float32 CUDA tensor, or a host array / tensor (its
+        staging copy then starts at once, in the background) — left unchanged until its
+        own register_scan; that call extracts it while registering.  None withdraws."""
         if scan is None:
             self._chk(self._L.fmx_next_scan(self.h, None, C.c_size_t(0), C.c_int(0)))
             return
         on_dev, ptr, n, keep = _scan_ptr(scan)
-        if not on_dev or keep is not scan:
-            raise ValueError("next_scan needs a contiguous (N, 4) float32 CUDA tensor")
-        self._chk(self._L.fmx_next_scan(self.h, ptr, C.c_size_t(n), C.c_int(1)))
+        if keep is not scan:  # a converted copy would not be the object later registered
+            raise ValueError("next_scan needs a contiguous (N, 4) float32 array or tensor")
+        self._chk(self._L.fmx_next_scan(self.h, ptr, C.c_size_t(n), C.c_int(on_dev)))
         # the tensor must outlive the extraction queued for it
         self._pf_keep = (getattr(self, "_pf_keep", (None, None))[1], scan)
 
@@ -526,7 +538,8 @@ class FORM:
     ``set_lidar_params``, ``set_imu_T_lidar``, ``initialize``, then ``add_lidar`` per
     scan, ``pose()`` and ``map()``.  ``add_lidar`` returns {"planar", "point"} as
     (F, 4) arrays of (x, y, z, scan) in the scan's frame — the reference's evalio
-    Points carry the scan index in `col` (bindings.cpp:31-41); ``map()`` the same in the
+    Points carry the scan index in `col` as a uint16 (bindings.cpp:31-41, so it wraps
+    modulo 65536); ``map()`` the same in the
     world frame, voxel by voxel (bindings.cpp:96-119)."""
 
     def __init__(self, device: int = 0):
@@ -618,12 +631,15 @@ class FORM:
         self._scan += 1
         self._pose = _pose44(self._est.current_pose()) @ self.lidar_T_imu
         d = self._est.extract_download()
+        # point_to_evalio stores the scan id as static_cast<uint16_t>(scan) in the
+        # point's col (bindings.cpp:31-41): it wraps past 65535 scans
+        sid = self._scan % 65536
         planar = np.zeros((len(d["planar"]), 4))
         planar[:, :3] = d["planar"][:, :3]
-        planar[:, 3] = self._scan
+        planar[:, 3] = sid
         point = np.zeros((len(d["point"]), 4))
         point[:, :3] = d["point"]
-        point[:, 3] = self._scan
+        point[:, 3] = sid
         return {"planar": planar, "point": point}
 
     def pose(self) -> np.ndarray:
@@ -640,6 +656,6 @@ class FORM:
         for name, (xyz, _, sc) in m.items():
             a = np.zeros((len(xyz), 4))
             a[:, :3] = xyz
-            a[:, 3] = sc
+            a[:, 3] = sc % 65536  # uint16 col, as add_lidar (map_download keeps the raw id)
             out[name] = a
         return out

@@ -98,9 +98,22 @@ const char* fmx_last_error(const fmx_ctx* ctx);
  * Replaces FeatureExtractor::extract<PointXYZf> (extraction.hpp:99-101,
  * extraction.tpp:29-132).  xyzw: rows*cols float4; src_on_device != 0 means
  * xyzw is a device pointer on the context's device, else host memory.
- * The features stay device-resident as the context's current query set. */
+ * The features stay device-resident as the context's current query set.
+ * Host scans (here, in fmx_register_scan and fmx_next_scan): page-locked memory (from
+ * fmx_scan_buffer, hipHostMalloc, hipHostRegister) is DMA'd directly; pageable memory
+ * (the reference's std::vector<PointXYZf>, form.hpp:82-83) is first copied into the
+ * context's pinned staging memory by a few helper threads and the caller, each part
+ * DMA'd as soon as it is copied (FMX_STAGE_THREADS, default 3 helpers).  The pad
+ * component must be 0, as every reference PointXYZf's is (utils.hpp:38-46). */
 fmx_status fmx_extract(fmx_ctx* ctx, const float* xyzw, size_t n_points, uint64_t scan_idx,
                        int src_on_device, fmx_feature_counts* out);
+/* A context-owned page-locked buffer of n_points float4 (PointXYZf layout) that a
+ * caller assembling its scans (as FORM::add_lidar does, bindings.cpp:150-159) can fill
+ * directly: passed as a host scan (src_on_device = 0) it is DMA'd with no staging copy.
+ * Three buffers are handed out in turn: the one returned here is returned again by the
+ * third next call, so a caller may fill scan k+1 while scan k registers.  Valid until
+ * fmx_destroy. */
+fmx_status fmx_scan_buffer(fmx_ctx* ctx, size_t n_points, float** out);
 /* Copy the last extraction to host (any pointer may be NULL):
  * planar[6*planar], planar_index[planar] (scan point index), point[3*point],
  * point_index[point], planar_mask[rows*cols] (compute_valid_points, 0/1). */
@@ -138,7 +151,17 @@ fmx_status fmx_map_build(fmx_ctx* ctx, const uint64_t* scans, const double* pose
  * bucketed per pair on the device.  counts_planar / counts_point (may be NULL):
  * K = n_scans accepted correspondences per pair.  With both NULL the call returns
  * without waiting for the device (once the map build's range check has been read);
- * the calls that read the results wait for them. */
+ * the calls that read the results wait for them.
+ * Deferred match: with both NULL on a large query set (>= 128k queries, windows of
+ * <= 256 scans) the match is not launched yet.  Arguments are validated by this call
+ * (FMX_E_INVAL / FMX_E_STATE are returned here, never by a later call).  If the next
+ * consumer is fmx_linearize_matched at the same pose, match and linearization run as
+ * ONE fused launch that writes no per-query results; its 7 x 7 sums are accumulated in
+ * a different order than the two-step path (equal to 1e-10 relative, not bit for bit).
+ * Any other reader (fmx_match_download, fmx_map_insert, fmx_linearize, ...) launches
+ * the deferred match first, so its results are those of an immediate match.  Calls
+ * that discard match results (fmx_set_queries*, fmx_extract, fmx_register_scan) drop
+ * a deferred match without launching it. */
 fmx_status fmx_match(fmx_ctx* ctx, const double pose_j34[12], double max_dist,
                      uint32_t* counts_planar, uint32_t* counts_point);
 /* Per-query match results of the last fmx_match, planar queries then point
@@ -169,7 +192,8 @@ fmx_status fmx_linearize(fmx_ctx* ctx, const double* poses_i34, const double* po
 fmx_status fmx_error(fmx_ctx* ctx, const double* poses_i34, const double* poses_j34,
                      double sigma, double* err);
 /* The single-pose ablation's whole linear system at X(j) = pose_j34 (X(i) fixed at
- * the built map's poses): sum over every accepted match of the last fmx_match of the
+ * the built map's poses; fused with a deferred fmx_match at the same pose, see
+ * fmx_match): sum over every accepted match of the last fmx_match of the
  * 7 x 7 [H_j b]^T [H_j b] — what GTSAM's LM eliminates from get_single_graph's
  * BinaryFactorWrapper<FeatureFactor>s (constraints.cpp:235-250, gtsam.hpp:40-54,
  * 144-170) — in one launch over the match outputs in query order.  out[0..27]: the
@@ -216,9 +240,12 @@ fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, i
  * that call extracts it (FeatureExtractor::extract, extraction.tpp:29-132) on a side
  * stream while it registers its own scan, and the register_scan of this scan then
  * skips its extraction.  Results are identical either way: extraction depends only on
- * the scan.  The scan must be device-resident (src_on_device = 1, else FMX_E_INVAL)
- * and unchanged until its own fmx_register_scan returns; registering a different
- * pointer discards the queued extraction.  xyzw = NULL withdraws the announcement. */
+ * the scan.  The scan may be device-resident (src_on_device = 1) or host memory (0: a
+ * pageable scan's staging copy starts at once on the helper threads, and the scan is
+ * DMA'd and extracted on the side stream as soon as that copy has finished); it must
+ * stay unchanged until its own fmx_register_scan returns.  That call must pass the
+ * same pointer with the same src_on_device, else the queued extraction is discarded
+ * and the scan extracted in the call.  xyzw = NULL withdraws the announcement. */
 fmx_status fmx_next_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, int src_on_device);
 /* Estimator::current_lidar_estimate (form/form.hpp:79). */
 fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);

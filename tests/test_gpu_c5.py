@@ -302,3 +302,65 @@ def test_two_rank_shards_match_unsharded(fmx_mod, tmp_path):
     S1, e1 = ctx.linearize_matched(Tj, 0.1)
     ref = np.append(S1, e1)
     assert np.all(np.abs(S[0] - ref) <= 1e-10 * np.abs(ref).max())
+
+
+def test_register_points_with_comm_is_identity(fmx_mod, c5_map):
+    """fmx_register_points with a one-rank RCCL communicator attached (every ICP
+    iteration's system all-reduced on the device, then published behind the completion
+    word) follows the no-communicator iterates bit for bit."""
+    pos4, nrm4 = c5_map
+    q4, n4 = shard.make_queries(pos4, nrm4, 300000, shard.c5_offset(), 0.03, 84)
+    out = []
+    for use_comm in (False, True):
+        ctx = _ctx(fmx_mod, pos4.shape[0])
+        if use_comm:
+            ctx.comm_init(fmx_mod.comm_unique_id(), 1, 0)
+        ctx.keypoints_add_device(0, pos4, nrm4)
+        ctx.map_build([0], I34[None], W)
+        ctx.set_queries_device(q4, n4)
+        out.append(ctx.register_points(I34, W, 0.1, 30, 1e-4))
+        ctx.close()
+    (T0, i0), (T1, i1) = out
+    assert i0 == i1 and np.array_equal(T0, T1)
+
+
+def test_dropped_deferred_match_is_never_launched(fmx_mod, c5_map):
+    """a registration leaves its last match deferred; a new query set drops
+    it instead of launching a 300k-query match nobody reads (the streaming C5 loop:
+    set_queries -> register_points -> set_queries -> register_points)."""
+    pos4, nrm4 = c5_map
+    ctx = _ctx(fmx_mod, pos4.shape[0])
+    ctx.keypoints_add_device(0, pos4, nrm4)
+    ctx.map_build([0], I34[None], W)
+    ctx.profile(True)
+    ctx.profile_reset()
+    for seed in (85, 86):
+        q4, n4 = shard.make_queries(pos4, nrm4, 300000, shard.c5_offset(), 0.03, seed)
+        ctx.set_queries_device(q4, n4)
+        ctx.register_points(I34, W, 0.1, 30, 1e-4)
+    prof = ctx.profile_read()
+    assert prof["match"]["launches"] == 0 and prof["match_linearize"]["launches"] >= 4
+    got = ctx.match_download()  # the last registration's match is still available on demand
+    assert (got["pair"] >= 0).sum() > 0.9 * 300000
+    assert ctx.profile_read()["match"]["launches"] == 1
+    ctx.close()
+
+
+def test_deferred_match_validates_its_arguments(fmx_mod):
+    """fmx_match reports a bad max_dist itself (a radius beyond the voxel
+    width of a subdivided map), before it defers the launch; the next call is unaffected."""
+    import torch
+    pos4, nrm4 = shard.terrain_map(801, W, synth.SEED, "cuda:0")
+    q4, n4 = shard.make_queries(pos4, nrm4, 200000, shard.c5_offset(), 0.03, 87)
+    torch.cuda.synchronize()
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(keypoint_pool_capacity=pos4.shape[0] + 1024, voxel_subdivision=2))
+    ctx.keypoints_add_device(0, pos4, nrm4)
+    ctx.map_build([0], I34[None], W)
+    ctx.set_queries_device(q4, n4)
+    with pytest.raises(fmx_mod.FmxError, match="FMX_E_INVAL"):
+        ctx.match(I34, 1.5 * W, counts=False)
+    ctx.map_build([0], I34[None], W)  # not poisoned by the rejected match
+    ctx.match(I34, W, counts=False)
+    S, e = ctx.linearize_matched(I34, 0.1)
+    assert e > 0 and np.isfinite(S).all()
+    ctx.close()

@@ -2,7 +2,7 @@
 side stream.  Extraction depends only on the scan, so a pipelined stream must give the
 same features and the same poses, bit for bit, as a sequential one — and as the oracle
 (1e-6).  Also: a registered scan that is not the announced one drops the queued
-extraction; announcing a host array is refused."""
+extraction; host-resident scans (staged through pinned memory) pipeline the same way."""
 import numpy as np
 import pytest
 
@@ -85,12 +85,95 @@ def test_unannounced_scan_drops_queued_extraction(fmx_mod, oracle):
         assert np.abs(ctx.current_pose() - To).max() < 1e-6, k
 
 
-def test_next_scan_rejects_host_array(fmx_mod):
+def test_next_scan_rejects_bad_scans(fmx_mod):
     geo = synth.GEOMETRIES["tiny"]
     p = synth.default_params(geo)
     ctx = _ctx(fmx_mod, p)
     s = synth.make_scan("tiny", 0)[0]
     with pytest.raises(ValueError):
-        ctx.next_scan(s)  # a CPU tensor
+        ctx.next_scan(s.numpy()[:, :3])  # not (N, 4)
+    with pytest.raises(ValueError):
+        ctx.next_scan(s.double().numpy())  # a converted copy would not be the registered object
     with pytest.raises(Exception):
         ctx.next_scan(s[:-1].to("cuda:0").contiguous())  # wrong size
+    with pytest.raises(Exception):
+        ctx.next_scan(s.numpy()[:-1])  # wrong size (host)
+
+
+def _host_stream(config, n):
+    world = synth.World()
+    return [synth.make_scan(config, k, world=world)[0].numpy().copy() for k in range(n)]
+
+
+@pytest.mark.parametrize("single", [False, True])
+def test_host_pipelined_stream_matches_oracle(fmx_mod, oracle, single):
+    """Host-resident scans (the reference's std::vector<PointXYZf> boundary) announced
+    with fmx_next_scan: staged into pinned memory in the background, DMA'd and extracted
+    during the previous registration; poses within 1e-6 of the oracle."""
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    n = 8
+    scans = _host_stream("tiny", n)
+    ctx = _ctx(fmx_mod, p, single)
+    prm = oracle.default_params(p)
+    prm.disable_smoothing = int(single)
+    oest = oracle.Estimator(prm)
+    for k in range(n):
+        if k + 1 < n:
+            ctx.next_scan(scans[k + 1])
+        ctx.register_scan(scans[k])
+        assert ctx.last_stats()["pipelined"] == (1 if k > 0 else 0)
+        To, _, _ = oest.register_scan(scans[k])
+        assert np.abs(ctx.current_pose() - To).max() < 1e-6, k
+
+
+def test_host_input_c4_equals_device_sequential(fmx_mod):
+    """A 24-scan C4 stream three ways — device sequential, host sequential (staged
+    copy + chunked DMA), host pipelined (background staging) — gives identical
+    features and poses after every registration."""
+    geo = synth.GEOMETRIES["c4"]
+    p = synth.default_params(geo)
+    n = 24
+    dev = _stream("c4", n)
+    host = [s.cpu().numpy().copy() for s in dev]
+    ref, hseq, hpip = _ctx(fmx_mod, p), _ctx(fmx_mod, p), _ctx(fmx_mod, p)
+    for k in range(n):
+        ref.register_scan(dev[k])
+        hseq.register_scan(host[k])
+        if k + 1 < n:
+            hpip.next_scan(host[k + 1])
+        hpip.register_scan(host[k])
+        for c in (hseq, hpip):
+            assert np.array_equal(ref.current_pose(), c.current_pose()), k
+            a, b = ref.extract_download(), c.extract_download()
+            for key in ("planar_index", "point_index", "planar", "point"):
+                assert np.array_equal(a[key], b[key]), (k, key)
+        assert hpip.last_stats()["pipelined"] == (1 if k > 0 else 0)
+        assert hseq.last_stats()["pipelined"] == 0
+
+
+def test_host_announcement_mismatch_drops(fmx_mod, oracle):
+    """A host announcement is matched by pointer and memory kind: registering the same
+    scan from another host array, or from the device, drops the queued extraction; a
+    later announcement of the same buffer object is still taken."""
+    geo = synth.GEOMETRIES["tiny"]
+    p = synth.default_params(geo)
+    host = _host_stream("tiny", 6)
+    ctx = _ctx(fmx_mod, p)
+    oest = oracle.Estimator(oracle.default_params(p))
+    import torch
+    steps = [  # (registered scan object, announcement, expected 'pipelined')
+        (host[0], host[1], 0),
+        (host[1].copy(), host[2], 0),            # same content, other pointer: dropped
+        (torch.from_numpy(host[2]).to("cuda:0"), host[3], 0),  # device copy of the announced scan: dropped
+        (host[3], host[4], 1),
+        (host[4], None, 1),
+        (host[5], None, 0),
+    ]
+    for k, (scan, ann, expect) in enumerate(steps):
+        if ann is not None:
+            ctx.next_scan(ann)
+        ctx.register_scan(scan)
+        assert ctx.last_stats()["pipelined"] == expect, (k, ctx.last_stats())
+        To, _, _ = oest.register_scan(host[k])
+        assert np.abs(ctx.current_pose() - To).max() < 1e-6, k
