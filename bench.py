@@ -57,6 +57,17 @@ def parse():
     ap.add_argument("--c5-steps", type=int, default=5, help="sharded C5 registrations timed beside the C4 line")
     ap.add_argument("--c5-warmup", type=int, default=1)
     ap.add_argument("--no-c5", action="store_true", help="skip the sharded C5 measurement beside the C4 line")
+    ap.add_argument("--sub-workloads", default="c2,c3",
+                    help="other scan configs timed beside the headline (BASELINE configs 2 and 3), each with "
+                         "prefill, roofline and a CPU-baseline sample; '' = skip")
+    ap.add_argument("--rehearse-ranks", action="store_true",
+                    help="TEST ONLY (tests/test_gpu_bench_ranks.py): run the --gpus N orchestration on a box with "
+                         "fewer GPUs — every rank on cuda:0, gloo for the control collectives, the C5 exchange "
+                         "as a host all-reduce in place of the RCCL communicator (RCCL refuses two ranks on one "
+                         "GPU).  Prints a rehearsal record, never a driver line.")
+    ap.add_argument("--no-host-input", action="store_true",
+                    help="skip the host_input block (the same stream fed from host memory, as the reference's "
+                         "std::vector<PointXYZf> boundary passes it)")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--profile-steps", type=int, default=None,
                     help="extra steps, after the timed ones, with per-kernel HIP-event timing (roofline); "
@@ -97,10 +108,13 @@ def spawn_ranks(n):
     sys.exit(subprocess.call(cmd))
 
 
-def dist_setup(n):
+_CTRL = {"gloo": False}  # rehearsal: the control collectives run on gloo (CPU tensors)
+
+
+def dist_setup(n, rehearse=False):
     if "WORLD_SIZE" not in os.environ:
         ndev = torch.cuda.device_count()
-        if n > ndev:
+        if n > ndev and not rehearse:
             print(f"bench.py: --gpus {n} but {ndev} HIP device(s) visible", file=sys.stderr)
             sys.exit(2)
         if n > 1:
@@ -111,10 +125,16 @@ def dist_setup(n):
     if world != n:
         print(f"bench.py: --gpus {n} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
+    if rehearse:
+        local = 0  # every rank on the one GPU
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+            _CTRL["gloo"] = True
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return rank, world, local
 
 
@@ -124,38 +144,42 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(x, world, local):
+def _over_ranks(x, world, local, op):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if _CTRL["gloo"] else f"cuda:{local}")
+    dist.all_reduce(t, op=op)
     return float(t.item())
+
+
+def max_over_ranks(x, world, local):
+    import torch.distributed as dist
+    return _over_ranks(x, world, local, dist.ReduceOp.MAX)
 
 
 def sum_over_ranks(x, world, local):
-    if world == 1:
-        return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _over_ranks(x, world, local, dist.ReduceOp.SUM)
 
 
-def pmc_traffic(a, name, workload=None):
+def pmc_traffic(a, name, workload=None, with_source=False):
     """HBM bytes per launch of kernel class `name` from the committed PMC summary of this
-    workload (tools/gpu_pmc.sh, tools/gpu_c5pmc.sh), or None."""
+    workload (tools/gpu_pmc.sh, tools/gpu_c5pmc.sh), or None; with_source: also
+    {file, measured_at (the commit of the measured code, tools/tag_profile.py)}."""
     workload = workload or a.workload
     path = (a.traffic_json if workload == a.workload else None) or os.path.join(
         ROOT, "profiles", "traffic_latest.json" if workload == "c4" else f"traffic_{workload}.json")
+    val, src = None, None
     try:
         with open(path) as f:
             tj = json.load(f)
         if tj.get("workload") == workload and name in tj.get("kernels", {}):
-            return tj["kernels"][name]["hbm_bytes_per_launch"]
+            val = tj["kernels"][name]["hbm_bytes_per_launch"]
+            src = {"file": os.path.relpath(path, ROOT), "measured_at": tj.get("measured_at")}
     except (OSError, ValueError, KeyError):
         pass
-    return None
+    return (val, src) if with_source else val
 
 
 def pin_thread(world, local):
@@ -248,6 +272,65 @@ def register(ctx, scans, k, pipeline):
     ctx.register_scan(scans[k])
 
 
+def host_input_block(a, new_ctx, dscans, single, start, steps):
+    """The headline stream fed from HOST memory, as the reference's boundary takes it
+    (form.hpp:82-83: a host std::vector<PointXYZf>, filled per measurement by
+    bindings.cpp:150-159): (a) pageable arrays — staged into pinned memory by libfmx's
+    helper threads and DMA'd, sequential and pipelined (fmx_next_scan of the host array);
+    (b) the caller assembling each scan in an fmx_scan_buffer (pinned; the assembly copy
+    is inside the timed region), sequential and pipelined.  Same scans and prefill as the
+    headline; the raw 4-MiB H2D copy times are reported beside."""
+    hscans = [s.cpu().numpy().copy() for s in dscans[: start + steps + 1]]
+    out = {}
+    for mode in ("pageable_sequential", "pageable_pipelined", "pinned_sequential", "pinned_pipelined"):
+        ctx = new_ctx(single)
+        pipe = mode.endswith("pipelined")
+        pinned = mode.startswith("pinned")
+        bufs = {}
+
+        def get(k):
+            if not pinned:
+                return hscans[k]
+            if k not in bufs:  # the caller's assembly of scan k, straight into pinned memory
+                b = ctx.scan_buffer()
+                np.copyto(b, hscans[k])
+                bufs[k] = b
+            return bufs[k]
+        for k in range(start - 1):  # prefill from the device copies
+            register(ctx, dscans[: start - 1], k, True)
+        if pipe:  # as in the headline, the first timed scan's extraction runs before the timed region
+            ctx.next_scan(get(start))
+        ctx.register_scan(dscans[start - 1])
+        ctx.sync()
+        t0 = time.perf_counter()
+        for k in range(start, start + steps):
+            if pipe:
+                ctx.next_scan(get(k + 1))
+            ctx.register_scan(get(k))
+            bufs.pop(k - 1, None)
+        ctx.sync()
+        dt = time.perf_counter() - t0
+        out[mode] = {"scans_per_s": round(steps / dt, 3), "ms_per_step": round(dt / steps * 1e3, 3),
+                     "pipelined_scans": ctx.last_stats()["pipelined"]}
+        ctx.close()
+    # raw copies of one scan (median of 10): what the staging has to hide
+    dst = torch.empty_like(dscans[0])
+    pin = torch.empty(dscans[0].shape, dtype=torch.float32).pin_memory()
+    times = {}
+    for name, fn in (("pageable_h2d_us", lambda h: dst.copy_(torch.from_numpy(h))),
+                     ("pinned_h2d_us", lambda h: dst.copy_(pin, non_blocking=True))):
+        ts = []
+        for k in range(12):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn(hscans[k])
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        times[name] = round(float(np.median(ts[2:])) * 1e6, 1)
+    out["copy_per_scan"] = {**times, "bytes": int(hscans[0].nbytes)}
+    return out
+
+
 def concurrent_streams(S, new_ctx, scans, start, steps, pipeline, single, aff):
     """S independent estimators on this GPU, each registering the same scans [start,
     start + steps) from its own host thread (ctypes drops the GIL inside each fmx
@@ -315,7 +398,9 @@ def c5_setup(a, rank, world, local):
     n_map = pos4.shape[0]
     prm = fmx.EstimatorParams(keypoint_pool_capacity=n_map + 1024, voxel_subdivision=a.subdiv or 1)
     ctx = fmx.Context(prm, device=local)
-    if world > 1:  # RCCL communicator of the exchange step (fmx_comm_init)
+    if world > 1 and a.rehearse_ranks:
+        pass  # rehearsal: the exchange is a host all-reduce (c5_register), no communicator
+    elif world > 1:  # RCCL communicator of the exchange step (fmx_comm_init)
         import torch.distributed as dist
         uid = [fmx.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -350,6 +435,24 @@ def c5_queries(a, dist_name, pos4, nrm4, rank, world):
     return q4[b:e].contiguous(), n4[b:e].contiguous(), Ttrue
 
 
+def c5_register_host_exchange(ctx, w, max_iters=30, thr=1e-4):
+    """Rehearsal only: the same ICP loop driven from Python, the shard systems summed by a
+    host all-reduce (gloo) instead of libfmx's RCCL exchange."""
+    from form_amd import shard
+    T = np.hstack([np.eye(3), np.zeros((3, 1))])
+    it = 0
+    while it < max_iters:
+        ctx.match(T, w, counts=False)
+        S, e = ctx.linearize_matched(T, 0.1)
+        S = shard.allreduce_sum(np.append(S, e))[:28]
+        dx = shard.gauss_newton_step(S)
+        T = shard.compose(T, shard.expmap(dx))
+        it += 1
+        if np.linalg.norm(dx) < thr:
+            break
+    return T, it
+
+
 def c5_register(ctx, w, max_iters=30, thr=1e-4):
     """One registration of the 2M-point scan: ICP iterations of match
     (this rank's shard) -> the shard's single-pose 7x7 normal equations, all-reduced
@@ -364,14 +467,15 @@ def c5_register(ctx, w, max_iters=30, thr=1e-4):
 def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmup, profile):
     """Time `steps` registrations of the current query set (max over ranks)."""
     from form_amd import shard
+    reg = c5_register_host_exchange if (world > 1 and a.rehearse_ranks) else c5_register
     for _ in range(warmup):
-        T, iters = c5_register(ctx, w)
+        T, iters = reg(ctx, w)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     it_total = 0
     for _ in range(steps):
-        T, iters = c5_register(ctx, w)
+        T, iters = reg(ctx, w)
         it_total += iters
     torch.cuda.synchronize()
     barrier(world)
@@ -382,7 +486,7 @@ def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmu
         ctx.profile(True)
         ctx.profile_reset()
         for _ in range(nprof):
-            c5_register(ctx, w)
+            reg(ctx, w)
         ctx.sync()
         prof = ctx.profile_read()
         work = ctx.match_work()
@@ -409,6 +513,7 @@ def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmu
                    "rccl_communicator": world > 1 or bool(a.c5_comm)},
         "pose_error": {"initial_m": round(e0t, 6), "initial_rad": round(e0r, 8), "final_m": round(et, 6),
                        "final_rad": round(er, 8)},
+        "pose": np.asarray(T).reshape(-1).tolist(),
     }
     if prof:
         name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
@@ -437,6 +542,81 @@ def run_c5(a, rank, world, local, steps, warmup, profile=True, dists=("local", "
     return out if rank == 0 else None
 
 
+def sub_stream_line(a, wl, rank, world, local, single, pipe):
+    """Another BASELINE scan config (c2: 64x1024 OS1-64, c3: 64x2048 HDL-64E stand-in with
+    8 % dropouts) timed like the headline: prefill to the steady state, warmup, `steps`
+    timed register_scans (max over ranks), then a profiled pass for the roofline and
+    the per-scan counters.  Returns (line or None on ranks > 0, host copies of the
+    first scans for the CPU baseline)."""
+    dev = f"cuda:{local}"
+    geo = synth.GEOMETRIES[wl]
+    params = synth.default_params(geo)
+    n_pts = geo.rows * geo.cols
+    pre, steps, warmup = a.prefill, a.steps, a.warmup
+    psteps = max(steps // 2, 5)
+    total = pre + warmup + steps + psteps
+    world_obj = synth.World()
+    k0 = 1000 * rank
+    scans = [synth.raycast(world_obj, synth.trajectory_pose(k0 + k), geo, synth.SEED + 7919 * (k0 + k + 1), dev)
+             for k in range(total)]
+    torch.cuda.synchronize()
+    ctx = fmx.Context(fmx.EstimatorParams(extraction=fmx.KeypointExtractionParams(**params),
+                                          voxel_subdivision=a.subdiv or 0, disable_smoothing=single), device=local)
+    for k in range(pre + warmup):
+        register(ctx, scans, k, pipe)
+    ctx.sync()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(pre + warmup, pre + warmup + steps):
+        register(ctx, scans, k, pipe)
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier(world)
+    t_local = time.perf_counter() - t0
+    ctx.profile(True)
+    ctx.profile_reset()
+    stats = []
+    for k in range(pre + warmup + steps, total):
+        register(ctx, scans, k, pipe)
+        stats.append(ctx.last_stats())
+    ctx.sync()
+    prof = ctx.profile_read()
+    work = ctx.match_work()
+    ctx.close()
+    t_max = max_over_ranks(t_local, world, local)
+    scans_total = sum_over_ranks(float(steps), world, local)
+    host = [s.cpu().numpy() for s in scans[:40]] if rank == 0 and world == 1 else None
+    del scans
+    if rank != 0:
+        return None, None
+    value = scans_total / t_max
+    ms = t_max / steps * 1e3
+    name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    kern_ms = {k: round(v["ms"] / psteps, 4) for k, v in prof.items() if v["ms"] > 0}
+    side = {"map_build"} | ({"extract_rows", "closest", "fit", "compact"} if pipe else set())
+    main_ms = sum(v for k, v in kern_ms.items() if k not in side)
+    st_mean = {k: float(np.mean([s_[k] for s_ in stats])) for k in stats[0]}
+    line = {
+        "metric": f"scans/sec + Mpts/sec scan-to-submap ICP ({wl}: {geo.rows}-beam)", "value": round(value, 3),
+        "unit": "scans/s", "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "scaling": "weak",
+        "config": {"workload": f"{wl}: {geo.rows}x{geo.cols} organized scan stream ({n_pts} pts/scan, "
+                               f"{geo.dropout:.0%} dropouts), register_scan, "
+                               f"{'single-pose ablation' if single else 'smoothing mode (ConstraintManager default)'}",
+                   "points_per_scan": n_pts, "prefill": pre, "timed_scans": [pre + warmup, pre + warmup + steps],
+                   "pipelined_extraction": pipe, "parallelism": f"replicas x{world}"},
+        "mpts_per_s": round(value * n_pts / 1e6, 3),
+        "roofline": roofline(a, name, d, wl),
+        "kernels_ms_per_step": kern_ms,
+        "main_stream_busy_frac": round(min(main_ms / ms, 1.0), 4),
+        "host_round_trips_per_scan": round(st_mean.get("host_waits", 0.0), 2),
+        "counters": st_mean,
+        "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
+    }
+    return line, (host, params, k0)
+
+
 def roofline(a, name, d, workload):
     """The roofline block of the dominant kernel class `name` (profile entry d): the §8(d)
     algorithmic bytes per launch over the HIP-event average launch time (frac), and the
@@ -445,10 +625,12 @@ def roofline(a, name, d, workload):
     avg_ms = d["ms"] / max(d["launches"], 1)
     bytes_per = d["bytes"] / max(d["launches"], 1)
     achieved = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = pmc_traffic(a, name, workload)
+    traffic, tsrc = pmc_traffic(a, name, workload, with_source=True)
     roof = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, avg_launch_us=round(avg_ms * 1e3, 3),
                 alg_bytes_per_launch=bytes_per)
+    if tsrc:
+        roof["traffic_source"] = tsrc
     if traffic and avg_ms > 0:
         hbm = traffic / (avg_ms * 1e-3) / 1e9
         roof["hbm_achieved"] = round(hbm, 3)
@@ -463,15 +645,29 @@ def roofline(a, name, d, workload):
         roof["wave_cycles"] = dict(valu_active=round(c["SQ_ACTIVE_INST_VALU"] / wc, 3),
                                    memory_wait=round(c["SQ_WAIT_ANY"] / wc, 3),
                                    issue_wait=round(c["SQ_WAIT_INST_ANY"] / wc, 3),
-                                   source=os.path.relpath(sq, ROOT))
+                                   source=os.path.relpath(sq, ROOT),
+                                   measured_at=json.load(open(sq)).get("measured_at"))
     except (OSError, KeyError, ValueError):
         pass
     return roof
 
 
+def rehearsal_record(out, a, world):
+    """--rehearse-ranks: what the N-rank path produced, marked so no driver takes it for
+    a measurement (the ranks shared one GPU)."""
+    keep = {k: out[k] for k in ("n_gpus", "steps", "warmup", "scaling") if k in out}
+    rec = {"rehearsal": True, "metric": "rehearsal of the --gpus N orchestration on one GPU (not a measurement)",
+           "value": None, "ranks": world, **keep, "c4_scans_per_s_all_ranks": out.get("value")}
+    for k in ("sharded_c5", "sharded_c5_wholemap"):
+        if k in out:
+            rec[k] = {"pose": out[k]["pose"], "icp_iters_per_registration": out[k]["icp_iters_per_registration"],
+                      "registrations_per_s": out[k]["value"]}
+    return rec
+
+
 def main():
     a = parse()
-    rank, world, local = dist_setup(a.gpus)
+    rank, world, local = dist_setup(a.gpus, a.rehearse_ranks)
     if a.workload == "c5":
         torch.cuda.set_device(local)
         dists = ("local", "wholemap") if a.c5_dist == "both" else (a.c5_dist,)
@@ -480,6 +676,8 @@ def main():
             out = res[dists[0]]
             if len(dists) > 1:
                 out["wholemap"] = res["wholemap"]
+            if a.rehearse_ranks:
+                out = {"rehearsal": True, "value": None, "ranks": world, "sharded_c5": {"pose": out["pose"]}}
             print(json.dumps(out), flush=True)
         if world > 1:
             import torch.distributed as dist
@@ -558,12 +756,21 @@ def main():
     multi = {}
     for S in ([int(x) for x in a.streams.split(",") if x.strip()] if world == 1 else []):  # a per-GPU figure
         multi[str(S)] = concurrent_streams(S, new_ctx, scans, pre + a.warmup, a.steps, pipe, single, prev_aff)
+    host_in = None
+    if world == 1 and not a.no_host_input:
+        host_in = host_input_block(a, new_ctx, scans, single, pre + a.warmup, a.steps)
     t_max = max_over_ranks(t_local, world, local)
     scans_total = sum_over_ranks(float(a.steps), world, local)
     # the sharded C5 registration beside the replica line: every rank takes part
     c5 = None
-    if not a.no_c5:
-        c5 = run_c5(a, rank, world, local, a.c5_steps, a.c5_warmup, profile=False)
+    if not a.no_c5:  # each C5 line ends with a short profiled pass (its roofline block)
+        c5 = run_c5(a, rank, world, local, a.c5_steps, a.c5_warmup, profile=True)
+    # BASELINE's other scan configs beside the headline (every rank takes part)
+    subs = {}
+    host = [s_.cpu().numpy() for s_ in scans[: min(total, 60)]] if not a.no_cpu_baseline and world == 1 else None
+    del scans
+    for wl in [w_.strip() for w_ in a.sub_workloads.split(",") if w_.strip() and w_.strip() != a.workload]:
+        subs[wl] = sub_stream_line(a, wl, rank, world, local, single, pipe)
     if rank == 0 and c5 is not None:
         c5_whole = c5["wholemap"]
         c5 = c5["local"]
@@ -628,24 +835,42 @@ def main():
         out["ablation"] = ablation
     if sequential is not None:
         out["sequential_extraction"] = sequential
+    if host_in is not None:
+        out["host_input"] = host_in
+        out["host_input"]["vs_device"] = {
+            "pipelined": round(host_in["pageable_pipelined"]["scans_per_s"] / value, 4),
+            "sequential": round(host_in["pageable_sequential"]["scans_per_s"] / sequential["scans_per_s"], 4)
+            if sequential else None,
+            "pinned_pipelined": round(host_in["pinned_pipelined"]["scans_per_s"] / value, 4),
+            "pinned_sequential": round(host_in["pinned_sequential"]["scans_per_s"] / sequential["scans_per_s"], 4)
+            if sequential else None}
     if c5 is not None:
         out["sharded_c5"] = c5
         out["sharded_c5_wholemap"] = c5_whole
     cp = os.path.join(ROOT, "profiles", f"critical_path_{a.workload}.json")
-    if os.path.exists(cp):
+    if os.path.exists(cp):  # a committed rocprofv3-trace figure, not measured by this run
         with open(cp) as f:
             out["critical_path_trace"] = json.load(f)
+        out["critical_path_trace"]["source"] = os.path.relpath(cp, ROOT)
     if prev_aff is not None:
         os.sched_setaffinity(0, prev_aff)  # the CPU baseline's threads use every host core
-    if not a.no_cpu_baseline and world == 1:
-        host = [s.cpu().numpy() for s in scans[: min(total, 60)]]
-        del scans
+    if host is not None:
         out["cpu_baseline"], opos = cpu_baseline(host, params, a.cpu_sample_s, single, cpu_threads())
         # one thread over the same scans: the pool's scaling (and a per-core figure)
         one, _ = cpu_baseline(host[:12], params, a.cpu_sample_s / 2, single, 1)
         out["cpu_baseline"]["single_thread"] = {"value": one["value"], "ms_per_scan": one["ms_per_scan"],
                                                 "sample": one["sample"]}
         out["ate"] = ate_block(host, opos, params, k0, local, single, pipe)
+    for wl, (line, cpu_in) in subs.items():
+        if line is None:
+            continue
+        if cpu_in is not None and cpu_in[0] is not None and not a.no_cpu_baseline:
+            sh, sp, sk0 = cpu_in
+            line["cpu_baseline"], sop = cpu_baseline(sh, sp, a.cpu_sample_s / 3, single, cpu_threads())
+            line["ate"] = ate_block(sh, sop, sp, sk0, local, single, pipe)
+        out[wl] = line
+    if a.rehearse_ranks:
+        out = rehearsal_record(out, a, world)
     print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -1271,6 +1271,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[10] = c->spec_hits - hits0;
   c->stats[11] = map_spec_used ? 1 : 0;
   c->stats[12] = c->pf_used - pf0;
+  c->stats[13] = e.values.size();
   if (out) *out = fc;
 }
 

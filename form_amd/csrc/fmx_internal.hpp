@@ -265,7 +265,7 @@ struct ExLaunch {
 
 }  // namespace fmx
 
-constexpr int kStatsN = 13;  // fmx_last_stats entries
+constexpr int kStatsN = 14;  // fmx_last_stats entries
 
 struct fmx_ctx {
   fmx_params P{};

@@ -390,7 +390,7 @@ class Context:
     def last_stats(self) -> dict:
         keys = ["icp_iters", "lm_iters", "matched_planar", "matched_point", "map_planar", "map_point",
                 "linearizations", "map_scans", "host_waits", "spec_matches", "spec_hits", "spec_map",
-                "pipelined"]
+                "pipelined", "window_poses"]
         s = np.zeros(len(keys), np.uint64)
         self._chk(self._L.fmx_last_stats(self.h, _p(s), C.c_int(len(keys))))
         return {k: int(v) for k, v in zip(keys, s)}
@@ -625,8 +625,11 @@ class FORM:
         if self._est is None:
             raise RuntimeError("FORM.add_lidar before initialize()")
         xyz = _points_xyz(mm)
-        scan = np.zeros((len(xyz), 4), np.float32)
-        scan[:, :3] = xyz.astype(np.float32)  # point_to_form: PointXYZf(x, y, z), bindings.cpp:43-45
+        # point_to_form: PointXYZf(x, y, z) (bindings.cpp:43-45), assembled straight into
+        # a pinned fmx_scan_buffer: the registration then DMAs it with no staging copy
+        scan = self._est.scan_buffer(len(xyz))
+        scan[:, :3] = xyz
+        scan[:, 3] = 0.0
         self._est.register_scan(scan)
         self._scan += 1
         self._pose = _pose44(self._est.current_pose()) @ self.lidar_T_imu

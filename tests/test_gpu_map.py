@@ -184,3 +184,82 @@ def test_repeated_builds_epoch_wrap(fmx_mod, oracle):
             assert np.array_equal(pair >= 0, acc), b
             assert np.array_equal(np.asarray(ids, np.uint64)[pair[acc]], ref["scan"][acc]), b
             assert np.array_equal(got["d2"][sl][acc], ref["d2"][acc]), b
+
+
+def test_dense_cells_warm_from_cell_cache(fmx_mod, oracle):
+    """The dense-cell fixture above matched at several poses on ONE map and query set:
+    every match after the first is warm (bounded by the previous NN record, the own cell
+    — range and dense bit — from the per-query cell cache, no brick probe).  Each match
+    is bit-exact to the oracle; the fixture puts thousands of queries in dense own cells;
+    and the warm match probes at least half a brick fewer per query than a cold match
+    at the same pose (the cache is hit)."""
+    rng = np.random.default_rng(11)
+    w = 0.8
+    scans, poses = [], []
+    for k in range(6):
+        c = rng.uniform(-0.8, 0.8, (2500, 3))
+        flat = np.c_[rng.uniform(2, 6, 1500), rng.uniform(-1, 1, 1500), rng.normal(0, 0.01, 1500) - 1.5]
+        pl = np.vstack([c, flat])
+        if k == 2:
+            pl = np.vstack([pl, np.c_[rng.uniform(3.25, 3.95, 9000), rng.uniform(4.05, 4.75, (9000, 2))]])
+        pt = rng.uniform(-0.8, 0.8, (600, 3))
+        T = I34.copy()
+        T[:, 3] = rng.normal(0, 0.01, 3)
+        poses.append(T)
+        scans.append((_planar(pl, rng), np.asarray(pt, np.float32)))
+    qpl = _planar(np.vstack([rng.uniform(-1.2, 1.2, (3000, 3)),
+                             np.c_[rng.uniform(2, 6, 1000), rng.uniform(-1, 1, 1000), np.full(1000, -1.45)],
+                             np.c_[rng.uniform(3.1, 4.1, 1000), rng.uniform(3.9, 4.9, (1000, 2))]]), rng)
+    qpt = np.asarray(rng.uniform(-1.2, 1.2, (1500, 3)), np.float32)
+    ctx = _ctx(fmx_mod)
+    for k, (pl, pt) in enumerate(scans):
+        ctx.keypoints_add(k, pl, pt)
+    omaps = [oracle.VoxelMap(w, 0), oracle.VoxelMap(w, 1)]
+    for k, (pl, pt) in enumerate(scans):
+        omaps[0].add_scan(k, poses[k], pl)
+        omaps[1].add_scan(k, poses[k], pt)
+    ctx.map_build(list(range(len(scans))), np.stack(poses), w)
+    # queries whose own cell is dense (> 128 records) in the world map
+    wp = np.vstack([pl[:, :3].astype(np.float64) @ poses[k][:, :3].T + poses[k][:, 3]
+                    for k, (pl, _) in enumerate(scans)])
+    cells, cnt = np.unique(np.floor(wp / w).astype(np.int64), axis=0, return_counts=True)
+    dense = {tuple(c) for c in cells[cnt > 128]}
+    assert sum(tuple(c) in dense for c in np.floor(qpl[:, :3].astype(np.float64) / w).astype(np.int64)) > 3000
+
+    def match_cmp(Tj):
+        cpl, cpt = ctx.match(Tj, w)
+        got = ctx.match_download()
+        npl = len(qpl)
+        for t, (om, Q) in enumerate(zip(omaps, (qpl, qpt))):
+            ref = om.match(Q, Tj)
+            sl = slice(0, npl) if t == 0 else slice(npl, None)
+            acc = ref["found"] & (ref["d2"] < w * w)
+            pair = got["pair"][sl]
+            assert np.array_equal(pair >= 0, acc)
+            assert np.array_equal(pair[acc].astype(np.uint64), ref["scan"][acc])
+            assert np.array_equal(got["d2"][sl][acc], ref["d2"][acc])
+            assert np.array_equal(got["pi"][sl][acc], ref["pi"][acc])
+            if t == 0:
+                assert np.array_equal(got["ni"][acc], ref["ni"][acc])
+            assert np.array_equal(got["d2"][sl] > 0.01, ~ref["found"] | (ref["d2"] > 0.01))
+        return ctx.match_work()
+
+    ctx.profile(True)
+    ctx.set_queries(qpl, qpt, 6)
+    steps = [(0.003, -0.002, 0.001), (0.0031, -0.0021, 0.0012), (0.0031, -0.0021, 0.00121), (0.05, 0.04, -0.03),
+             (0.0031, -0.0021, 0.00121)]
+    warm = None
+    for i, tr in enumerate(steps):
+        Tj = I34.copy()
+        Tj[:, 3] = tr
+        wk = match_cmp(Tj)
+        if i == 2:
+            warm = wk
+    nq = len(qpl) + len(qpt)
+    ctx.set_queries(qpl, qpt, 6)  # same features, new query set: a cold match
+    Tj = I34.copy()
+    Tj[:, 3] = steps[2]
+    cold = match_cmp(Tj)
+    ctx.profile(False)
+    assert warm["probes"] < cold["probes"] - 0.5 * nq, (warm, cold, nq)
+    assert warm["candidates"] <= cold["candidates"], (warm, cold)

@@ -124,6 +124,38 @@ def test_match_matches_oracle(fmx_mod, oracle, config, subdiv, rot, trans):
         assert np.array_equal((cpl if t == 0 else cpt), counts)
 
 
+def _warm_build(ctx, oracle, feats, scans, w):
+    scans = list(scans)
+    omaps = [oracle.VoxelMap(w, 0), oracle.VoxelMap(w, 1)]
+    for k in scans:
+        omaps[0].add_scan(k, feats[k]["pose"], feats[k]["planar"])
+        omaps[1].add_scan(k, feats[k]["pose"], feats[k]["point"])
+    ctx.map_build(scans, np.stack([feats[k]["pose"] for k in scans]), w)
+    return omaps, np.array(scans, np.uint64)
+
+
+def _warm_check(ctx, built, q, Tj, w):
+    """fmx_match at Tj bit-exact to the oracle (pairs, d^2, p_i, n_i, inserts, counts)."""
+    omaps, scan_of = built  # pair index -> scan id
+    cpl, cpt = ctx.match(Tj, w)
+    got = ctx.match_download()
+    npl = len(q["planar"])
+    for t, (om, Q) in enumerate(zip(omaps, (q["planar"], q["point"]))):
+        ref = om.match(Q, Tj)
+        sl = slice(0, npl) if t == 0 else slice(npl, None)
+        acc_ref = ref["found"] & (ref["d2"] < w * w)
+        pair = got["pair"][sl]
+        assert np.array_equal(pair >= 0, acc_ref)
+        assert np.array_equal(scan_of[pair[acc_ref]], ref["scan"][acc_ref])
+        assert np.array_equal(got["d2"][sl][acc_ref], ref["d2"][acc_ref])
+        assert np.array_equal(got["pi"][sl][acc_ref], ref["pi"][acc_ref])
+        if t == 0:
+            assert np.array_equal(got["ni"][acc_ref], ref["ni"][acc_ref])
+        assert np.array_equal(got["d2"][sl] > 0.01, ~ref["found"] | (ref["d2"] > 0.01))
+        idx = np.searchsorted(scan_of, ref["scan"][acc_ref])  # (scan lists ascending)
+        assert np.array_equal(cpl if t == 0 else cpt, np.bincount(idx, minlength=len(scan_of)))
+
+
 @pytest.mark.parametrize("config,subdiv", [("c2", 1), ("c2", 2), ("c3", 1)])
 def test_warm_matches_match_oracle(fmx_mod, oracle, config, subdiv):
     """Matches after the first on the same map and query set start warm: each search is
@@ -139,49 +171,56 @@ def test_warm_matches_match_oracle(fmx_mod, oracle, config, subdiv):
     w = 0.8
     for k in range(6):
         ctx.keypoints_add(k, feats[k]["planar"], feats[k]["point"])
-
-    def build(scans):
-        scans = list(scans)
-        omaps = [oracle.VoxelMap(w, 0), oracle.VoxelMap(w, 1)]
-        for k in scans:
-            omaps[0].add_scan(k, feats[k]["pose"], feats[k]["planar"])
-            omaps[1].add_scan(k, feats[k]["pose"], feats[k]["point"])
-        ctx.map_build(scans, np.stack([feats[k]["pose"] for k in scans]), w)
-        return omaps, np.array(scans, np.uint64)
-
-    def check(built, q, Tj):
-        omaps, scan_of = built  # pair index -> scan id
-        cpl, cpt = ctx.match(Tj, w)
-        got = ctx.match_download()
-        npl = len(q["planar"])
-        for t, (om, Q) in enumerate(zip(omaps, (q["planar"], q["point"]))):
-            ref = om.match(Q, Tj)
-            sl = slice(0, npl) if t == 0 else slice(npl, None)
-            acc_ref = ref["found"] & (ref["d2"] < w * w)
-            pair = got["pair"][sl]
-            assert np.array_equal(pair >= 0, acc_ref)
-            assert np.array_equal(scan_of[pair[acc_ref]], ref["scan"][acc_ref])
-            assert np.array_equal(got["d2"][sl][acc_ref], ref["d2"][acc_ref])
-            assert np.array_equal(got["pi"][sl][acc_ref], ref["pi"][acc_ref])
-            if t == 0:
-                assert np.array_equal(got["ni"][acc_ref], ref["ni"][acc_ref])
-            assert np.array_equal(got["d2"][sl] > 0.01, ~ref["found"] | (ref["d2"] > 0.01))
-            idx = np.searchsorted(scan_of, ref["scan"][acc_ref])  # (scan lists ascending)
-            assert np.array_equal(cpl if t == 0 else cpt, np.bincount(idx, minlength=len(scan_of)))
-
     rng = np.random.default_rng(11)
-    built = build(range(5))
+    built = _warm_build(ctx, oracle, feats, range(5), w)
     q = feats[5]
     ctx.set_queries(q["planar"], q["point"], 5)
     for rot, trans in [(0.02, 0.35), (0.005, 0.03), (0.001, 0.004), (0.0, 0.0), (0.02, 0.35), (0.03, 0.5)]:
-        check(built, q, perturb(q["pose"], rng, rot, trans) if rot else q["pose"])
-    built = build([1, 3, 4])  # a new map: the warm state of the old one must not be used
+        _warm_check(ctx, built, q, perturb(q["pose"], rng, rot, trans) if rot else q["pose"], w)
+    built = _warm_build(ctx, oracle, feats, [1, 3, 4], w)  # a new map: the old one's warm state must not be used
     for rot, trans in [(0.005, 0.03), (0.001, 0.004)]:
-        check(built, q, perturb(q["pose"], rng, rot, trans))
+        _warm_check(ctx, built, q, perturb(q["pose"], rng, rot, trans), w)
     q = feats[6]  # a new query set
     ctx.set_queries(q["planar"], q["point"], 6)
     for rot, trans in [(0.005, 0.03), (0.02, 0.35)]:
-        check(built, q, perturb(q["pose"], rng, rot, trans))
+        _warm_check(ctx, built, q, perturb(q["pose"], rng, rot, trans), w)
+
+
+def test_warm_matches_c4_icp_sequence(fmx_mod, oracle):
+    """C4 (128 x 2048), where the map holds dense cells (> 128 records per 0.8 m cell:
+    the DENSE k_match variant, sub-cell headers) and every ICP iteration after a scan's
+    first match starts warm: an ICP-like pose sequence — an initial error of ~0.6 deg /
+    10 cm, then steps that shrink it ~4x per iteration down to the 1e-4 break threshold
+    (form.cpp:83-88) — every match bit-exact to the oracle per query; then a rebuilt map
+    (warm state dropped) and two more steps."""
+    feats = stream_features(oracle, "c4", 6)
+    p = feats[0]["params"]
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(extraction=fmx_mod.KeypointExtractionParams(**p)))
+    w = 0.8
+    for k in range(5):
+        ctx.keypoints_add(k, feats[k]["planar"], feats[k]["point"])
+    built = _warm_build(ctx, oracle, feats, range(5), w)
+    # the map holds dense cells, and queries whose own cell is one
+    wp = np.vstack([feats[k]["planar"][:, :3].astype(np.float64) @ feats[k]["pose"][:, :3].T + feats[k]["pose"][:, 3]
+                    for k in range(5)])
+    cells, cnt = np.unique(np.floor(wp / w).astype(np.int64), axis=0, return_counts=True)
+    dense = {tuple(c) for c in cells[cnt > 128]}
+    assert len(dense) > 10
+    q = feats[5]
+    qw = q["planar"][:, :3].astype(np.float64) @ q["pose"][:, :3].T + q["pose"][:, 3]
+    in_dense = sum(tuple(c) in dense for c in np.floor(qw / w).astype(np.int64))
+    assert in_dense > 1000, in_dense
+    ctx.set_queries(q["planar"], q["point"], 5)
+    rng = np.random.default_rng(23)
+    T = perturb(q["pose"], rng, 0.01, 0.1)
+    scale = 1.0
+    for it in range(8):
+        _warm_check(ctx, built, q, T, w)
+        scale *= 0.25
+        T = perturb(q["pose"], rng, 0.01 * scale, 0.1 * scale)
+    built = _warm_build(ctx, oracle, feats, [0, 2, 3, 4], w)
+    for rot, trans in [(0.002, 0.02), (0.0005, 0.005)]:
+        _warm_check(ctx, built, q, perturb(q["pose"], rng, rot, trans), w)
 
 
 def test_match_large_query_set_matches_oracle(fmx_mod, oracle):

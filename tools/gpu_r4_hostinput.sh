@@ -11,3 +11,5 @@ for v in "FMX_STAGE_THREADS=0" "FMX_STAGE_THREADS=7" "FMX_STAGE_DMAS=1" "FMX_STA
   env $v timeout -k 10 400 python -u tools/host_input_probe.py --modes device_sequential,host_sequential,host_pipelined > gpurun_out/r4/probe_v.json 2> gpurun_out/r4/probe.err || { tail -20 gpurun_out/r4/probe.err; exit 1; }
   cat gpurun_out/r4/probe_v.json
 done
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gpu_seam.py > gpurun_out/r4/t3.log 2>&1 || { tail -30 gpurun_out/r4/t3.log; exit 1; }
+tail -2 gpurun_out/r4/t3.log
