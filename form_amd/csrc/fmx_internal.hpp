@@ -153,7 +153,18 @@ struct VoxMap {
   DBuf<uint2> rinfo;            // per build-order record: cell, rank in the cell
   DBuf<uint32_t> claim, dense;  // claimed bricks, dense cells of the last build
   DBuf<double4> pos, nrm;       // grouped by cell
+  uint32_t rsh = 5;             // record stride 1 << rsh bytes: 5 = pos / nrm arrays, 6 = interleaved in pos
+  double4* nrm_p = nullptr;     // normals: nrm.p, or pos.p + 1 when interleaved
 };
+// Maps of at least this many records interleave positions and normals (voxelmap.hip,
+// rec_at); FMX_INTERLEAVE_MIN overrides (A/B), 0 = always.
+inline uint32_t interleave_min() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("FMX_INTERLEAVE_MIN");
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)(4u << 20);
+  }();
+  return v;
+}
 
 struct Seg {
   uint32_t off;       // first build-order record
@@ -366,6 +377,8 @@ struct fmx_ctx {
   uint64_t warm_gen = 1;      // bumped by every map build and query-set change
   uint64_t warm_rec_gen = 0;  // warm_gen when m_rec was last written (0: never)
   fmx::DBuf<uint32_t> thist;  // tiled pair sort: per-(type, pair, tile) counts, self-resetting
+  fmx::DBuf<float> cert_b2;   // FMX_CERT_DIAG builds: per query the last match's second-best bound
+  double cert_pose[12] = {};  // ... and that match's pose
   bool have_match = false;
 
   // ---- sorted correspondences (pair-major SoA) + chunk table
@@ -484,6 +497,7 @@ struct MatchDiag {
   double span = 0, p50 = 0, p90 = 0, p99 = 0, pmax = 0, f50 = 0, f90 = 0, f99 = 0, mq_all = 0, mq_slow = 0;
   uint64_t mq_hist[8] = {0};
   double walk_rounds = 0, walk_steps = 0, walk_listed = 0, waves = 0;  // FMX_DIAG_WALK builds
+  double cert = 0, viol = 0, warmq = 0, cert_slow = 0, warm_slow = 0, cert_bl = 0, blocks = 0;  // FMX_CERT_DIAG builds
   double ph50[4] = {0, 0, 0, 0}, ph99[4] = {0, 0, 0, 0};              // FMX_DIAG_PHASE builds
   ~MatchDiag() {
     if (!on || !launches) return;
@@ -493,6 +507,12 @@ struct MatchDiag {
                     "%.1f / %.1f, faces %.1f / %.1f, edges+corners %.1f / %.1f\n",
             ph50[0] / n, ph99[0] / n, ph50[1] / n, ph99[1] / n, ph50[2] / n, ph99[2] / n, ph50[3] / n, ph99[3] / n);
 #endif
+    if (warmq > 0)
+      fprintf(stderr,
+              "match diag: warm certificate: %.0f of %.0f warm queries certifiable (%.3f), %.0f certified with a "
+              "changed NN (must be 0); slowest 1%% of blocks: %.3f of their warm queries; blocks all certifiable: "
+              "%.3f\n",
+              cert, warmq, cert / warmq, viol, warm_slow > 0 ? cert_slow / warm_slow : 0.0, cert_bl / blocks);
     if (walk_listed > 0)
       fprintf(stderr, "match diag: ring-1 list walk: %.2f rounds per wave, %.3f steps and %.3f listed cells per query\n",
               walk_rounds / waves, walk_steps / (waves * 64), walk_listed / (waves * 64));
@@ -529,6 +549,16 @@ inline void match_diag_add(const uint32_t* w, uint32_t nb) {
     d.ph50[k] += v[nb / 2];
     d.ph99[k] += v[std::min<size_t>(nb - 1, (size_t)(0.99 * nb))];
   }
+#elif FMX_CERT_DIAG
+  for (uint32_t b = 0; b < nb; ++b) {
+    d.cert += w[8 * b + 3];
+    d.viol += w[8 * b + 6];
+    d.warmq += w[8 * b + 7];
+    if (w[8 * b + 7] > 0) {
+      d.blocks += 1;
+      d.cert_bl += w[8 * b + 3] == w[8 * b + 7] ? 1 : 0;
+    }
+  }
 #else
   for (uint32_t b = 0; b < nb; ++b) {
     d.walk_rounds += w[8 * b + 3];
@@ -546,6 +576,18 @@ inline void match_diag_add(const uint32_t* w, uint32_t nb) {
     for (uint32_t v = w[8 * b + 2]; v >= 16 && h < 7; v >>= 1) ++h;
     d.mq_hist[h]++;
   }
+#if FMX_CERT_DIAG
+  {  // the slowest 1 % of blocks: how many of their warm queries certify
+    std::vector<std::pair<double, uint32_t>> bd;
+    for (uint32_t b = 0; b < nb; ++b) bd.push_back({dur[b], b});
+    std::sort(bd.begin(), bd.end());
+    const size_t ns = std::max<size_t>(1, nb / 100);
+    for (size_t i = nb - ns; i < nb; ++i) {
+      d.cert_slow += w[8 * bd[i].second + 3];
+      d.warm_slow += w[8 * bd[i].second + 7];
+    }
+  }
+#endif
   std::sort(dur.begin(), dur.end());
   std::sort(fin.begin(), fin.end());
   std::sort(by.begin(), by.end());

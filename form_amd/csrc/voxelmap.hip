@@ -132,7 +132,20 @@ struct BuildArgs {
   unsigned long long* info;  // pinned host word: epoch << 32 | dense cells (k_match<DENSE> choice)
   double4* pos;
   double4* nrm;
+  uint32_t rsh;  // record stride: 1 << rsh bytes (5: separate pos / nrm arrays, 6: interleaved)
 };
+
+// Record slot i of a record array with stride 1 << rsh bytes.  Small maps keep
+// positions and normals in two arrays (32-B stride: a walk over a cell reads 2
+// positions per 64-B line); large maps (C5) interleave them (64-B stride, nrm = pos +
+// 32 B): a candidate record's line then also holds its normal, so the winner's normal
+// costs no second random line (whole-map PMC traffic 1.37x the byte model).
+__device__ __forceinline__ double4& rec_at(double4* base, uint32_t i, uint32_t rsh) {
+  return *reinterpret_cast<double4*>(reinterpret_cast<char*>(base) + ((size_t)i << rsh));
+}
+__device__ __forceinline__ const double4& rec_at(const double4* base, uint32_t i, uint32_t rsh) {
+  return *reinterpret_cast<const double4*>(reinterpret_cast<const char*>(base) + ((size_t)i << rsh));
+}
 
 // world position (and normal) of build-order record rec
 struct RecW {
@@ -340,8 +353,8 @@ __global__ __launch_bounds__(256) void k_map_scatter(BuildArgs a) {
   const uint32_t c = ri.x & 7;
   const uint32_t o = B.beg[c] + (((B.dense >> c) & 1) ? kHdr : 0) + ri.y;
   const RecW R = rec_world(a, rec, true);
-  a.pos[o] = make_double4(R.p[0], R.p[1], R.p[2], rec_tag(rec, R.seg));
-  if (R.t == 0) a.nrm[o] = make_double4(R.n[0], R.n[1], R.n[2], 0.0);
+  rec_at(a.pos, o, a.rsh) = make_double4(R.p[0], R.p[1], R.p[2], rec_tag(rec, R.seg));
+  if (R.t == 0) rec_at(a.nrm, o, a.rsh) = make_double4(R.n[0], R.n[1], R.n[2], 0.0);
 }
 
 // sub-cell of a position inside cell origin o (per axis), width sw = w / 4
@@ -359,7 +372,7 @@ __device__ void dense_sort_cell(const BuildArgs& a, uint32_t cell, uint32_t* s_c
   const uint32_t c = cell & 7;
   const uint32_t beg = B.beg[c], n = B.beg[c + 1] - beg - kHdr, first = beg + kHdr;
   const bool planar = (cell >> 3) < a.off1;
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(a.pos + beg);
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(&rec_at(a.pos, beg, a.rsh));  // 256 B in kHdr (>= 4) slots
   const int tid = threadIdx.x;
   if (n > (uint32_t)(kDenseThreads * kDenseRecs)) {
     if (tid == 0) hdr[0] = kUnsorted;
@@ -367,7 +380,7 @@ __device__ void dense_sort_cell(const BuildArgs& a, uint32_t cell, uint32_t* s_c
   }
   if (tid < kSubCells) s_cnt[tid] = 0;
   // the cell's origin from any of its records (all of them map to this cell)
-  const double4 p0 = a.pos[first];
+  const double4 p0 = rec_at(a.pos, first, a.rsh);
   const double ox = floor(p0.x / a.w) * a.w, oy = floor(p0.y / a.w) * a.w, oz = floor(p0.z / a.w) * a.w;
   const double sw = a.w / kSubPerAxis;
   __syncthreads();
@@ -377,8 +390,8 @@ __device__ void dense_sort_cell(const BuildArgs& a, uint32_t cell, uint32_t* s_c
   for (int u = 0; u < kDenseRecs; ++u) {
     const uint32_t i = (uint32_t)(u * kDenseThreads + tid);
     if (i < n) {
-      rp[u] = a.pos[first + i];
-      if (planar) rn[u] = a.nrm[first + i];
+      rp[u] = rec_at(a.pos, first + i, a.rsh);
+      if (planar) rn[u] = rec_at(a.nrm, first + i, a.rsh);
       const uint32_t sub = (uint32_t)(sub_axis(rp[u].x, ox, sw) + kSubPerAxis * sub_axis(rp[u].y, oy, sw) +
                                       kSubPerAxis * kSubPerAxis * sub_axis(rp[u].z, oz, sw));
       rs[u] = sub | (atomicAdd(&s_cnt[sub], 1u) << 8);
@@ -400,8 +413,8 @@ __device__ void dense_sort_cell(const BuildArgs& a, uint32_t cell, uint32_t* s_c
     const uint32_t i = (uint32_t)(u * kDenseThreads + tid);
     if (i < n) {
       const uint32_t o = first + s_off[rs[u] & 0xFF] + (rs[u] >> 8);
-      a.pos[o] = rp[u];
-      if (planar) a.nrm[o] = rn[u];
+      rec_at(a.pos, o, a.rsh) = rp[u];
+      if (planar) rec_at(a.nrm, o, a.rsh) = rn[u];
     }
   }
 }
@@ -423,6 +436,7 @@ struct MapView {
   const double4* pos;
   const double4* nrm;
   uint32_t epoch;
+  uint32_t rsh;  // record stride shift (rec_at)
 };
 
 // Cell shifts searched around the query's cell: [0] own cell, [1,7) the 6 face
@@ -486,6 +500,13 @@ struct MatchArgs {
   // per query, its own cell as the last match found it (packed cell coordinates, record
   // range, dense bit; fmx_ctx::m_cell): read when `warm` is set, rewritten with rec
   uint4* cell;
+#if FMX_CERT_DIAG
+  // warm certificate diagnostic (FMX_CERT_DIAG builds, VERDICT r3 "next round" 5): per
+  // query the previous match's second-best bound B2 (fp32, rounded down: every record
+  // other than its NN was at d^2 >= B2, or could not be examined), and that match's pose
+  float* cert_b2;
+  double Tprev[12];
+#endif
 };
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
@@ -651,6 +672,9 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_F32_BOUNDS
 #define FMX_F32_BOUNDS 1  // cell lower bounds in fp32 from the query's in-cell offset (A/B switch)
 #endif
+#ifndef FMX_CERT_DIAG
+#define FMX_CERT_DIAG 0  // diagnostic build: count the warm queries a second-best certificate settles
+#endif
 #ifndef FMX_WARM_START
 #define FMX_WARM_START 1  // bound each search by the previous match's record (compile-time A/B switch)
 #endif
@@ -691,7 +715,13 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
                                           uint32_t& best_sg,
                                           uint32_t& n_probe, uint32_t& n_cand, uint32_t& n_iter, uint32_t& n_list,
                                           double warm_b = INFINITY, uint32_t* phase = nullptr,
-                                          uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u}, uint4* oc_out = nullptr) {
+                                          uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u}, uint4* oc_out = nullptr,
+                                          double* b2_out = nullptr) {
+  // FMX_CERT_DIAG: the second-best bound of this search.  b2: the least d^2 of the
+  // examined records other than the lane's current best record; pr: the least lower
+  // bound of the cells / sub-cells pruned.  (The one-lane compact walk is not covered.)
+  constexpr bool kCert = FMX_CERT_DIAG && G > 1;
+  double b2 = INFINITY, pr = INFINITY;
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
   // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
   // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
@@ -749,10 +779,13 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     const unsigned long long t = tag_bits(p.w);
     const uint32_t tk = rk | ((uint32_t)t & 0x07FFFFFFu);  // build order: low bits
     if (d2 <= best && (d2 < best || tk < best_rid)) {
+      if (kCert && best_i != 0xFFFFFFFFu) b2 = fmin(b2, best);  // the displaced record
       best = d2;
       best_rid = tk;
       best_i = i;
       best_sg = (uint32_t)(t >> 32);  // the record's segment, for the epilogue's pose loads
+    } else if (kCert) {
+      b2 = fmin(b2, d2);
     }
   };
   // The same argmin in three reductions instead of one over (d^2, tie, index) moves:
@@ -790,6 +823,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false));
       };
       const double mine = best;
+      const bool rec_mine = best_i != 0xFFFFFFFFu;
       if constexpr (G >= 16) dmin(std::integral_constant<int, 0x140>{});  // row_mirror: l <-> 15-l
       if constexpr (G >= 8) dmin(std::integral_constant<int, 0x141>{});   // row_half_mirror
       if constexpr (G >= 4) dmin(std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]
@@ -800,6 +834,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       if constexpr (G >= 4) umin(r, std::integral_constant<int, 0x4E>{});
       if constexpr (G >= 2) umin(r, std::integral_constant<int, 0xB1>{});
       const bool win = mine == best && best_rid == r;
+      if (kCert && !win && rec_mine) b2 = fmin(b2, mine);  // a lane's record that lost the argmin
       uint32_t i = win ? best_i : 0xFFFFFFFFu, sg = win ? best_sg : 0xFFFFFFFFu;
       if constexpr (G >= 16) umin(i, std::integral_constant<int, 0x140>{});
       if constexpr (G >= 8) umin(i, std::integral_constant<int, 0x141>{});
@@ -848,16 +883,16 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       for (; i + (D - 1) * G < end; i += D * G) {
         double4 pr[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) pr[d] = M.pos[i + d * G];
+        for (int d = 0; d < D; ++d) pr[d] = rec_at(M.pos, i + d * G, M.rsh);
 #pragma unroll
         for (int d = 0; d < D; ++d) fold(pr[d], i + d * G, rk);
       }
-      for (; i < end; i += G) fold(M.pos[i], i, rk);
+      for (; i < end; i += G) fold(rec_at(M.pos, i, M.rsh), i, rk);
       group_min();
       return;
     }
     constexpr int kPer = kSubCells / G;  // sub-cells per lane
-    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(M.pos + first);
+    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(&rec_at(M.pos, first, M.rsh));
     const uint32_t base = dense ? first + kHdr : first;
     // the query's offset from this cell's origin, per axis
     const float ox = qo[0] - sx * wf, oy = qo[1] - sy * wf, oz = qo[2] - sz * wf;
@@ -915,6 +950,8 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         if (e0 > s0 && sub_lb(qs) <= best) {
           mask = 1ull << qs;
           tot = e0 - s0;
+        } else if (kCert && e0 > s0) {
+          pr = fmin(pr, sub_lb(qs));
         }
       } else {  // lane g bounds sub-cells g, g + G, ...; a ballot per stride
 #pragma unroll 1
@@ -922,6 +959,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           const int sub = u * G + g;
           const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
           const bool lv = sub != qs && e0 > s0 && sub_lb(sub) <= best;
+          if (kCert && !lv && sub != qs && e0 > s0) pr = fmin(pr, sub_lb(sub));
           if (lv) tot += e0 - s0;
           mask |= group_bits<G>(__ballot(lv)) << (u * G);
         }
@@ -950,13 +988,13 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
 #pragma unroll
         for (int d = 0; d < D; ++d) ix[d] = locate(v + d * G);
 #pragma unroll
-        for (int d = 0; d < D; ++d) pr[d] = M.pos[ix[d]];
+        for (int d = 0; d < D; ++d) pr[d] = rec_at(M.pos, ix[d], M.rsh);
 #pragma unroll
         for (int d = 0; d < D; ++d) fold(pr[d], ix[d], rk);
       }
       for (; v < tot; v += G) {
         const uint32_t i = locate(v);
-        fold(M.pos[i], i, rk);
+        fold(rec_at(M.pos, i, M.rsh), i, rk);
       }
       group_min();
     }
@@ -1032,6 +1070,8 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           if (own && s == 0 && oc_out) *oc_out = uint4{own_key.x, own_key.y, vf, vc | (vd ? 0x80000000u : 0u)};
         }
         vlb = lb;
+      } else if (kCert) {
+        pr = fmin(pr, lb);
       }
     } else if (own && s == 0 && oc_out) {
       *oc_out = uint4{0u, 0x80000000u, 0u, 0u};  // no entry
@@ -1049,7 +1089,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       double4 pr[kSmallCell];
 #pragma unroll
       for (int u = 0; u < kSmallCell; ++u)
-        if (u < (int)vc) pr[u] = M.pos[vf + u];
+        if (u < (int)vc) pr[u] = rec_at(M.pos, vf + u, M.rsh);
 #pragma unroll
       for (int u = 0; u < kSmallCell; ++u)
         if (u < (int)vc) fold(pr[u], vf + u, rk);
@@ -1061,7 +1101,10 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       const int l = __ffsll((unsigned long long)live) - 1;
       live &= live - 1;
       const double lb = __shfl(vlb, l, G);
-      if (lb > best) continue;  // best is group-uniform here
+      if (lb > best) {  // best is group-uniform here
+        if (kCert) pr = fmin(pr, lb);
+        continue;
+      }
       const uint32_t cnt = __shfl(vc, l, G);
       const uint32_t first = __shfl(vf, l, G);
       const bool dn = __shfl((int)vd, l, G) != 0;
@@ -1085,7 +1128,9 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     uint64_t m0 = 0, m1 = 0;  // admitted shifts: bit s - 1
     for (int u = 0; u * G < nsh; ++u) {
       const int s = 1 + u * G + g;
-      const bool ad = inr && s <= nsh && shift_lb(s) <= best;
+      const double slb = inr && s <= nsh ? shift_lb(s) : INFINITY;
+      const bool ad = inr && s <= nsh && slb <= best;
+      if (kCert && !ad) pr = fmin(pr, slb);
       const uint64_t b = group_bits<G>(__ballot(ad));
       const int bit = u * G;
       if (bit < 64) m0 |= b << bit;
@@ -1223,7 +1268,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           double4 pr[kSmallCell];
 #pragma unroll
           for (int u = 0; u < kSmallCell; ++u)
-            if (u < (int)vc) pr[u] = M.pos[vf + u];
+            if (u < (int)vc) pr[u] = rec_at(M.pos, vf + u, M.rsh);
 #pragma unroll
           for (int u = 0; u < kSmallCell; ++u)
             if (u < (int)vc) fold(pr[u], vf + u, rk);
@@ -1233,6 +1278,12 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         }
       }
     }
+  }
+  if constexpr (kCert) {
+    double v = fmin(b2, pr);
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) v = fmin(v, __shfl_xor(v, o, G));
+    if (b2_out) *b2_out = fmin(v, a.bound);  // records beyond the search bound were never examined
   }
 }
 
@@ -1361,8 +1412,8 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     if (found) {
       // the record, its normal and its segment's inverse pose in flight together (the
       // segment came with the argmin)
-      const double4 p = M.pos[best_i];
-      const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);
+      const double4 p = rec_at(M.pos, best_i, M.rsh);
+      const double4 n = planar ? rec_at(M.nrm, best_i, M.rsh) : make_double4(0, 0, 0, 0);
       const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
       double o[3];
       d_xform(Ti, p.x, p.y, p.z, o);
@@ -1391,6 +1442,10 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
 #else
   uint32_t* phase = nullptr;
 #endif
+#if FMX_CERT_DIAG
+  bool cert_q = false, warm_q = false, viol_q = false;
+  double b2q = INFINITY;
+#endif
   if (qi < nq) {
     double wq[3];
     world_query(qi, wq);
@@ -1407,13 +1462,33 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     constexpr bool kWarm = FMX_WARM_START && !FUSED;
     uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u};
     if (kWarm && a.warm && a.cell) ocv = a.cell[gq];
+    uint32_t warm_r = 0xFFFFFFFFu;
     if (kWarm && a.warm) {
       const uint32_t r = a.warm[gq];
+      warm_r = r;
       if (r != 0xFFFFFFFFu) {
-        const double4 p = M.pos[r];
+        const double4 p = rec_at(M.pos, r, M.rsh);
         const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
         const double d2 = (dx * dx + dz * dz) + dy * dy;
         if (d2 <= a.warm_lim) warm_b = d2;
+#if FMX_CERT_DIAG
+        // the certificate: the query moved by delta since the previous match (same
+        // own cell: same 27 cells); its NN then had distance d1 and every other
+        // candidate >= sqrt(B2), so if sqrt(B2) - delta > d1 + delta the NN is unchanged
+        if (a.cert_b2 && a.rings == 1 && !FUSED && kGroup > 1) {
+          const float4 lq = planar ? q_pl[qi] : q_pt[qi];
+          double wo[3];
+          d_xform(a.Tprev, (double)lq.x, (double)lq.y, (double)lq.z, wo);
+          const double ex = wo[0] - p.x, ey = wo[1] - p.y, ez = wo[2] - p.z;
+          const double d1o = (ex * ex + ez * ez) + ey * ey;
+          const double mx = wq[0] - wo[0], my = wq[1] - wo[1], mz = wq[2] - wo[2];
+          const double delta = sqrt(mx * mx + my * my + mz * mz);
+          const int cx = (int)floor(wq[0] / a.w), cy = (int)floor(wq[1] / a.w), cz = (int)floor(wq[2] / a.w);
+          const bool same = (int)floor(wo[0] / a.w) == cx && (int)floor(wo[1] / a.w) == cy &&
+                            (int)floor(wo[2] / a.w) == cz;
+          cert_q = same && sqrt((double)a.cert_b2[gq]) - delta > sqrt(d1o) + delta + 1e-7;
+        }
+#endif
       }
     }
     nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, best_sg, n_probe,
@@ -1423,7 +1498,16 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
 #else
                              phase,
 #endif
-                             ocv, kWarm && a.cell && g == 0 ? a.cell + gq : nullptr);
+                             ocv, kWarm && a.cell && g == 0 ? a.cell + gq : nullptr
+#if FMX_CERT_DIAG
+                             , &b2q
+#endif
+    );
+#if FMX_CERT_DIAG
+    if (a.cert_b2 && g == 0 && kGroup > 1) a.cert_b2[gq] = __double2float_rd(b2q);
+    warm_q = warm_r != 0xFFFFFFFFu;
+    viol_q = cert_q && best_i != warm_r;
+#endif
   }
   // work counters for the algorithmic-byte model and the match diagnostics (one plain
   // store per block, summed on the host): probes, candidate records, the largest
@@ -1446,6 +1530,16 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; ++k) atomicMax(&s_ph[k], phase[k] - t_begin);
+#endif
+#if FMX_CERT_DIAG  // per block: certifiable queries, certified but changed NN (must be 0), warm queries
+  __shared__ uint32_t s_cert[3];
+  if (threadIdx.x < 3) s_cert[threadIdx.x] = 0;
+  __syncthreads();
+  if (qi < nq && g == 0) {
+    if (cert_q) atomicAdd(&s_cert[0], 1u);
+    if (viol_q) atomicAdd(&s_cert[1], 1u);
+    if (warm_q) atomicAdd(&s_cert[2], 1u);
+  }
 #endif
 #ifdef FMX_DIAG_WALK  // per block: sum over waves of the wave's walk rounds, lanes' walk steps, listed cells
   __shared__ uint32_t s_walk[3][kMatchThreads / kWave];
@@ -1482,6 +1576,11 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     d0 = min(s_ph[0], 0xFFFFu) | min(s_ph[1], 0xFFFFu) << 16;
     d1 = min(s_ph[2], 0xFFFFu) | min(s_ph[3], 0xFFFFu) << 16;
 #endif
+#if FMX_CERT_DIAG
+    d0 = s_cert[0];
+    d1 = s_cert[1];
+    d2 = s_cert[2];
+#endif
     w4[0] = make_uint4(tp, tc, mq, d0);
     w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), d1, d2);
   }
@@ -1495,8 +1594,8 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     double pi[3] = {0, 0, 0}, ni[3] = {0, 0, 0}, pj[3] = {0, 0, 0};
     const double* Ti = fz.poses;
     if (acc_q) {
-      const double4 p = M.pos[best_i];
-      const double4 n = planar ? M.nrm[best_i] : make_double4(0, 0, 0, 0);
+      const double4 p = rec_at(M.pos, best_i, M.rsh);
+      const double4 n = planar ? rec_at(M.nrm, best_i, M.rsh) : make_double4(0, 0, 0, 0);
       const uint32_t sg = best_sg;  // (with the argmin: the pose loads need not wait for p)
       const double* Tinv = inv_poses + 12 * sg;  // matcher.hpp:95
       d_xform(Tinv, p.x, p.y, p.z, pi);
@@ -1996,8 +2095,17 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   // planar slots [0, pt_base): records + the header slots of at most n0 / (kDenseMin + 1)
   // dense cells; point slots from pt_base
   const uint32_t pt_base = nrec[0] + nrec[0] / (kDenseMin + 1) * kHdr;
-  M.pos.ensure((size_t)pt_base + nrec[1] + nrec[1] / (kDenseMin + 1) * kHdr + 1);
-  M.nrm.ensure((size_t)pt_base + 1);
+  const size_t rslots = (size_t)pt_base + nrec[1] + nrec[1] / (kDenseMin + 1) * kHdr + 1;
+  // record layout (rec_at): interleaved pos + normal for large maps
+  M.rsh = n >= interleave_min() ? 6u : 5u;
+  if (M.rsh == 6) {
+    M.pos.ensure(2 * rslots);
+    M.nrm_p = M.pos.p + 1;
+  } else {
+    M.pos.ensure(rslots);
+    M.nrm.ensure((size_t)pt_base + 1);
+    M.nrm_p = M.nrm.p;
+  }
   // algorithmic bytes: read local records (16 B pos + 16 B planar normal, twice: insert
   // and scatter recompute the transform) + write world records (32 B + 32 B planar) + the
   // 64-B brick of each record's cell (claim + count, then its range) + rank word
@@ -2029,7 +2137,8 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   ba.st = bst + (M.epoch & 1);
   ba.st_next = bst + ((M.epoch + 1) & 1);
   ba.pos = M.pos.p;
-  ba.nrm = M.nrm.p;
+  ba.nrm = M.nrm_p;
+  ba.rsh = M.rsh;
   if (!c->h_mapinfo.p) {
     c->h_mapinfo.ensure(1);
     c->h_mapinfo.p[0] = 0;
@@ -2115,6 +2224,14 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     a.rec = c->m_rec.p;
     a.cell = no_cell_cache() ? nullptr : c->m_cell.p;
     c->warm_rec_gen = c->warm_gen;
+#if FMX_CERT_DIAG
+    const float* cb = c->cert_b2.p;
+    c->cert_b2.ensure((size_t)c->n_qpl + c->n_qpt + 1);
+    if (c->cert_b2.p != cb) a.warm = nullptr;  // regrown: no previous bounds
+    a.cert_b2 = c->cert_b2.p;
+    std::memcpy(a.Tprev, c->cert_pose, sizeof(a.Tprev));
+    std::memcpy(c->cert_pose, a.Tj, sizeof(a.Tj));
+#endif
   }
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
@@ -2160,7 +2277,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   auto view = [&](int t) {  // type t's table section over the shared record arrays
     VoxMap& M = c->map;
     return MapView{reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
-                   M.pos.p, M.nrm.p, M.epoch};
+                   M.pos.p, M.nrm_p, M.epoch, M.rsh};
   };
   // Algorithmic bytes of a match launch: query read (16 B) +
   // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + one 64-B line per
@@ -2253,6 +2370,9 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   a.rec = nullptr;
   a.cell = nullptr;
   a.warm_lim = 0.0;
+#if FMX_CERT_DIAG
+  a.cert_b2 = nullptr;
+#endif
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
@@ -2277,7 +2397,7 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   auto view = [&](int t) {
     VoxMap& M = c->map;
     return MapView{reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
-                   M.pos.p, M.nrm.p, M.epoch};
+                   M.pos.p, M.nrm_p, M.epoch, M.rsh};
   };
   bool dense = c->map.n[0] + c->map.n[1] > 0;
   if (dense && c->h_mapinfo.p) {
