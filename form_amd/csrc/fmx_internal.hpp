@@ -549,7 +549,7 @@ inline void match_diag_add(const uint32_t* w, uint32_t nb) {
     d.ph50[k] += v[nb / 2];
     d.ph99[k] += v[std::min<size_t>(nb - 1, (size_t)(0.99 * nb))];
   }
-#elif FMX_CERT_DIAG
+#elif FMX_CERT_DIAG || FMX_WARM_CERT
   for (uint32_t b = 0; b < nb; ++b) {
     d.cert += w[8 * b + 3];
     d.viol += w[8 * b + 6];
@@ -576,7 +576,7 @@ inline void match_diag_add(const uint32_t* w, uint32_t nb) {
     for (uint32_t v = w[8 * b + 2]; v >= 16 && h < 7; v >>= 1) ++h;
     d.mq_hist[h]++;
   }
-#if FMX_CERT_DIAG
+#if FMX_CERT_DIAG || FMX_WARM_CERT
   {  // the slowest 1 % of blocks: how many of their warm queries certify
     std::vector<std::pair<double, uint32_t>> bd;
     for (uint32_t b = 0; b < nb; ++b) bd.push_back({dur[b], b});

@@ -500,10 +500,10 @@ struct MatchArgs {
   // per query, its own cell as the last match found it (packed cell coordinates, record
   // range, dense bit; fmx_ctx::m_cell): read when `warm` is set, rewritten with rec
   uint4* cell;
-#if FMX_CERT_DIAG
-  // warm certificate diagnostic (FMX_CERT_DIAG builds, VERDICT r3 "next round" 5): per
-  // query the previous match's second-best bound B2 (fp32, rounded down: every record
-  // other than its NN was at d^2 >= B2, or could not be examined), and that match's pose
+#if FMX_CERT_DIAG || FMX_WARM_CERT
+  // warm certificate (VERDICT r3 "next round" 5): per query the previous match's
+  // second-best bound B2 (fp32, never above the truth: every record other than its NN
+  // was at d^2 >= B2, or could not be examined), and that match's pose
   float* cert_b2;
   double Tprev[12];
 #endif
@@ -675,6 +675,10 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_CERT_DIAG
 #define FMX_CERT_DIAG 0  // diagnostic build: count the warm queries a second-best certificate settles
 #endif
+#ifndef FMX_WARM_CERT
+#define FMX_WARM_CERT 0  // warm queries whose certificate holds skip the search (A/B switch)
+#endif
+#define FMX_CERT_ANY (FMX_CERT_DIAG || FMX_WARM_CERT)
 #ifndef FMX_WARM_START
 #define FMX_WARM_START 1  // bound each search by the previous match's record (compile-time A/B switch)
 #endif
@@ -707,6 +711,10 @@ __device__ __forceinline__ int ring1_index(int dx, int dy, int dz) {
     return dz == 0 ? 7 + 2 * (dx < 0) + (dy < 0) : (dy == 0 ? 11 + 2 * (dx < 0) + (dz < 0) : 15 + 2 * (dy < 0) + (dz < 0));
   return 19 + 4 * (dx < 0) + 2 * (dy < 0) + (dz < 0);
 }
+// A non-negative double as an fp32 value never above it (round to nearest, then shrink
+// by 2^-22 relative: past both roundings); +inf stays +inf.
+__device__ __forceinline__ float cdown(double v) { return (float)v * (1.0f - 0x1p-22f); }
+
 // VoxelMap::find_closest (map.tpp:70-91) of one query by a group of G lanes (lane g of
 // the group), bounded by the incoming best (a.bound, or +inf).
 template <int G, bool DENSE>
@@ -716,12 +724,13 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
                                           uint32_t& n_probe, uint32_t& n_cand, uint32_t& n_iter, uint32_t& n_list,
                                           double warm_b = INFINITY, uint32_t* phase = nullptr,
                                           uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u}, uint4* oc_out = nullptr,
-                                          double* b2_out = nullptr) {
-  // FMX_CERT_DIAG: the second-best bound of this search.  b2: the least d^2 of the
-  // examined records other than the lane's current best record; pr: the least lower
-  // bound of the cells / sub-cells pruned.  (The one-lane compact walk is not covered.)
-  constexpr bool kCert = FMX_CERT_DIAG && G > 1;
-  double b2 = INFINITY, pr = INFINITY;
+                                          float* b2_out = nullptr) {
+  // The warm certificate's second-best bound of this search (FMX_CERT_ANY builds): b2,
+  // the least d^2 of the examined records other than the lane's current best record;
+  // pr, the least lower bound of the cells / sub-cells pruned.  fp32, rounded down
+  // (cdown): a bound may only be too small.  (The one-lane compact walk is not covered.)
+  constexpr bool kCert = FMX_CERT_ANY && G > 1;
+  float b2 = INFINITY, pr = INFINITY;
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
   // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
   // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
@@ -779,13 +788,13 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     const unsigned long long t = tag_bits(p.w);
     const uint32_t tk = rk | ((uint32_t)t & 0x07FFFFFFu);  // build order: low bits
     if (d2 <= best && (d2 < best || tk < best_rid)) {
-      if (kCert && best_i != 0xFFFFFFFFu) b2 = fmin(b2, best);  // the displaced record
+      if (kCert && best_i != 0xFFFFFFFFu) b2 = fminf(b2, cdown(best));  // the displaced record
       best = d2;
       best_rid = tk;
       best_i = i;
       best_sg = (uint32_t)(t >> 32);  // the record's segment, for the epilogue's pose loads
     } else if (kCert) {
-      b2 = fmin(b2, d2);
+      b2 = fminf(b2, cdown(d2));
     }
   };
   // The same argmin in three reductions instead of one over (d^2, tie, index) moves:
@@ -834,7 +843,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       if constexpr (G >= 4) umin(r, std::integral_constant<int, 0x4E>{});
       if constexpr (G >= 2) umin(r, std::integral_constant<int, 0xB1>{});
       const bool win = mine == best && best_rid == r;
-      if (kCert && !win && rec_mine) b2 = fmin(b2, mine);  // a lane's record that lost the argmin
+      if (kCert && !win && rec_mine) b2 = fminf(b2, cdown(mine));  // a lane's record that lost the argmin
       uint32_t i = win ? best_i : 0xFFFFFFFFu, sg = win ? best_sg : 0xFFFFFFFFu;
       if constexpr (G >= 16) umin(i, std::integral_constant<int, 0x140>{});
       if constexpr (G >= 8) umin(i, std::integral_constant<int, 0x141>{});
@@ -951,7 +960,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           mask = 1ull << qs;
           tot = e0 - s0;
         } else if (kCert && e0 > s0) {
-          pr = fmin(pr, sub_lb(qs));
+          pr = fminf(pr, cdown(sub_lb(qs)));
         }
       } else {  // lane g bounds sub-cells g, g + G, ...; a ballot per stride
 #pragma unroll 1
@@ -959,7 +968,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           const int sub = u * G + g;
           const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
           const bool lv = sub != qs && e0 > s0 && sub_lb(sub) <= best;
-          if (kCert && !lv && sub != qs && e0 > s0) pr = fmin(pr, sub_lb(sub));
+          if (kCert && !lv && sub != qs && e0 > s0) pr = fminf(pr, cdown(sub_lb(sub)));
           if (lv) tot += e0 - s0;
           mask |= group_bits<G>(__ballot(lv)) << (u * G);
         }
@@ -1071,7 +1080,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         }
         vlb = lb;
       } else if (kCert) {
-        pr = fmin(pr, lb);
+        pr = fminf(pr, cdown(lb));
       }
     } else if (own && s == 0 && oc_out) {
       *oc_out = uint4{0u, 0x80000000u, 0u, 0u};  // no entry
@@ -1102,7 +1111,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       live &= live - 1;
       const double lb = __shfl(vlb, l, G);
       if (lb > best) {  // best is group-uniform here
-        if (kCert) pr = fmin(pr, lb);
+        if (kCert) pr = fminf(pr, cdown(lb));
         continue;
       }
       const uint32_t cnt = __shfl(vc, l, G);
@@ -1130,7 +1139,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       const int s = 1 + u * G + g;
       const double slb = inr && s <= nsh ? shift_lb(s) : INFINITY;
       const bool ad = inr && s <= nsh && slb <= best;
-      if (kCert && !ad) pr = fmin(pr, slb);
+      if (kCert && !ad) pr = fminf(pr, cdown(slb));
       const uint64_t b = group_bits<G>(__ballot(ad));
       const int bit = u * G;
       if (bit < 64) m0 |= b << bit;
@@ -1280,10 +1289,10 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     }
   }
   if constexpr (kCert) {
-    double v = fmin(b2, pr);
+    float v = fminf(b2, pr);
 #pragma unroll
-    for (int o = 1; o < G; o <<= 1) v = fmin(v, __shfl_xor(v, o, G));
-    if (b2_out) *b2_out = fmin(v, a.bound);  // records beyond the search bound were never examined
+    for (int o = 1; o < G; o <<= 1) v = fminf(v, __shfl_xor(v, o, G));
+    if (b2_out) *b2_out = fminf(v, cdown(a.bound));  // records beyond the search bound were never examined
   }
 }
 
@@ -1442,9 +1451,9 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
 #else
   uint32_t* phase = nullptr;
 #endif
-#if FMX_CERT_DIAG
+#if FMX_CERT_ANY
   bool cert_q = false, warm_q = false, viol_q = false;
-  double b2q = INFINITY;
+  float b2q = INFINITY;
 #endif
   if (qi < nq) {
     double wq[3];
@@ -1471,10 +1480,11 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
         const double d2 = (dx * dx + dz * dz) + dy * dy;
         if (d2 <= a.warm_lim) warm_b = d2;
-#if FMX_CERT_DIAG
+#if FMX_CERT_ANY
         // the certificate: the query moved by delta since the previous match (same
         // own cell: same 27 cells); its NN then had distance d1 and every other
         // candidate >= sqrt(B2), so if sqrt(B2) - delta > d1 + delta the NN is unchanged
+        // (strictly: no tie), and the search would return it again
         if (a.cert_b2 && a.rings == 1 && !FUSED && kGroup > 1) {
           const float4 lq = planar ? q_pl[qi] : q_pt[qi];
           double wo[3];
@@ -1486,11 +1496,23 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
           const int cx = (int)floor(wq[0] / a.w), cy = (int)floor(wq[1] / a.w), cz = (int)floor(wq[2] / a.w);
           const bool same = (int)floor(wo[0] / a.w) == cx && (int)floor(wo[1] / a.w) == cy &&
                             (int)floor(wo[2] / a.w) == cz;
-          cert_q = same && sqrt((double)a.cert_b2[gq]) - delta > sqrt(d1o) + delta + 1e-7;
+          const double rb = sqrt((double)a.cert_b2[gq]) - delta;
+          cert_q = same && rb > sqrt(d1o) + delta + 1e-7;
+#if FMX_WARM_CERT
+          if (cert_q) {  // settled: the NN at the new pose, and the bound carried forward
+            best = d2;
+            best_i = r;
+            best_sg = (uint32_t)(tag_bits(p.w) >> 32);
+            b2q = cdown(rb * rb);
+          }
+#endif
         }
 #endif
       }
     }
+#if FMX_WARM_CERT
+    if (!cert_q)
+#endif
     nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, best_sg, n_probe,
                              n_cand, n_iter, n_list, warm_b,
 #ifdef FMX_DIAG_PHASE
@@ -1499,12 +1521,12 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
                              phase,
 #endif
                              ocv, kWarm && a.cell && g == 0 ? a.cell + gq : nullptr
-#if FMX_CERT_DIAG
+#if FMX_CERT_ANY
                              , &b2q
 #endif
     );
-#if FMX_CERT_DIAG
-    if (a.cert_b2 && g == 0 && kGroup > 1) a.cert_b2[gq] = __double2float_rd(b2q);
+#if FMX_CERT_ANY
+    if (a.cert_b2 && g == 0 && kGroup > 1) a.cert_b2[gq] = b2q;
     warm_q = warm_r != 0xFFFFFFFFu;
     viol_q = cert_q && best_i != warm_r;
 #endif
@@ -1531,7 +1553,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
 #pragma unroll
   for (int k = 0; k < 4; ++k) atomicMax(&s_ph[k], phase[k] - t_begin);
 #endif
-#if FMX_CERT_DIAG  // per block: certifiable queries, certified but changed NN (must be 0), warm queries
+#if FMX_CERT_ANY  // per block: certifiable queries, certified but changed NN (must be 0), warm queries
   __shared__ uint32_t s_cert[3];
   if (threadIdx.x < 3) s_cert[threadIdx.x] = 0;
   __syncthreads();
@@ -1576,7 +1598,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     d0 = min(s_ph[0], 0xFFFFu) | min(s_ph[1], 0xFFFFu) << 16;
     d1 = min(s_ph[2], 0xFFFFu) | min(s_ph[3], 0xFFFFu) << 16;
 #endif
-#if FMX_CERT_DIAG
+#if FMX_CERT_ANY
     d0 = s_cert[0];
     d1 = s_cert[1];
     d2 = s_cert[2];
@@ -2224,7 +2246,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     a.rec = c->m_rec.p;
     a.cell = no_cell_cache() ? nullptr : c->m_cell.p;
     c->warm_rec_gen = c->warm_gen;
-#if FMX_CERT_DIAG
+#if FMX_CERT_ANY
     const float* cb = c->cert_b2.p;
     c->cert_b2.ensure((size_t)c->n_qpl + c->n_qpt + 1);
     if (c->cert_b2.p != cb) a.warm = nullptr;  // regrown: no previous bounds
@@ -2370,7 +2392,7 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   a.rec = nullptr;
   a.cell = nullptr;
   a.warm_lim = 0.0;
-#if FMX_CERT_DIAG
+#if FMX_CERT_ANY
   a.cert_b2 = nullptr;
 #endif
   a.nq_pl = c->n_qpl;
