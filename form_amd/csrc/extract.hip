@@ -1395,6 +1395,23 @@ __global__ __launch_bounds__(256) void k_write_features(const float4* __restrict
 
 }  // namespace
 
+namespace {
+// A host scan DMA'd as packed x, y, z (stage.hpp pack3: a PointXYZf's pad is always 0,
+// utils.hpp:38-46, and no kernel reads it) back in the float4 layout the extraction
+// reads: one lane per point, three dword loads (a wave reads 768 contiguous bytes each).
+__global__ __launch_bounds__(256) void k_unpack_xyz(const float* __restrict__ p3, float4* __restrict__ out, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = make_float4(p3[3 * (size_t)i], p3[3 * (size_t)i + 1], p3[3 * (size_t)i + 2], 0.0f);
+}
+}  // namespace
+
+void unpack_xyz(fmx_ctx* c, const float* d_packed, float4* d_out, size_t n, hipStream_t st) {
+  if (!n) return;
+  ProfScope ps(c->prof, PROF_UNPACK, 28.0 * n, st);
+  hipLaunchKernelGGL(k_unpack_xyz, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, d_packed, d_out, (uint32_t)n);
+  FMX_HIP(hipGetLastError());
+}
+
 ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
                         uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq) {
   const auto& E = c->P.extraction;

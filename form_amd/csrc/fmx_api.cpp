@@ -65,7 +65,7 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
 // ============================================================================ profiling
 static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest",   "fit",       "compact", "map_build",
                                              "match",        "pair_sort", "linearize", "insert",  "window",
-                                             "match_linearize"};
+                                             "match_linearize", "unpack"};
 
 ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), bytes(by), st(s) {
   if (!pr.on) return;
@@ -353,6 +353,12 @@ bool host_pageable() {
   static const bool v = std::getenv("FMX_HOST_PAGEABLE") != nullptr;
   return v;
 }
+// Staged host scans cross PCIe as packed x, y, z (12 of 16 bytes; k_unpack_xyz restores
+// the layout on the device); FMX_STAGE_PACK=0 sends the float4 points as they are.
+bool stage_pack() {
+  static const bool v = env_int("FMX_STAGE_PACK", 1) != 0;
+  return v;
+}
 // Pinned staging buffers of `bytes` each (grown only; growing drains every stream and
 // staging request first, since DMAs may still read the old ones).
 void pinned_ensure(fmx_ctx* c, size_t bytes) {
@@ -375,7 +381,7 @@ void pinned_ensure(fmx_ctx* c, size_t bytes) {
 void stage_submit(fmx_ctx* c, StageReq& r, const void* src, void* dst, size_t bytes) {
   c->stager.retire(&r);
   c->stager.start(stage_threads());
-  r.reset(src, dst, bytes, stage_chunk());
+  r.reset(src, dst, bytes, stage_chunk(), stage_pack());
   if (c->stager.threads() > 0) c->stager.submit(&r);
 }
 // Every chunk of r copied (this thread helps) and r released by the helpers.
@@ -415,21 +421,26 @@ const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n) {
   // the host waited for: it has completed
   StageReq& r = c->st_seq;
   stage_submit(c, r, xyzw, c->pin_seq, bytes);
-  uint8_t* dev = reinterpret_cast<uint8_t*>(c->scan.p);
+  // packed: the DMA lands in scan3 and k_unpack_xyz writes c->scan; offsets scale by 3/4
+  if (r.pack3) c->scan3.ensure(3 * n);
+  uint8_t* dev = r.pack3 ? reinterpret_cast<uint8_t*>(c->scan3.p) : reinterpret_cast<uint8_t*>(c->scan.p);
+  auto dsz = [&](size_t x) { return r.pack3 ? x / 16 * 12 : x; };
   const uint32_t step = std::max<uint32_t>(1, (r.nchunks + stage_dmas() - 1) / stage_dmas());
   uint32_t issued = 0;
   while (issued < r.nchunks) {
     uint32_t ready = issued;
     while (ready < r.nchunks && r.chunk_done(ready)) ++ready;
     if (ready - issued >= step || ready == r.nchunks) {
-      const size_t a = (size_t)issued * r.chunk, b = std::min(bytes, (size_t)ready * r.chunk);
+      const size_t a = dsz((size_t)issued * r.chunk), b = dsz(std::min(bytes, (size_t)ready * r.chunk));
       FMX_HIP(hipMemcpyAsync(dev + a, c->pin_seq + a, b - a, hipMemcpyHostToDevice, c->stream));
       issued = ready;
       continue;
     }
     if (!r.work_one()) std::this_thread::yield();  // help; then wait for the helpers' chunks
   }
+  const bool packed = r.pack3;
   c->stager.retire(&r);
+  if (packed) unpack_xyz(c, c->scan3.p, c->scan.p, n, c->stream);
   return c->scan.p;
 }
 
@@ -500,8 +511,16 @@ void pf_launch(fmx_ctx* c, bool force = true) {
   FMX_HIP(hipStreamWaitEvent(c->side2, c->ev_pf_fork, 0));
   if (c->ann_host) {  // the staged copy -> the device (side2: behind the previous queued extraction's reads)
     c->pf_scan.ensure(c->ann_n);
-    const void* src = c->ann_pinned ? static_cast<const void*>(c->ann_ptr) : c->pin_pf[c->ann_slot];
-    FMX_HIP(hipMemcpyAsync(c->pf_scan.p, src, c->ann_n * sizeof(float4), hipMemcpyHostToDevice, c->side2));
+    if (c->ann_pinned) {
+      FMX_HIP(hipMemcpyAsync(c->pf_scan.p, c->ann_ptr, c->ann_n * sizeof(float4), hipMemcpyHostToDevice, c->side2));
+    } else if (c->st_pf[c->ann_slot].pack3) {
+      c->pf_scan3.ensure(3 * c->ann_n);
+      FMX_HIP(hipMemcpyAsync(c->pf_scan3.p, c->pin_pf[c->ann_slot], c->ann_n * 12, hipMemcpyHostToDevice, c->side2));
+      unpack_xyz(c, c->pf_scan3.p, c->pf_scan.p, c->ann_n, c->side2);
+    } else {
+      FMX_HIP(hipMemcpyAsync(c->pf_scan.p, c->pin_pf[c->ann_slot], c->ann_n * sizeof(float4), hipMemcpyHostToDevice,
+                             c->side2));
+    }
     d = c->pf_scan.p;
   }
   swap_query_set(c);
@@ -1375,6 +1394,8 @@ void fmx_destroy(fmx_ctx* c) {
   for (uint8_t* b : {c->pin_seq, c->pin_pf[0], c->pin_pf[1]})
     if (b) (void)hipHostFree(b);
   c->pf_scan.release();
+  c->scan3.release();
+  c->pf_scan3.release();
   for (auto& B : c->scanbuf)
     if (B.p) (void)hipHostFree(B.p);
   for (int t = 0; t < 2; ++t) {

@@ -107,6 +107,7 @@ enum ProfId {
   PROF_INSERT,
   PROF_WINDOW,
   PROF_MATCH_LIN,
+  PROF_UNPACK,
   PROF_COUNT
 };
 
@@ -338,6 +339,7 @@ struct fmx_ctx {
   int ann_slot = 0, pf_slot = 0;  // pf_slot -1: the queued extraction's DMA read caller memory
   bool pf_host = false;         // the queued extraction's scan was host memory
   fmx::DBuf<float4> pf_scan;    // device copy of a host-announced scan (side2 order)
+  fmx::DBuf<float> scan3, pf_scan3;  // packed x, y, z of staged host scans (DMA targets)
   struct ScanBuf {              // fmx_scan_buffer: pinned scan buffers handed to the caller
     float4* p = nullptr;
     size_t cap = 0;
@@ -700,6 +702,8 @@ ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStrea
 void extract_collect(fmx_ctx* c, const ExLaunch& L, fmx_feature_counts* out);
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
                  const std::function<void()>& while_waiting = nullptr);
+// packed x, y, z (a staged host scan) -> float4 points with pad 0, on stream st
+void unpack_xyz(fmx_ctx* c, const float* d_packed, float4* d_out, size_t n, hipStream_t st);
 // st: stream to build on (default the context stream; register_scan uses the side
 // stream so the build overlaps extraction)
 void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double* poses34, double w,

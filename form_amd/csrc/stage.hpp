@@ -24,10 +24,14 @@
 namespace fmx {
 
 // One staging request: bytes [0, n) of src -> dst in `chunks` pieces.  Chunks are
-// claimed by any thread (helpers or the caller) and flagged when copied.
+// claimed by any thread (helpers or the caller) and flagged when copied.  pack3: src is
+// float4 points and dst receives their x, y, z only (12 of every 16 bytes: the pad of a
+// PointXYZf is always 0, utils.hpp:38-46, so a quarter of the DMA is dropped); offsets
+// and chunk sizes are then counted in source bytes, dst offsets are 3/4 of them.
 struct StageReq {
   const uint8_t* src = nullptr;
   uint8_t* dst = nullptr;
+  bool pack3 = false;
   size_t bytes = 0, chunk = 0;
   uint32_t nchunks = 0;
   std::atomic<uint32_t> next{0};  // next unclaimed chunk
@@ -37,11 +41,12 @@ struct StageReq {
   uint32_t done_cap = 0;
   bool active = false;  // submitted, not yet waited for (owner's view)
 
-  void reset(const void* s, void* d, size_t n, size_t ch) {
+  void reset(const void* s, void* d, size_t n, size_t ch, bool pack = false) {
     src = static_cast<const uint8_t*>(s);
     dst = static_cast<uint8_t*>(d);
+    pack3 = pack;
     bytes = n;
-    chunk = std::max<size_t>(ch, 4096);
+    chunk = std::max<size_t>(ch, 4096) & ~(size_t)15;  // whole points
     nchunks = (uint32_t)((n + chunk - 1) / chunk);
     if (nchunks > done_cap) {
       done.reset(new std::atomic<uint8_t>[nchunks]);
@@ -56,7 +61,18 @@ struct StageReq {
     const uint32_t i = next.fetch_add(1, std::memory_order_acq_rel);
     if (i >= nchunks) return false;
     const size_t off = (size_t)i * chunk, len = std::min(chunk, bytes - off);
-    std::memcpy(dst + off, src + off, len);
+    if (!pack3) {
+      std::memcpy(dst + off, src + off, len);
+    } else {
+      const float* s4 = reinterpret_cast<const float*>(src + off);
+      float* d3 = reinterpret_cast<float*>(dst + off / 16 * 12);
+      const size_t np = len / 16;
+      for (size_t p = 0; p < np; ++p) {
+        d3[3 * p] = s4[4 * p];
+        d3[3 * p + 1] = s4[4 * p + 1];
+        d3[3 * p + 2] = s4[4 * p + 2];
+      }
+    }
     done[i].store(1, std::memory_order_release);
     ndone.fetch_add(1, std::memory_order_acq_rel);
     return true;
