@@ -1,0 +1,65 @@
+// test_stage.cpp — the host staging of pageable scans (form_amd/csrc/stage.hpp) on the
+// CPU: requests copied by helper threads and the caller together, plain and packed
+// (float4 -> x, y, z), several requests in flight, reuse after retire, helpers stopped
+// and restarted.  Built twice by tests/cpp/Makefile: plain and with
+// -fsanitize=thread (data races between the helpers, the caller and retire/reset).
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "stage.hpp"
+
+static int g_fail = 0;
+#define CHECK(c)                                                 \
+  do {                                                           \
+    if (!(c)) {                                                  \
+      std::fprintf(stderr, "FAIL %s:%d %s\n", __FILE__, __LINE__, #c); \
+      ++g_fail;                                                  \
+    }                                                            \
+  } while (0)
+
+int main() {
+  std::mt19937 g(7);
+  fmx::Stager st;
+  fmx::StageReq r[3];
+  for (int round = 0; round < 40; ++round) {
+    const int threads = round % 4;  // 0: the caller copies alone
+    if (round % 10 == 0) st.stop();
+    st.start(threads);
+    const size_t npts = 1000 + (g() % 70000);
+    std::vector<std::vector<float>> src(3, std::vector<float>(4 * npts));
+    std::vector<std::vector<float>> dst(3, std::vector<float>(4 * npts, -1.0f));
+    for (int k = 0; k < 3; ++k)
+      for (auto& v : src[k]) v = (float)(g() % 100000) * 0.01f;
+    for (int k = 0; k < 3; ++k) {
+      st.retire(&r[k]);
+      r[k].reset(src[k].data(), dst[k].data(), npts * 16, 4096 * (1 + k + round % 5), (round + k) % 2 == 1);
+      if (st.threads() > 0) st.submit(&r[k]);
+    }
+    for (int k = 0; k < 3; ++k) {  // the caller helps, then waits, as stage_finish does
+      while (r[k].work_one()) {
+      }
+      while (!r[k].complete()) {
+      }
+      st.retire(&r[k]);
+      for (uint32_t c = 0; c < r[k].nchunks; ++c) CHECK(r[k].chunk_done(c));
+      if (!r[k].pack3) {
+        CHECK(std::memcmp(src[k].data(), dst[k].data(), npts * 16) == 0);
+      } else {
+        bool ok = true;
+        for (size_t p = 0; p < npts && ok; ++p)
+          for (int d = 0; d < 3; ++d) ok &= dst[k][3 * p + d] == src[k][4 * p + d];
+        CHECK(ok);
+        CHECK(dst[k][3 * npts] == -1.0f);  // nothing past the packed bytes
+      }
+    }
+  }
+  st.stop();
+  if (g_fail) {
+    std::fprintf(stderr, "%d checks failed\n", g_fail);
+    return 1;
+  }
+  std::printf("stage ok\n");
+  return 0;
+}

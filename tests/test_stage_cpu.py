@@ -1,0 +1,20 @@
+"""Host staging of pageable scans (form_amd/csrc/stage.hpp), CPU only: helper threads and
+the caller copying the chunks of several requests together, plain and packed
+(float4 -> xyz), reuse after retire, helpers restarted — once plain and once under
+ThreadSanitizer (tests/cpp/test_stage.cpp, built by __graft_entry__.build())."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("name", ["test_stage", "test_stage_tsan"])
+def test_stage_helpers(name):
+    path = os.path.join(ROOT, "tests", "cpp", name)
+    if not os.path.exists(path):
+        pytest.fail(f"{path} missing: run __graft_entry__.build() (make -C tests/cpp)")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([path], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "stage ok" in r.stdout, r.stdout + r.stderr[-3000:]
