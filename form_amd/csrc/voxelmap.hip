@@ -1093,6 +1093,8 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     // records itself, every lane's loads in flight together, one group min after;
     // the argmin on (d^2, tie key) does not depend on the folding order
     const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
+    // (a probed small cell the warm bound has since pruned: its records stay unexamined)
+    if (kCert && vc != 0 && vc <= (uint32_t)kSmallCell && !(vlb <= best)) pr = fminf(pr, cdown(vlb));
     if (small) {
       const uint32_t rk = srank_s(s);
       double4 pr[kSmallCell];
