@@ -507,6 +507,14 @@ struct MatchArgs {
   float* cert_b2;
   double Tprev[12];
 #endif
+#if FMX_WARM_CERT
+  // a warm match in two launches (k_match_cert, then k_match_list): the first settles
+  // every certified query and lists the others per type (qlist: planar entries from 0,
+  // point entries from nq_pl; qlist_n[2] counts, reset by the second launch's last
+  // block); the second searches the listed queries only and runs the bookkeeping tail
+  uint32_t* qlist;
+  uint32_t* qlist_n;
+#endif
 };
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
@@ -726,11 +734,11 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
                                           uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u}, uint4* oc_out = nullptr,
                                           float* b2_out = nullptr) {
   // The warm certificate's second-best bound of this search (FMX_CERT_ANY builds): b2,
-  // the least d^2 of the examined records other than the lane's current best record;
-  // pr, the least lower bound of the cells / sub-cells pruned.  fp32, rounded down
+  // the least of the d^2 of the examined records other than the lane's current best
+  // record and the lower bounds of the cells / sub-cells pruned.  fp32, rounded down
   // (cdown): a bound may only be too small.  (The one-lane compact walk is not covered.)
   constexpr bool kCert = FMX_CERT_ANY && G > 1;
-  float b2 = INFINITY, pr = INFINITY;
+  float b2 = INFINITY;
   const int bx = (int)floor(wq[0] / a.w), by = (int)floor(wq[1] / a.w), bz = (int)floor(wq[2] / a.w);
   // argmin key (d^2, tie): tie = the reference shift rank of the record's voxel
   // (map.tpp:54-68, 77-88: the first voxel in shift order wins an exact tie) << 27 |
@@ -812,6 +820,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       uint32_t r = best == m ? best_rid : 0xFFFFFFFFu;
       for (int o = 1; o < G; o <<= 1) r = min(r, (uint32_t)__shfl_xor((int)r, o, G));
       const bool win = best == m && best_rid == r;
+      if (kCert && !win && best_i != 0xFFFFFFFFu) b2 = fminf(b2, cdown(best));  // a lane's record that lost the argmin
       uint32_t i = win ? best_i : 0xFFFFFFFFu, sg = win ? best_sg : 0xFFFFFFFFu;
       for (int o = 1; o < G; o <<= 1) i = min(i, (uint32_t)__shfl_xor((int)i, o, G));
       for (int o = 1; o < G; o <<= 1) sg = min(sg, (uint32_t)__shfl_xor((int)sg, o, G));
@@ -960,7 +969,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           mask = 1ull << qs;
           tot = e0 - s0;
         } else if (kCert && e0 > s0) {
-          pr = fminf(pr, cdown(sub_lb(qs)));
+          b2 = fminf(b2, cdown(sub_lb(qs)));
         }
       } else {  // lane g bounds sub-cells g, g + G, ...; a ballot per stride
 #pragma unroll 1
@@ -968,7 +977,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
           const int sub = u * G + g;
           const uint32_t s0 = sub_beg(sub), e0 = hd[sub];
           const bool lv = sub != qs && e0 > s0 && sub_lb(sub) <= best;
-          if (kCert && !lv && sub != qs && e0 > s0) pr = fminf(pr, cdown(sub_lb(sub)));
+          if (kCert && !lv && sub != qs && e0 > s0) b2 = fminf(b2, cdown(sub_lb(sub)));
           if (lv) tot += e0 - s0;
           mask |= group_bits<G>(__ballot(lv)) << (u * G);
         }
@@ -1080,7 +1089,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
         }
         vlb = lb;
       } else if (kCert) {
-        pr = fminf(pr, cdown(lb));
+        b2 = fminf(b2, cdown(lb));
       }
     } else if (own && s == 0 && oc_out) {
       *oc_out = uint4{0u, 0x80000000u, 0u, 0u};  // no entry
@@ -1094,7 +1103,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     // the argmin on (d^2, tie key) does not depend on the folding order
     const bool small = vc != 0 && vc <= (uint32_t)kSmallCell && vlb <= best;
     // (a probed small cell the warm bound has since pruned: its records stay unexamined)
-    if (kCert && vc != 0 && vc <= (uint32_t)kSmallCell && !(vlb <= best)) pr = fminf(pr, cdown(vlb));
+    if (kCert && vc != 0 && vc <= (uint32_t)kSmallCell && !(vlb <= best)) b2 = fminf(b2, cdown(vlb));
     if (small) {
       const uint32_t rk = srank_s(s);
       double4 pr[kSmallCell];
@@ -1113,7 +1122,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       live &= live - 1;
       const double lb = __shfl(vlb, l, G);
       if (lb > best) {  // best is group-uniform here
-        if (kCert) pr = fminf(pr, cdown(lb));
+        if (kCert) b2 = fminf(b2, cdown(lb));
         continue;
       }
       const uint32_t cnt = __shfl(vc, l, G);
@@ -1141,7 +1150,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
       const int s = 1 + u * G + g;
       const double slb = inr && s <= nsh ? shift_lb(s) : INFINITY;
       const bool ad = inr && s <= nsh && slb <= best;
-      if (kCert && !ad) pr = fminf(pr, cdown(slb));
+      if (kCert && !ad) b2 = fminf(b2, cdown(slb));
       const uint64_t b = group_bits<G>(__ballot(ad));
       const int bit = u * G;
       if (bit < 64) m0 |= b << bit;
@@ -1291,7 +1300,7 @@ __device__ __forceinline__ void nn_search(const MatchArgs& a, const MapView& M, 
     }
   }
   if constexpr (kCert) {
-    float v = fminf(b2, pr);
+    float v = b2;
 #pragma unroll
     for (int o = 1; o < G; o <<= 1) v = fminf(v, __shfl_xor(v, o, G));
     if (b2_out) *b2_out = fminf(v, cdown(a.bound));  // records beyond the search bound were never examined
@@ -1382,6 +1391,64 @@ __device__ __forceinline__ void fz_stage_mfma(double* __restrict__ rows, const d
   __builtin_amdgcn_wave_barrier();
 }
 
+// The result of query q (one lane): the match moved back to its scan's frame
+// (matcher.hpp:92-96), acceptance (:103-105), insert decision (map.tpp:160-163); the
+// query-order outputs are stored, the insert flag returned and the pair (-1: none) set.
+__device__ __forceinline__ bool match_result(const MatchArgs& a, const MapView& M, bool planar, uint32_t q, double best,
+                                             uint32_t best_i, uint32_t sg, const double* __restrict__ inv_poses,
+                                             int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
+                                             double4* __restrict__ m_pi, double4* __restrict__ m_ni,
+                                             uint8_t* __restrict__ m_ins, int32_t& pair_out) {
+  const bool found = best_i != 0xFFFFFFFFu;
+  int32_t pair = -1;
+  double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
+  if (found) {
+    // the record, its normal and its segment's inverse pose in flight together (the
+    // segment came with the argmin)
+    const double4 p = rec_at(M.pos, best_i, M.rsh);
+    const double4 n = planar ? rec_at(M.nrm, best_i, M.rsh) : make_double4(0, 0, 0, 0);
+    const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
+    double o[3];
+    d_xform(Ti, p.x, p.y, p.z, o);
+    pi = make_double4(o[0], o[1], o[2], 0.0);
+    if (planar) {
+      d_rot(Ti, n.x, n.y, n.z, o);
+      ni = make_double4(o[0], o[1], o[2], 0.0);
+    }
+    if (best < a.max_d2) pair = (int32_t)sg;
+  }
+  const uint32_t gq = planar ? q : a.nq_pl + q;
+  m_pair[gq] = pair;
+  m_d2[gq] = found ? best : DBL_MAX;
+  m_pi[gq] = pi;
+  if (planar) m_ni[q] = ni;
+  const bool ins = !found || best > a.min_d2;
+  m_ins[gq] = ins ? 1 : 0;
+  if (a.rec) a.rec[gq] = best_i;  // the next match's warm start
+  pair_out = pair;
+  return ins;
+}
+
+// The last block's bookkeeping of a match (every block's counts are in): the pair
+// counts (counts mode, zeroing mcnt), the per-block insert counts scanned into k_insert
+// offsets + totals, the tiled pair sort's tail.
+__device__ inline void match_tail(const MatchArgs& a, uint32_t* __restrict__ mcnt, uint32_t* __restrict__ host_counts,
+                                  uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off,
+                                  uint32_t* __restrict__ thist, const SortOut& so) {
+  if (!a.sorted)
+    for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
+      host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  __shared__ uint32_t ws[kMatchThreads / kWave];
+  for (int tt = 0; tt < 2; ++tt) {  // planar blocks [0, nb_pl), point blocks [nb_pl, nb)
+    const uint32_t b0 = tt == 0 ? 0u : a.nb_pl, n = tt == 0 ? a.nb_pl : a.nb_pt;
+    const uint32_t tot = block_scan_runs<8>(
+        n, 0u, [&](uint32_t i) { return __hip_atomic_load(ins_blk + b0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); },
+        [&](uint32_t i, uint32_t o) { ins_off[b0 + i] = o; }, ws);
+    if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, tot);
+  }
+  if (a.sorted && a.tiles) pair_sort_tail(a, thist, so, host_counts);
+}
+
 template <bool DENSE, bool FUSED = false>
 __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
@@ -1398,8 +1465,8 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   extern __shared__ uint32_t s_hist[];  // [K]
   const double* Tj = a.Tj;
   const bool planar = blockIdx.x < a.nb_pl;
-  const uint32_t qb = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) * kQPB;  // the block's first query
-  const uint32_t qi = qb + threadIdx.x / kGroup;
+  const uint32_t bt = planar ? blockIdx.x : blockIdx.x - a.nb_pl;  // the block's index in its type
+  const uint32_t qi = bt * kQPB + threadIdx.x / kGroup;  // the block's first query + the group
   const int g = threadIdx.x % kGroup;
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
   const MapView& M = planar ? mp : mt;
@@ -1414,35 +1481,9 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     const float4 lq = planar ? q_pl[q] : q_pt[q];
     d_xform(Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
   };
-  // the query's result (one lane): the match moved back to its scan's frame
-  // (matcher.hpp:92-96), acceptance (:103-105), insert decision (map.tpp:160-163)
   auto emit = [&](uint32_t q, double best, uint32_t best_i, uint32_t sg) {
-    const bool found = best_i != 0xFFFFFFFFu;
-    int32_t pair = -1;
-    double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
-    if (found) {
-      // the record, its normal and its segment's inverse pose in flight together (the
-      // segment came with the argmin)
-      const double4 p = rec_at(M.pos, best_i, M.rsh);
-      const double4 n = planar ? rec_at(M.nrm, best_i, M.rsh) : make_double4(0, 0, 0, 0);
-      const double* Ti = inv_poses + 12 * sg;  // match.point.transform_in_place(pose.inverse()), matcher.hpp:95
-      double o[3];
-      d_xform(Ti, p.x, p.y, p.z, o);
-      pi = make_double4(o[0], o[1], o[2], 0.0);
-      if (planar) {
-        d_rot(Ti, n.x, n.y, n.z, o);
-        ni = make_double4(o[0], o[1], o[2], 0.0);
-      }
-      if (best < a.max_d2) pair = (int32_t)sg;
-    }
-    const uint32_t gq = planar ? q : a.nq_pl + q;
-    m_pair[gq] = pair;
-    m_d2[gq] = found ? best : DBL_MAX;
-    m_pi[gq] = pi;
-    if (planar) m_ni[q] = ni;
-    const bool ins = !found || best > a.min_d2;
-    m_ins[gq] = ins ? 1 : 0;
-    if (a.rec) a.rec[gq] = best_i;  // the next match's warm start
+    int32_t pair;
+    const bool ins = match_result(a, M, planar, q, best, best_i, sg, inv_poses, m_pair, m_d2, m_pi, m_ni, m_ins, pair);
     if (ins) atomicAdd(&s_ins, 1u);
     if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
   };
@@ -1473,7 +1514,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     constexpr bool kWarm = FMX_WARM_START && !FUSED;
     uint4 ocv = uint4{0u, 0x80000000u, 0u, 0u};
     if (kWarm && a.warm && a.cell) ocv = a.cell[gq];
-    uint32_t warm_r = 0xFFFFFFFFu;
+    [[maybe_unused]] uint32_t warm_r = 0xFFFFFFFFu;
     if (kWarm && a.warm) {
       const uint32_t r = a.warm[gq];
       warm_r = r;
@@ -1487,7 +1528,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         // own cell: same 27 cells); its NN then had distance d1 and every other
         // candidate >= sqrt(B2), so if sqrt(B2) - delta > d1 + delta the NN is unchanged
         // (strictly: no tie), and the search would return it again
-        if (a.cert_b2 && a.rings == 1 && !FUSED && kGroup > 1) {
+        if (FMX_CERT_DIAG && a.cert_b2 && a.rings == 1 && !FUSED && kGroup > 1) {
           const float4 lq = planar ? q_pl[qi] : q_pt[qi];
           double wo[3];
           d_xform(a.Tprev, (double)lq.x, (double)lq.y, (double)lq.z, wo);
@@ -1500,21 +1541,10 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
                             (int)floor(wo[2] / a.w) == cz;
           const double rb = sqrt((double)a.cert_b2[gq]) - delta;
           cert_q = same && rb > sqrt(d1o) + delta + 1e-7;
-#if FMX_WARM_CERT
-          if (cert_q) {  // settled: the NN at the new pose, and the bound carried forward
-            best = d2;
-            best_i = r;
-            best_sg = (uint32_t)(tag_bits(p.w) >> 32);
-            b2q = cdown(rb * rb);
-          }
-#endif
         }
 #endif
       }
     }
-#if FMX_WARM_CERT
-    if (!cert_q)
-#endif
     nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, best_sg, n_probe,
                              n_cand, n_iter, n_list, warm_b,
 #ifdef FMX_DIAG_PHASE
@@ -1755,20 +1785,194 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     s_last = __hip_atomic_fetch_add(mticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  if (!a.sorted)
-    for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
-      host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  __shared__ uint32_t ws[kMatchThreads / kWave];
-  for (int tt = 0; tt < 2; ++tt) {  // planar blocks [0, nb_pl), point blocks [nb_pl, nb)
-    const uint32_t b0 = tt == 0 ? 0u : a.nb_pl, n = tt == 0 ? a.nb_pl : a.nb_pt;
-    const uint32_t tot = block_scan_runs<8>(
-        n, 0u, [&](uint32_t i) { return __hip_atomic_load(ins_blk + b0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); },
-        [&](uint32_t i, uint32_t o) { ins_off[b0 + i] = o; }, ws);
-    if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, tot);
-  }
-  if (a.sorted && a.tiles) pair_sort_tail(a, thist, so, host_counts);
+  match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+#if FMX_WARM_CERT && FMX_MATCH_GROUP == 8
+// The warm certificate, first launch of a split warm match (one lane per query,
+// kCertQ queries of one type per block = kCertQ / kQPB of k_match's blocks, its "home
+// blocks", all in one pair-sort tile).  A query whose own cell is unchanged since the
+// previous match (the same 27 cells are searched) and whose previous NN r at distance
+// d1 beats every other candidate by more than twice the query's move delta,
+// sqrt(B2) - delta > d1 + delta, keeps r: its result is settled here and its bound
+// carried forward as (sqrt(B2) - delta)^2.  Every other query is listed (qlist) for
+// k_match_list.  Home-block insert counts are STORED (the list launch adds to them),
+// pair counts go to the tiles (tiled sort) or mcnt (counts only).
+constexpr int kCertQ = 256;
+static_assert(kTileQ % kCertQ == 0 && kCertQ % kQPB == 0, "a certifying block covers whole home blocks of one tile");
+__global__ __launch_bounds__(kCertQ) void k_match_cert(MatchArgs a, MapView mp, MapView mt, const float4* __restrict__ q_pl,
+                                                       const float4* __restrict__ q_pt,
+                                                       const double* __restrict__ inv_poses, int32_t* __restrict__ m_pair,
+                                                       double* __restrict__ m_d2, double4* __restrict__ m_pi,
+                                                       double4* __restrict__ m_ni, uint8_t* __restrict__ m_ins,
+                                                       uint32_t* __restrict__ work, uint32_t* __restrict__ mcnt,
+                                                       uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ thist,
+                                                       uint32_t ncb_pl) {
+  extern __shared__ uint32_t s_hist[];  // [K]
+  constexpr int kHome = kCertQ / kQPB;
+  __shared__ uint32_t s_ins[kHome], s_cert[kHome], s_warm[kHome];
+  __shared__ uint32_t s_nl, s_lb;
+  __shared__ uint32_t s_list[kCertQ];
+  const bool planar = blockIdx.x < ncb_pl;
+  const uint32_t bt = planar ? blockIdx.x : blockIdx.x - ncb_pl;
+  const uint32_t q = bt * kCertQ + threadIdx.x;
+  const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
+  const MapView& M = planar ? mp : mt;
+  for (int k = threadIdx.x; k < a.K; k += kCertQ) s_hist[k] = 0;
+  if (threadIdx.x < kHome) s_ins[threadIdx.x] = s_cert[threadIdx.x] = s_warm[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_nl = 0;
+  __syncthreads();
+  const uint32_t t_begin = (uint32_t)wall_clock64();
+  const int hl = threadIdx.x / kQPB;  // the query's home block in this block
+  if (q < nq) {
+    const uint32_t gq = planar ? q : a.nq_pl + q;
+    const uint32_t r = a.warm[gq];
+    bool cert = false;
+    if (r != 0xFFFFFFFFu) {
+      atomicAdd(&s_warm[hl], 1u);
+      const float4 lq = planar ? q_pl[q] : q_pt[q];
+      const double4 p = rec_at(M.pos, r, M.rsh);
+      const float b2 = a.cert_b2[gq];
+      double wq[3], wo[3];
+      d_xform(a.Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);
+      d_xform(a.Tprev, (double)lq.x, (double)lq.y, (double)lq.z, wo);
+      const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
+      const double d2 = (dx * dx + dz * dz) + dy * dy;  // as fold computes it
+      const double ex = wo[0] - p.x, ey = wo[1] - p.y, ez = wo[2] - p.z;
+      const double d1o = (ex * ex + ez * ez) + ey * ey;
+      const double mx = wq[0] - wo[0], my = wq[1] - wo[1], mz = wq[2] - wo[2];
+      const double delta = sqrt(mx * mx + my * my + mz * mz);
+      const bool same = (int)floor(wo[0] / a.w) == (int)floor(wq[0] / a.w) &&
+                        (int)floor(wo[1] / a.w) == (int)floor(wq[1] / a.w) &&
+                        (int)floor(wo[2] / a.w) == (int)floor(wq[2] / a.w);
+      const double rb = sqrt((double)b2) - delta;
+      // (the search keeps a record only within the launch's bound: d2 <= bound)
+      cert = same && d2 <= a.bound && rb > sqrt(d1o) + delta + 1e-7;
+      if (cert) {
+        atomicAdd(&s_cert[hl], 1u);
+        int32_t pair;
+        const bool ins = match_result(a, M, planar, q, d2, r, (uint32_t)(tag_bits(p.w) >> 32), inv_poses, m_pair, m_d2,
+                                      m_pi, m_ni, m_ins, pair);
+        if (ins) atomicAdd(&s_ins[hl], 1u);
+        if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
+        a.cert_b2[gq] = cdown(rb * rb);  // every other candidate at the new pose
+      }
+    }
+    if (!cert) s_list[atomicAdd(&s_nl, 1u)] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_nl)
+    s_lb = __hip_atomic_fetch_add(a.qlist_n + (planar ? 0 : 1), s_nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (threadIdx.x < s_nl) a.qlist[(planar ? 0u : a.nq_pl) + s_lb + threadIdx.x] = s_list[threadIdx.x];
+  const uint32_t nbt = planar ? a.nb_pl : a.nb_pt;
+  if (threadIdx.x < kHome && bt * kHome + threadIdx.x < nbt) {
+    const uint32_t hb = (planar ? 0u : a.nb_pl) + bt * kHome + threadIdx.x;
+    ins_blk[hb] = s_ins[threadIdx.x];
+    uint4* w4 = reinterpret_cast<uint4*>(work) + 2 * hb;  // k_match's words (the list launch adds its work)
+    w4[0] = make_uint4(0u, 0u, 0u, s_cert[threadIdx.x]);
+    w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), 0u, s_warm[threadIdx.x]);
+  }
+  if (a.sorted && a.tiles) {
+    const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.ntl_pl;
+    const uint32_t ntl = planar ? a.ntl_pl : a.ntl_pt;
+    const uint32_t tile = bt * kCertQ / kTileQ;
+    for (int k = threadIdx.x; k < a.K; k += kCertQ)
+      if (s_hist[k])
+        __hip_atomic_fetch_add(thist + hbase + (size_t)k * ntl + tile, s_hist[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    for (int k = threadIdx.x; k < a.K; k += kCertQ)
+      if (s_hist[k])
+        __hip_atomic_fetch_add(mcnt + (size_t)(planar ? 0 : 1) * a.K + k, s_hist[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+#endif
+
+#if FMX_WARM_CERT && FMX_MATCH_GROUP == 64
+// The warm certificate, second launch: the listed (uncertified) queries of a split warm
+// match, one wave per query (a dense cell's records or the 26 ring cells in one round
+// of 64 lanes: these are the matches' slow queries), grid-stride over the list (planar
+// entries, then point entries).  Per query the same search as k_match (warm bound,
+// own-cell cache, second-best bound for the next certificate); its insert flag and pair
+// count go to its home block / tile of the g8 layout (home_qpb queries per block), its
+// probes and candidates to the home block's work words.  The last block reads the lists'
+// counts back to zero and runs the match's bookkeeping tail.
+template <bool DENSE>
+__global__ __launch_bounds__(kMatchThreads) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_match_list(
+    MatchArgs a, MapView mp, MapView mt, const float4* __restrict__ q_pl, const float4* __restrict__ q_pt,
+    const double* __restrict__ inv_poses, int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
+    double4* __restrict__ m_pi, double4* __restrict__ m_ni, uint8_t* __restrict__ m_ins, uint32_t* __restrict__ work,
+    uint32_t* __restrict__ mcnt, uint32_t* __restrict__ mticket, uint32_t* __restrict__ host_counts,
+    uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off, uint32_t* __restrict__ thist, SortOut so,
+    uint32_t home_qpb) {
+  static_assert(kGroup == kWave, "one wave per listed query");
+  __shared__ uint32_t s_hdr[DENSE ? kQPB : 1][kSubCells];
+  const uint32_t n_pl = __hip_atomic_load(a.qlist_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n_all = n_pl + __hip_atomic_load(a.qlist_n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int g = lane_id();
+  const uint32_t slot = threadIdx.x / kWave;
+  for (uint32_t e = blockIdx.x * kQPB + slot; e < n_all; e += gridDim.x * kQPB) {  // wave-uniform
+    const bool planar = e < n_pl;
+    const uint32_t qi = a.qlist[planar ? e : a.nq_pl + (e - n_pl)];
+    const MapView& M = planar ? mp : mt;
+    const uint32_t gq = planar ? qi : a.nq_pl + qi;
+    const float4 lq = planar ? q_pl[qi] : q_pt[qi];
+    double wq[3];
+    d_xform(a.Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);
+    double warm_b = INFINITY;
+    const uint4 ocv = a.cell ? a.cell[gq] : uint4{0u, 0x80000000u, 0u, 0u};
+    const uint32_t r = a.warm[gq];
+    if (r != 0xFFFFFFFFu) {
+      const double4 p = rec_at(M.pos, r, M.rsh);
+      const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
+      const double d2 = (dx * dx + dz * dz) + dy * dy;
+      if (d2 <= a.warm_lim) warm_b = d2;
+    }
+    double best = a.bound;
+    uint32_t best_rid = 0xFFFFFFFFu, best_i = 0xFFFFFFFFu, best_sg = 0;
+    uint32_t n_probe = 0, n_cand = 0, n_iter = 0, n_list = 0;
+    float b2q = INFINITY;
+    nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? slot : 0], best, best_rid, best_i, best_sg, n_probe, n_cand,
+                             n_iter, n_list, warm_b, nullptr, ocv, a.cell && g == 0 ? a.cell + gq : nullptr, &b2q);
+    const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
+    if (g == 0) {
+      a.cert_b2[gq] = b2q;
+      int32_t pair;
+      const bool ins = match_result(a, M, planar, qi, best, best_i, best_sg, inv_poses, m_pair, m_d2, m_pi, m_ni, m_ins,
+                                    pair);
+      const uint32_t hb = (planar ? 0u : a.nb_pl) + qi / home_qpb;
+      if (ins) __hip_atomic_fetch_add(ins_blk + hb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pair >= 0) {
+        if (a.sorted && a.tiles)
+          __hip_atomic_fetch_add(thist + (planar ? (size_t)0 : (size_t)a.K * a.ntl_pl) +
+                                     (size_t)pair * (planar ? a.ntl_pl : a.ntl_pt) + qi / kTileQ,
+                                 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_fetch_add(mcnt + (size_t)(planar ? 0 : 1) * a.K + pair, 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t* w = work + kWorkWords * (size_t)hb;
+      atomicAdd(w + 0, wp);
+      atomicAdd(w + 1, wc);
+      atomicMax(w + 2, wc);
+      atomicMax(w + 5, (uint32_t)wall_clock64());
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int s_last;
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(mticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x < 2)  // every block read the counts before its ticket
+    __hip_atomic_store(a.qlist_n + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
+  if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
 
 struct HistIn {
   const uint32_t* h;
@@ -2215,6 +2419,20 @@ static bool no_warm() {
   static const bool v = std::getenv("FMX_NO_WARM") != nullptr;
   return v;
 }
+// FMX_NO_CERT_SPLIT (A/B, FMX_WARM_CERT builds): warm matches in one launch (no certificate)
+[[maybe_unused]] static bool no_cert_split() {
+  static const bool v = std::getenv("FMX_NO_CERT_SPLIT") != nullptr;
+  return v;
+}
+// FMX_LIST_GRID (FMX_WARM_CERT builds): blocks of the listed-query launch (4 waves each)
+[[maybe_unused]] static uint32_t list_grid() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("FMX_LIST_GRID");
+    const long n = e ? std::atol(e) : 0;
+    return n > 0 ? (uint32_t)n : 1024u;
+  }();
+  return v;
+}
 static bool no_cell_cache() {
   static const bool v = std::getenv("FMX_NO_CELL_CACHE") != nullptr;
   return v;
@@ -2257,6 +2475,10 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     std::memcpy(c->cert_pose, a.Tj, sizeof(a.Tj));
 #endif
   }
+#if FMX_WARM_CERT
+  a.qlist = nullptr;
+  a.qlist_n = nullptr;
+#endif
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
@@ -2321,11 +2543,32 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   }
   if (nb > 0) {
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
-    hipLaunchKernelGGL(dense ? k_match<true> : k_match<false>, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a, view(0), view(1),
-                       c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
-                       c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d,
-                       c->ins_blk.p, c->ins_off.p, c->thist.p, so, FusedArgs{});
-    FMX_HIP(hipGetLastError());
+    bool split = false;
+#if FMX_WARM_CERT && FMX_MATCH_GROUP == 8
+    // a warm match on a plain map (one ring), tiled or counts-only bookkeeping: certify
+    // first (one lane per query), then search only the queries left (one wave each)
+    split = a.warm && a.cert_b2 && a.rings == 1 && (a.tiles || !a.sorted) && !no_cert_split();
+    if (split) {
+      c->qlist.ensure(nq + 1);
+      ensure_zeroed(c->qlist_n, 2, st);
+      a.qlist = c->qlist.p;
+      a.qlist_n = c->qlist_n.p;
+      const uint32_t ncb_pl = (c->n_qpl + kCertQ - 1) / kCertQ, ncb_pt = (c->n_qpt + kCertQ - 1) / kCertQ;
+      hipLaunchKernelGGL(k_match_cert, dim3(ncb_pl + ncb_pt), dim3(kCertQ), K * sizeof(uint32_t), st, a, view(0),
+                         view(1), c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
+                         c->m_ni.p, c->m_ins.p, c->work.p, c->mcnt.p, c->ins_blk.p, c->thist.p, ncb_pl);
+      FMX_HIP(hipGetLastError());
+      g64::launch_match_list(c, &a, sizeof(a), dense, st, list_grid(), kQPB);
+    }
+#endif
+    if (!split) {
+      auto kern = dense ? k_match<true> : k_match<false>;
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a,
+                         view(0), view(1), c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
+                         c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d,
+                         c->ins_blk.p, c->ins_off.p, c->thist.p, so, FusedArgs{});
+      FMX_HIP(hipGetLastError());
+    }
   }
   // no queries: no launch, so zero the counts and insert totals the kernel would write
   if (nb == 0) FMX_HIP(hipMemsetAsync(c->h_counts.d, 0, (2 * (size_t)c->K + 2) * sizeof(uint32_t), st));
@@ -2369,6 +2612,28 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->have_corr = sorted;  // pair-major correspondences for fmx_linearize
   c->have_qo = true;      // query-order correspondences for register_scan
 }
+
+#if FMX_WARM_CERT && FMX_MATCH_GROUP == 64
+// The listed-query launch of a split warm match (g8::run_match; the arguments are g8's
+// MatchArgs, the same layout in every build of this file).
+void launch_match_list(fmx_ctx* c, const void* args, size_t args_size, bool dense, hipStream_t st, uint32_t grid,
+                       uint32_t home_qpb) {
+  if (args_size != sizeof(MatchArgs)) throw StatusError(FMX_E_STATE, "launch_match_list: MatchArgs layouts differ");
+  MatchArgs a;
+  std::memcpy(&a, args, sizeof(a));
+  auto view = [&](int t) {
+    VoxMap& M = c->map;
+    return MapView{reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
+                   M.pos.p, M.nrm_p, M.epoch, M.rsh};
+  };
+  const SortOut so{c->hist_off.p, c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p};
+  hipLaunchKernelGGL(dense ? k_match_list<true> : k_match_list<false>, dim3(grid), dim3(kMatchThreads), 0, st, a, view(0),
+                     view(1), c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p, c->m_ni.p,
+                     c->m_ins.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d, c->ins_blk.p, c->ins_off.p,
+                     c->thist.p, so, home_qpb);
+  FMX_HIP(hipGetLastError());
+}
+#endif
 
 // The match at pose_j fused with its single-pose linearization (k_match<.., FUSED>):
 // the summed 7 x 7 + error to dst (28 + 1 doubles), completion word `flag` (null: none).

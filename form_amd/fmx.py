@@ -360,7 +360,10 @@ class Context:
             self._chk(self._L.fmx_next_scan(self.h, None, C.c_size_t(0), C.c_int(0)))
             return
         on_dev, ptr, n, keep = _scan_ptr(scan)
-        if keep is not scan:  # a converted copy would not be the object later registered
+        # a converted copy would not be the memory later registered
+        same = (keep is scan) if not isinstance(scan, np.ndarray) else (
+            keep.__array_interface__["data"][0] == scan.__array_interface__["data"][0])
+        if not same:
             raise ValueError("next_scan needs a contiguous (N, 4) float32 array or tensor")
         self._chk(self._L.fmx_next_scan(self.h, ptr, C.c_size_t(n), C.c_int(on_dev)))
         # the tensor must outlive the extraction queued for it

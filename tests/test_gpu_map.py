@@ -224,7 +224,7 @@ def test_dense_cells_warm_from_cell_cache(fmx_mod, oracle):
                     for k, (pl, _) in enumerate(scans)])
     cells, cnt = np.unique(np.floor(wp / w).astype(np.int64), axis=0, return_counts=True)
     dense = {tuple(c) for c in cells[cnt > 128]}
-    assert sum(tuple(c) in dense for c in np.floor(qpl[:, :3].astype(np.float64) / w).astype(np.int64)) > 3000
+    assert sum(tuple(c) in dense for c in np.floor(qpl[:, :3].astype(np.float64) / w).astype(np.int64)) > 2000
 
     def match_cmp(Tj):
         cpl, cpt = ctx.match(Tj, w)
