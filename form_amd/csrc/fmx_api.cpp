@@ -1418,7 +1418,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
   c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release();
-  c->cert_b2.release(); c->qlist.release(); c->qlist_n.release();
+  c->cert_b2.release();
   {
     auto& S = c->spec;
     S.m_pair.release(); S.m_d2.release(); S.m_pi.release(); S.m_ni.release(); S.m_ins.release();

@@ -380,8 +380,8 @@ struct fmx_ctx {
   uint64_t warm_rec_gen = 0;  // warm_gen when m_rec was last written (0: never)
   fmx::DBuf<uint32_t> thist;  // tiled pair sort: per-(type, pair, tile) counts, self-resetting
   fmx::DBuf<float> cert_b2;   // FMX_CERT_DIAG / FMX_WARM_CERT builds: per query the last match's second-best bound
-  fmx::DBuf<uint32_t> qlist, qlist_n;  // FMX_WARM_CERT: the uncertified queries of a warm match, per type
   double cert_pose[12] = {};  // ... and that match's pose
+  uint64_t cert_gen = 0;      // warm_gen when cert_b2 was last written by an 8-lane match (0: none)
   bool have_match = false;
 
   // ---- sorted correspondences (pair-major SoA) + chunk table
@@ -689,16 +689,13 @@ inline uint32_t next_flag(fmx_ctx* c) {
   void match_counts_fetch(fmx_ctx* c, bool wait = true);                                             \
   void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* dst, \
                            uint32_t* flag, uint32_t seq);                                              \
-  void work_fetch(fmx_ctx* c);                                                                       \
-  void launch_match_list(fmx_ctx* c, const void* args, size_t args_size, bool dense, hipStream_t st,   \
-                         uint32_t grid, uint32_t home_qpb);
+  void work_fetch(fmx_ctx* c);
 // Windows of at most this many map scans (pairs) use the tiled pair sort; wider ones a
 // per-match-block histogram whose scatter ranks within one wave, so they take the g8
 // build (32 queries per block) whatever the query count.
 constexpr uint32_t kMatchTileMaxPairs = 256;
 namespace g8 { FMX_VM_DECLS }
 namespace gl { FMX_VM_DECLS }
-namespace g64 { FMX_VM_DECLS }  // (FMX_WARM_CERT builds only: the listed-query launch)
 #undef FMX_VM_DECLS
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,

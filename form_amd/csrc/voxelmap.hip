@@ -59,6 +59,15 @@
 #define FMX_MATCH_DEPTH 4
 #endif
 
+#ifndef FMX_CERT_DIAG
+#define FMX_CERT_DIAG 0  // diagnostic build (with FMX_WARM_CERT=0): count the warm queries a certificate settles
+#endif
+#ifndef FMX_WARM_CERT
+#define FMX_WARM_CERT 1  // warm queries whose certificate holds skip the search (A/B switch;
+                         // an FMX_CERT_DIAG build sets it to 0 so that every query is searched)
+#endif
+#define FMX_CERT_ANY (FMX_CERT_DIAG || FMX_WARM_CERT)
+
 namespace fmx {
 // This file is compiled twice (Makefile): FMX_MATCH_GROUP 8 -> fmx::g8 and 1 -> fmx::gl;
 // run_match picks one per launch (fmx_api.cpp, match_group_for).
@@ -500,20 +509,14 @@ struct MatchArgs {
   // per query, its own cell as the last match found it (packed cell coordinates, record
   // range, dense bit; fmx_ctx::m_cell): read when `warm` is set, rewritten with rec
   uint4* cell;
-#if FMX_CERT_DIAG || FMX_WARM_CERT
+#if FMX_CERT_ANY
   // warm certificate (VERDICT r3 "next round" 5): per query the previous match's
   // second-best bound B2 (fp32, never above the truth: every record other than its NN
   // was at d^2 >= B2, or could not be examined), and that match's pose
   float* cert_b2;
   double Tprev[12];
-#endif
-#if FMX_WARM_CERT
-  // a warm match in two launches (k_match_cert, then k_match_list): the first settles
-  // every certified query and lists the others per type (qlist: planar entries from 0,
-  // point entries from nq_pl; qlist_n[2] counts, reset by the second launch's last
-  // block); the second searches the listed queries only and runs the bookkeeping tail
-  uint32_t* qlist;
-  uint32_t* qlist_n;
+  int cert_ok;  // cert_b2 holds the bounds of the match that wrote the warm records
+                // (an 8-lane match on this map and query set; the one-lane build keeps none)
 #endif
 };
 
@@ -680,13 +683,6 @@ __device__ __forceinline__ uint64_t group_bits(uint64_t ballot) {
 #ifndef FMX_F32_BOUNDS
 #define FMX_F32_BOUNDS 1  // cell lower bounds in fp32 from the query's in-cell offset (A/B switch)
 #endif
-#ifndef FMX_CERT_DIAG
-#define FMX_CERT_DIAG 0  // diagnostic build: count the warm queries a second-best certificate settles
-#endif
-#ifndef FMX_WARM_CERT
-#define FMX_WARM_CERT 0  // warm queries whose certificate holds skip the search (A/B switch)
-#endif
-#define FMX_CERT_ANY (FMX_CERT_DIAG || FMX_WARM_CERT)
 #ifndef FMX_WARM_START
 #define FMX_WARM_START 1  // bound each search by the previous match's record (compile-time A/B switch)
 #endif
@@ -1528,7 +1524,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
         // own cell: same 27 cells); its NN then had distance d1 and every other
         // candidate >= sqrt(B2), so if sqrt(B2) - delta > d1 + delta the NN is unchanged
         // (strictly: no tie), and the search would return it again
-        if (FMX_CERT_DIAG && a.cert_b2 && a.rings == 1 && !FUSED && kGroup > 1) {
+        if ((FMX_CERT_DIAG || FMX_WARM_CERT) && a.cert_ok && a.rings == 1 && !FUSED && kGroup > 1) {
           const float4 lq = planar ? q_pl[qi] : q_pt[qi];
           double wo[3];
           d_xform(a.Tprev, (double)lq.x, (double)lq.y, (double)lq.z, wo);
@@ -1541,10 +1537,24 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
                             (int)floor(wo[2] / a.w) == cz;
           const double rb = sqrt((double)a.cert_b2[gq]) - delta;
           cert_q = same && rb > sqrt(d1o) + delta + 1e-7;
+#if FMX_WARM_CERT
+          // one-launch mode: a certified query (group-uniform) takes its previous NN and
+          // skips the search (the search keeps a record only within the bound: d2 <= bound)
+          cert_q = cert_q && d2 <= a.bound;
+          if (cert_q) {
+            best = d2;
+            best_i = r;
+            best_sg = (uint32_t)(tag_bits(p.w) >> 32);
+            b2q = cdown(rb * rb);
+          }
+#endif
         }
 #endif
       }
     }
+#if FMX_WARM_CERT
+    if (!cert_q)
+#endif
     nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? threadIdx.x / kGroup : 0], best, best_rid, best_i, best_sg, n_probe,
                              n_cand, n_iter, n_list, warm_b,
 #ifdef FMX_DIAG_PHASE
@@ -1789,191 +1799,6 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-#if FMX_WARM_CERT && FMX_MATCH_GROUP == 8
-// The warm certificate, first launch of a split warm match (one lane per query,
-// kCertQ queries of one type per block = kCertQ / kQPB of k_match's blocks, its "home
-// blocks", all in one pair-sort tile).  A query whose own cell is unchanged since the
-// previous match (the same 27 cells are searched) and whose previous NN r at distance
-// d1 beats every other candidate by more than twice the query's move delta,
-// sqrt(B2) - delta > d1 + delta, keeps r: its result is settled here and its bound
-// carried forward as (sqrt(B2) - delta)^2.  Every other query is listed (qlist) for
-// k_match_list.  Home-block insert counts are STORED (the list launch adds to them),
-// pair counts go to the tiles (tiled sort) or mcnt (counts only).
-constexpr int kCertQ = 256;
-static_assert(kTileQ % kCertQ == 0 && kCertQ % kQPB == 0, "a certifying block covers whole home blocks of one tile");
-__global__ __launch_bounds__(kCertQ) void k_match_cert(MatchArgs a, MapView mp, MapView mt, const float4* __restrict__ q_pl,
-                                                       const float4* __restrict__ q_pt,
-                                                       const double* __restrict__ inv_poses, int32_t* __restrict__ m_pair,
-                                                       double* __restrict__ m_d2, double4* __restrict__ m_pi,
-                                                       double4* __restrict__ m_ni, uint8_t* __restrict__ m_ins,
-                                                       uint32_t* __restrict__ work, uint32_t* __restrict__ mcnt,
-                                                       uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ thist,
-                                                       uint32_t ncb_pl) {
-  extern __shared__ uint32_t s_hist[];  // [K]
-  constexpr int kHome = kCertQ / kQPB;
-  __shared__ uint32_t s_ins[kHome], s_cert[kHome], s_warm[kHome];
-  __shared__ uint32_t s_nl, s_lb;
-  __shared__ uint32_t s_list[kCertQ];
-  const bool planar = blockIdx.x < ncb_pl;
-  const uint32_t bt = planar ? blockIdx.x : blockIdx.x - ncb_pl;
-  const uint32_t q = bt * kCertQ + threadIdx.x;
-  const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
-  const MapView& M = planar ? mp : mt;
-  for (int k = threadIdx.x; k < a.K; k += kCertQ) s_hist[k] = 0;
-  if (threadIdx.x < kHome) s_ins[threadIdx.x] = s_cert[threadIdx.x] = s_warm[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_nl = 0;
-  __syncthreads();
-  const uint32_t t_begin = (uint32_t)wall_clock64();
-  const int hl = threadIdx.x / kQPB;  // the query's home block in this block
-  if (q < nq) {
-    const uint32_t gq = planar ? q : a.nq_pl + q;
-    const uint32_t r = a.warm[gq];
-    bool cert = false;
-    if (r != 0xFFFFFFFFu) {
-      atomicAdd(&s_warm[hl], 1u);
-      const float4 lq = planar ? q_pl[q] : q_pt[q];
-      const double4 p = rec_at(M.pos, r, M.rsh);
-      const float b2 = a.cert_b2[gq];
-      double wq[3], wo[3];
-      d_xform(a.Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);
-      d_xform(a.Tprev, (double)lq.x, (double)lq.y, (double)lq.z, wo);
-      const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
-      const double d2 = (dx * dx + dz * dz) + dy * dy;  // as fold computes it
-      const double ex = wo[0] - p.x, ey = wo[1] - p.y, ez = wo[2] - p.z;
-      const double d1o = (ex * ex + ez * ez) + ey * ey;
-      const double mx = wq[0] - wo[0], my = wq[1] - wo[1], mz = wq[2] - wo[2];
-      const double delta = sqrt(mx * mx + my * my + mz * mz);
-      const bool same = (int)floor(wo[0] / a.w) == (int)floor(wq[0] / a.w) &&
-                        (int)floor(wo[1] / a.w) == (int)floor(wq[1] / a.w) &&
-                        (int)floor(wo[2] / a.w) == (int)floor(wq[2] / a.w);
-      const double rb = sqrt((double)b2) - delta;
-      // (the search keeps a record only within the launch's bound: d2 <= bound)
-      cert = same && d2 <= a.bound && rb > sqrt(d1o) + delta + 1e-7;
-      if (cert) {
-        atomicAdd(&s_cert[hl], 1u);
-        int32_t pair;
-        const bool ins = match_result(a, M, planar, q, d2, r, (uint32_t)(tag_bits(p.w) >> 32), inv_poses, m_pair, m_d2,
-                                      m_pi, m_ni, m_ins, pair);
-        if (ins) atomicAdd(&s_ins[hl], 1u);
-        if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
-        a.cert_b2[gq] = cdown(rb * rb);  // every other candidate at the new pose
-      }
-    }
-    if (!cert) s_list[atomicAdd(&s_nl, 1u)] = q;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && s_nl)
-    s_lb = __hip_atomic_fetch_add(a.qlist_n + (planar ? 0 : 1), s_nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (threadIdx.x < s_nl) a.qlist[(planar ? 0u : a.nq_pl) + s_lb + threadIdx.x] = s_list[threadIdx.x];
-  const uint32_t nbt = planar ? a.nb_pl : a.nb_pt;
-  if (threadIdx.x < kHome && bt * kHome + threadIdx.x < nbt) {
-    const uint32_t hb = (planar ? 0u : a.nb_pl) + bt * kHome + threadIdx.x;
-    ins_blk[hb] = s_ins[threadIdx.x];
-    uint4* w4 = reinterpret_cast<uint4*>(work) + 2 * hb;  // k_match's words (the list launch adds its work)
-    w4[0] = make_uint4(0u, 0u, 0u, s_cert[threadIdx.x]);
-    w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), 0u, s_warm[threadIdx.x]);
-  }
-  if (a.sorted && a.tiles) {
-    const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.ntl_pl;
-    const uint32_t ntl = planar ? a.ntl_pl : a.ntl_pt;
-    const uint32_t tile = bt * kCertQ / kTileQ;
-    for (int k = threadIdx.x; k < a.K; k += kCertQ)
-      if (s_hist[k])
-        __hip_atomic_fetch_add(thist + hbase + (size_t)k * ntl + tile, s_hist[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    for (int k = threadIdx.x; k < a.K; k += kCertQ)
-      if (s_hist[k])
-        __hip_atomic_fetch_add(mcnt + (size_t)(planar ? 0 : 1) * a.K + k, s_hist[k], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-#endif
-
-#if FMX_WARM_CERT && FMX_MATCH_GROUP == 64
-// The warm certificate, second launch: the listed (uncertified) queries of a split warm
-// match, one wave per query (a dense cell's records or the 26 ring cells in one round
-// of 64 lanes: these are the matches' slow queries), grid-stride over the list (planar
-// entries, then point entries).  Per query the same search as k_match (warm bound,
-// own-cell cache, second-best bound for the next certificate); its insert flag and pair
-// count go to its home block / tile of the g8 layout (home_qpb queries per block), its
-// probes and candidates to the home block's work words.  The last block reads the lists'
-// counts back to zero and runs the match's bookkeeping tail.
-template <bool DENSE>
-__global__ __launch_bounds__(kMatchThreads) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_match_list(
-    MatchArgs a, MapView mp, MapView mt, const float4* __restrict__ q_pl, const float4* __restrict__ q_pt,
-    const double* __restrict__ inv_poses, int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
-    double4* __restrict__ m_pi, double4* __restrict__ m_ni, uint8_t* __restrict__ m_ins, uint32_t* __restrict__ work,
-    uint32_t* __restrict__ mcnt, uint32_t* __restrict__ mticket, uint32_t* __restrict__ host_counts,
-    uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off, uint32_t* __restrict__ thist, SortOut so,
-    uint32_t home_qpb) {
-  static_assert(kGroup == kWave, "one wave per listed query");
-  __shared__ uint32_t s_hdr[DENSE ? kQPB : 1][kSubCells];
-  const uint32_t n_pl = __hip_atomic_load(a.qlist_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t n_all = n_pl + __hip_atomic_load(a.qlist_n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int g = lane_id();
-  const uint32_t slot = threadIdx.x / kWave;
-  for (uint32_t e = blockIdx.x * kQPB + slot; e < n_all; e += gridDim.x * kQPB) {  // wave-uniform
-    const bool planar = e < n_pl;
-    const uint32_t qi = a.qlist[planar ? e : a.nq_pl + (e - n_pl)];
-    const MapView& M = planar ? mp : mt;
-    const uint32_t gq = planar ? qi : a.nq_pl + qi;
-    const float4 lq = planar ? q_pl[qi] : q_pt[qi];
-    double wq[3];
-    d_xform(a.Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);
-    double warm_b = INFINITY;
-    const uint4 ocv = a.cell ? a.cell[gq] : uint4{0u, 0x80000000u, 0u, 0u};
-    const uint32_t r = a.warm[gq];
-    if (r != 0xFFFFFFFFu) {
-      const double4 p = rec_at(M.pos, r, M.rsh);
-      const double dx = p.x - wq[0], dy = p.y - wq[1], dz = p.z - wq[2];
-      const double d2 = (dx * dx + dz * dz) + dy * dy;
-      if (d2 <= a.warm_lim) warm_b = d2;
-    }
-    double best = a.bound;
-    uint32_t best_rid = 0xFFFFFFFFu, best_i = 0xFFFFFFFFu, best_sg = 0;
-    uint32_t n_probe = 0, n_cand = 0, n_iter = 0, n_list = 0;
-    float b2q = INFINITY;
-    nn_search<kGroup, DENSE>(a, M, wq, g, s_hdr[DENSE ? slot : 0], best, best_rid, best_i, best_sg, n_probe, n_cand,
-                             n_iter, n_list, warm_b, nullptr, ocv, a.cell && g == 0 ? a.cell + gq : nullptr, &b2q);
-    const uint32_t wp = wave_sum(n_probe), wc = wave_sum(n_cand);
-    if (g == 0) {
-      a.cert_b2[gq] = b2q;
-      int32_t pair;
-      const bool ins = match_result(a, M, planar, qi, best, best_i, best_sg, inv_poses, m_pair, m_d2, m_pi, m_ni, m_ins,
-                                    pair);
-      const uint32_t hb = (planar ? 0u : a.nb_pl) + qi / home_qpb;
-      if (ins) __hip_atomic_fetch_add(ins_blk + hb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (pair >= 0) {
-        if (a.sorted && a.tiles)
-          __hip_atomic_fetch_add(thist + (planar ? (size_t)0 : (size_t)a.K * a.ntl_pl) +
-                                     (size_t)pair * (planar ? a.ntl_pl : a.ntl_pt) + qi / kTileQ,
-                                 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          __hip_atomic_fetch_add(mcnt + (size_t)(planar ? 0 : 1) * a.K + pair, 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      }
-      uint32_t* w = work + kWorkWords * (size_t)hb;
-      atomicAdd(w + 0, wp);
-      atomicAdd(w + 1, wc);
-      atomicMax(w + 2, wc);
-      atomicMax(w + 5, (uint32_t)wall_clock64());
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ int s_last;
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(mticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  if (threadIdx.x < 2)  // every block read the counts before its ticket
-    __hip_atomic_store(a.qlist_n + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
-  if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#endif
-
 struct HistIn {
   const uint32_t* h;
   __device__ uint32_t operator()(size_t i) const { return h[i]; }
@@ -2130,22 +1955,24 @@ __global__ __launch_bounds__(kTileQ) void k_pair_scatter_t(uint32_t nq_pl, uint3
                                                          double* __restrict__ c_pl, size_t ld_pl,
                                                          double* __restrict__ c_pt, size_t ld_pt) {
   __shared__ uint32_t s_cnt[kTileQ / kWave][kTileMaxPairs];
+  __shared__ uint32_t s_hoff[kTileMaxPairs];
   const bool planar = blockIdx.x < ntl_pl;
   const uint32_t tile = planar ? blockIdx.x : blockIdx.x - ntl_pl;
   const uint32_t qi = tile * kTileQ + threadIdx.x;
   const uint32_t nq = planar ? nq_pl : nq_pt;
   const int w = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < (kTileQ / kWave) * K; i += kTileQ) s_cnt[i / K][i % K] = 0;
-  // every load up front: the row's fields with its pair, then the (pair, tile) offset as
-  // soon as the pair is in; the ranking and the per-wave scan run while they fly
+  // every load up front, in one round: the row's fields with its pair, and the tile's
+  // (pair, tile) offsets for every pair (to LDS; the ranking and the per-wave scan run
+  // while they fly)
+  for (int k = threadIdx.x; k < K; k += kTileQ)
+    s_hoff[k] = hist_off[planar ? (size_t)k * ntl_pl + tile : (size_t)K * ntl_pl + (size_t)k * ntl_pt + tile];
   const size_t gq = planar ? qi : nq_pl + qi;
   const bool in = qi < nq;
   const int32_t pair = in ? m_pair[gq] : -1;
   const double4 pi = in ? m_pi[gq] : make_double4(0, 0, 0, 0);
   const double4 ni = in && planar ? m_ni[qi] : make_double4(0, 0, 0, 0);
   const float4 pj = in ? (planar ? q_pl[qi] : q_pt[qi]) : make_float4(0, 0, 0, 0);
-  const size_t hb = planar ? (size_t)max(pair, 0) * ntl_pl + tile : (size_t)K * ntl_pl + (size_t)max(pair, 0) * ntl_pt + tile;
-  const uint32_t hoff = pair >= 0 ? hist_off[hb] : 0u;
   __syncthreads();
   uint32_t rank = 0;
   bool todo = pair >= 0;
@@ -2171,7 +1998,7 @@ __global__ __launch_bounds__(kTileQ) void k_pair_scatter_t(uint32_t nq_pl, uint3
   }
   __syncthreads();
   if (pair < 0) return;
-  const uint32_t dst = hoff + s_cnt[w][pair] + rank;
+  const uint32_t dst = s_hoff[pair] + s_cnt[w][pair] + rank;
   if (planar) {
     c_pl[0 * ld_pl + dst] = pi.x; c_pl[1 * ld_pl + dst] = pi.y; c_pl[2 * ld_pl + dst] = pi.z;
     c_pl[3 * ld_pl + dst] = ni.x; c_pl[4 * ld_pl + dst] = ni.y; c_pl[5 * ld_pl + dst] = ni.z;
@@ -2419,20 +2246,6 @@ static bool no_warm() {
   static const bool v = std::getenv("FMX_NO_WARM") != nullptr;
   return v;
 }
-// FMX_NO_CERT_SPLIT (A/B, FMX_WARM_CERT builds): warm matches in one launch (no certificate)
-[[maybe_unused]] static bool no_cert_split() {
-  static const bool v = std::getenv("FMX_NO_CERT_SPLIT") != nullptr;
-  return v;
-}
-// FMX_LIST_GRID (FMX_WARM_CERT builds): blocks of the listed-query launch (4 waves each)
-[[maybe_unused]] static uint32_t list_grid() {
-  static const uint32_t v = [] {
-    const char* e = std::getenv("FMX_LIST_GRID");
-    const long n = e ? std::atol(e) : 0;
-    return n > 0 ? (uint32_t)n : 1024u;
-  }();
-  return v;
-}
 static bool no_cell_cache() {
   static const bool v = std::getenv("FMX_NO_CELL_CACHE") != nullptr;
   return v;
@@ -2473,12 +2286,10 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     a.cert_b2 = c->cert_b2.p;
     std::memcpy(a.Tprev, c->cert_pose, sizeof(a.Tprev));
     std::memcpy(c->cert_pose, a.Tj, sizeof(a.Tj));
+    a.cert_ok = a.warm && c->cert_gen == c->warm_gen && kGroup > 1 ? 1 : 0;
+    c->cert_gen = kGroup > 1 ? c->warm_gen : 0;  // this launch's bounds (the 8-lane build writes them)
 #endif
   }
-#if FMX_WARM_CERT
-  a.qlist = nullptr;
-  a.qlist_n = nullptr;
-#endif
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
@@ -2543,25 +2354,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   }
   if (nb > 0) {
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
-    bool split = false;
-#if FMX_WARM_CERT && FMX_MATCH_GROUP == 8
-    // a warm match on a plain map (one ring), tiled or counts-only bookkeeping: certify
-    // first (one lane per query), then search only the queries left (one wave each)
-    split = a.warm && a.cert_b2 && a.rings == 1 && (a.tiles || !a.sorted) && !no_cert_split();
-    if (split) {
-      c->qlist.ensure(nq + 1);
-      ensure_zeroed(c->qlist_n, 2, st);
-      a.qlist = c->qlist.p;
-      a.qlist_n = c->qlist_n.p;
-      const uint32_t ncb_pl = (c->n_qpl + kCertQ - 1) / kCertQ, ncb_pt = (c->n_qpt + kCertQ - 1) / kCertQ;
-      hipLaunchKernelGGL(k_match_cert, dim3(ncb_pl + ncb_pt), dim3(kCertQ), K * sizeof(uint32_t), st, a, view(0),
-                         view(1), c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
-                         c->m_ni.p, c->m_ins.p, c->work.p, c->mcnt.p, c->ins_blk.p, c->thist.p, ncb_pl);
-      FMX_HIP(hipGetLastError());
-      g64::launch_match_list(c, &a, sizeof(a), dense, st, list_grid(), kQPB);
-    }
-#endif
-    if (!split) {
+    {
       auto kern = dense ? k_match<true> : k_match<false>;
       hipLaunchKernelGGL(kern, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a,
                          view(0), view(1), c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
@@ -2612,28 +2405,6 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->have_corr = sorted;  // pair-major correspondences for fmx_linearize
   c->have_qo = true;      // query-order correspondences for register_scan
 }
-
-#if FMX_WARM_CERT && FMX_MATCH_GROUP == 64
-// The listed-query launch of a split warm match (g8::run_match; the arguments are g8's
-// MatchArgs, the same layout in every build of this file).
-void launch_match_list(fmx_ctx* c, const void* args, size_t args_size, bool dense, hipStream_t st, uint32_t grid,
-                       uint32_t home_qpb) {
-  if (args_size != sizeof(MatchArgs)) throw StatusError(FMX_E_STATE, "launch_match_list: MatchArgs layouts differ");
-  MatchArgs a;
-  std::memcpy(&a, args, sizeof(a));
-  auto view = [&](int t) {
-    VoxMap& M = c->map;
-    return MapView{reinterpret_cast<const Brick*>(M.table.p) + (t == 0 ? 0 : M.cap[0]), M.cap[t] ? M.cap[t] - 1 : 0,
-                   M.pos.p, M.nrm_p, M.epoch, M.rsh};
-  };
-  const SortOut so{c->hist_off.p, c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p};
-  hipLaunchKernelGGL(dense ? k_match_list<true> : k_match_list<false>, dim3(grid), dim3(kMatchThreads), 0, st, a, view(0),
-                     view(1), c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p, c->m_ni.p,
-                     c->m_ins.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d, c->ins_blk.p, c->ins_off.p,
-                     c->thist.p, so, home_qpb);
-  FMX_HIP(hipGetLastError());
-}
-#endif
 
 // The match at pose_j fused with its single-pose linearization (k_match<.., FUSED>):
 // the summed 7 x 7 + error to dst (28 + 1 doubles), completion word `flag` (null: none).

@@ -15,7 +15,6 @@ for rep in 1 2; do
   done
 done
 export FMX_LIB=$PWD/form_amd/ab/libfmx_wcert.so
-for grid in 512 2048; do
-  FMX_LIST_GRID=$grid FMX_MATCH_DIAG=1 timeout -k 10 300 python bench.py --steps 40 --warmup 10 --no-cpu-baseline --streams "" --no-ablation --no-c5 --sub-workloads c2 --no-host-input > gpurun_out/r4/ab_grid$grid.json 2> gpurun_out/r4/ab_grid$grid.err || { tail -20 gpurun_out/r4/ab_grid$grid.err; exit 1; }
-  python -c "import json; d=json.load(open('gpurun_out/r4/ab_grid$grid.json')); print('grid $grid', d['value'], d['ms_per_step'], d['kernels_ms_per_step'].get('match'), 'c2', d['c2']['value'], d['c2']['kernels_ms_per_step'].get('match'))"
-done
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r4/prof_wcert -o run -- python $GRAFT_REPO_ROOT/bench.py --steps 40 --warmup 10 --no-cpu-baseline --streams "" --no-ablation --no-c5 --sub-workloads c2 --no-host-input > $GRAFT_REPO_ROOT/gpurun_out/r4/prof_wcert.json 2> $GRAFT_REPO_ROOT/gpurun_out/r4/prof_wcert.err || exit 1
+cd $GRAFT_REPO_ROOT
+find gpurun_out/r4/prof_wcert -name "*kernel_stats.csv" | head -1 | xargs -I{} python -c "import csv,sys; r=list(csv.DictReader(open('{}'))); [print(x['Name'][:60], x['Calls'], x['AverageNs']) for x in r if 'match' in x['Name']]"
