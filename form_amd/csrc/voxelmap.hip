@@ -67,6 +67,9 @@
                          // an FMX_CERT_DIAG build sets it to 0 so that every query is searched)
 #endif
 #define FMX_CERT_ANY (FMX_CERT_DIAG || FMX_WARM_CERT)
+#ifndef FMX_TAIL_ONEPASS
+#define FMX_TAIL_ONEPASS 1  // the match's last block: all its scans in one round of loads (A/B switch)
+#endif
 
 namespace fmx {
 // This file is compiled twice (Makefile): FMX_MATCH_GROUP 8 -> fmx::g8 and 1 -> fmx::gl;
@@ -597,31 +600,14 @@ __device__ __forceinline__ uint32_t block_scan_runs(uint32_t n, uint32_t carry, 
   return carry;
 }
 
-// The match kernel's last block, tiled sort: scan the (type, pair, tile) counts
-// (read and reset), then what k_pair_base does: per-pair counts and first rows, host
-// copy of the counts, the linearize chunk table.  K <= kTileMaxPairs.
-__device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist, const SortOut& so,
-                               uint32_t* __restrict__ host_counts) {
+// What k_pair_base does, for the tiled sort (K <= kTileMaxPairs), from the per-type
+// first rows s_pb (filled by the caller's scan of the (type, pair, tile) counts):
+// per-pair counts and first rows, the host copy of the counts, the linearize chunk table.
+__device__ void pair_sort_finish(const MatchArgs& a, const SortOut& so, uint32_t* __restrict__ host_counts,
+                                 uint32_t (*s_pb)[kTileMaxPairs + 1]) {
   __shared__ uint32_t ws[kMatchThreads / kWave];
-  __shared__ uint32_t s_pb[2][kTileMaxPairs + 1];  // per type: first row of pair k, [K] = total
   __shared__ uint32_t s_cr[kTileMaxPairs + 1];
   const int K = a.K;
-  for (int t = 0; t < 2; ++t) {
-    const uint32_t ntl = t ? a.ntl_pt : a.ntl_pl;
-    const size_t base = t ? (size_t)K * a.ntl_pl : 0;
-    const uint32_t n = (uint32_t)K * ntl;
-    const uint32_t carry = block_scan_runs<4>(
-        n, 0u,
-        [&](uint32_t i) { return __hip_atomic_exchange(thist + base + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); },
-        [&](uint32_t i, uint32_t o) {
-          so.hist_off[base + i] = o;
-          if (i % ntl == 0) s_pb[t][i / ntl] = o;
-        },
-        ws);
-    for (int k = threadIdx.x; k < K; k += kMatchThreads)
-      if (ntl == 0) s_pb[t][k] = 0;
-    if (threadIdx.x == 0) s_pb[t][K] = carry;
-  }
   __syncthreads();
   uint32_t carry = 0;
   for (int k0 = 0; k0 < K; k0 += kMatchThreads) {
@@ -668,6 +654,58 @@ __device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist,
     }
   }
   if (threadIdx.x == 0) *so.n_chunks = carry;
+}
+
+// The match kernel's last block, tiled sort: scan the (type, pair, tile) counts (read
+// and reset), then pair_sort_finish.
+__device__ void pair_sort_tail(const MatchArgs& a, uint32_t* __restrict__ thist, const SortOut& so,
+                               uint32_t* __restrict__ host_counts, uint32_t (*s_pb)[kTileMaxPairs + 1]) {
+  __shared__ uint32_t ws[kMatchThreads / kWave];
+  const int K = a.K;
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t ntl = t ? a.ntl_pt : a.ntl_pl;
+    const size_t base = t ? (size_t)K * a.ntl_pl : 0;
+    const uint32_t n = (uint32_t)K * ntl;
+    const uint32_t carry = block_scan_runs<4>(
+        n, 0u,
+        [&](uint32_t i) { return __hip_atomic_exchange(thist + base + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); },
+        [&](uint32_t i, uint32_t o) {
+          so.hist_off[base + i] = o;
+          if (i % ntl == 0) s_pb[t][i / ntl] = o;
+        },
+        ws);
+    for (int k = threadIdx.x; k < K; k += kMatchThreads)
+      if (ntl == 0) s_pb[t][k] = 0;
+    if (threadIdx.x == 0) s_pb[t][K] = carry;
+  }
+  pair_sort_finish(a, so, host_counts, s_pb);
+}
+
+// Exclusive scans of four values per thread over a kMatchThreads block at once (one
+// pair of barriers for all four); totals returned.
+__device__ __forceinline__ void block_excl_scan4(const uint32_t (&v)[4], uint32_t (&ex)[4], uint32_t (&tot)[4],
+                                                 uint32_t (*ws)[4]) {
+  uint32_t incl[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) incl[q] = wave_incl_scan(v[q]);
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == kWave - 1)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ws[w][q] = incl[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t off = 0, t = 0;
+#pragma unroll
+    for (int i = 0; i < kMatchThreads / kWave; ++i) {
+      const uint32_t x = ws[i][q];
+      if (i < w) off += x;
+      t += x;
+    }
+    ex[q] = off + incl[q] - v[q];
+    tot[q] = t;
+  }
+  __syncthreads();
 }
 
 // Lanes of a wave holding G-lane group g's bits of a ballot.
@@ -1435,6 +1473,66 @@ __device__ inline void match_tail(const MatchArgs& a, uint32_t* __restrict__ mcn
     for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
       host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   __shared__ uint32_t ws[kMatchThreads / kWave];
+  __shared__ uint32_t s_pb[2][kTileMaxPairs + 1];  // tiled sort: per type, first row of pair k, [K] = total
+  const bool tiled = a.sorted && a.tiles;
+  const uint32_t nth0 = tiled ? (uint32_t)a.K * a.ntl_pl : 0u, nth1 = tiled ? (uint32_t)a.K * a.ntl_pt : 0u;
+  constexpr int R = 8;
+  if (FMX_TAIL_ONEPASS && max(max(a.nb_pl, a.nb_pt), max(nth0, nth1)) <= (uint32_t)(kMatchThreads * R)) {
+    // every scan in one pass: the four inputs (insert counts per type, (pair, tile)
+    // counts per type) in ONE round of loads, then one four-way block scan
+    __shared__ uint32_t ws4[kMatchThreads / kWave][4];
+    const uint32_t b = threadIdx.x * R;
+    uint32_t v[4][R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint32_t i = b + u;
+      v[0][u] = i < a.nb_pl ? __hip_atomic_load(ins_blk + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      v[1][u] = i < a.nb_pt ? __hip_atomic_load(ins_blk + a.nb_pl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      v[2][u] = i < nth0 ? __hip_atomic_exchange(thist + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      v[3][u] = i < nth1 ? __hip_atomic_exchange(thist + nth0 + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    }
+    uint32_t sum[4], ex[4], tot[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sum[q] = 0;
+#pragma unroll
+      for (int u = 0; u < R; ++u) sum[q] += v[q][u];
+    }
+    block_excl_scan4(sum, ex, tot, ws4);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint32_t i = b + u;
+      if (i < a.nb_pl) ins_off[i] = ex[0];
+      if (i < a.nb_pt) ins_off[a.nb_pl + i] = ex[1];
+      ex[0] += v[0][u];
+      ex[1] += v[1][u];
+    }
+    if (threadIdx.x == 0) {
+      host_store(host_counts + 2 * a.K, tot[0]);
+      host_store(host_counts + 2 * a.K + 1, tot[1]);
+    }
+    if (tiled) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t ntl = t ? a.ntl_pt : a.ntl_pl, n = t ? nth1 : nth0, base = t ? nth0 : 0u;
+        uint32_t e = ex[2 + t];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          const uint32_t i = b + u;
+          if (i < n) {
+            so.hist_off[base + i] = e;
+            if (i % ntl == 0) s_pb[t][i / ntl] = e;
+          }
+          e += v[2 + t][u];
+        }
+        for (int k = threadIdx.x; k < a.K; k += kMatchThreads)
+          if (ntl == 0) s_pb[t][k] = 0;
+        if (threadIdx.x == 0) s_pb[t][a.K] = tot[2 + t];
+      }
+      pair_sort_finish(a, so, host_counts, s_pb);
+    }
+    return;
+  }
   for (int tt = 0; tt < 2; ++tt) {  // planar blocks [0, nb_pl), point blocks [nb_pl, nb)
     const uint32_t b0 = tt == 0 ? 0u : a.nb_pl, n = tt == 0 ? a.nb_pl : a.nb_pt;
     const uint32_t tot = block_scan_runs<8>(
@@ -1442,7 +1540,7 @@ __device__ inline void match_tail(const MatchArgs& a, uint32_t* __restrict__ mcn
         [&](uint32_t i, uint32_t o) { ins_off[b0 + i] = o; }, ws);
     if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, tot);
   }
-  if (a.sorted && a.tiles) pair_sort_tail(a, thist, so, host_counts);
+  if (tiled) pair_sort_tail(a, thist, so, host_counts, s_pb);
 }
 
 template <bool DENSE, bool FUSED = false>
