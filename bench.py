@@ -576,8 +576,10 @@ def sub_stream_line(a, wl, rank, world, local, single, pipe):
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    marks = [t0]
     for k in range(pre + warmup, pre + warmup + steps):
         register(ctx, scans, k, pipe)
+        marks.append(time.perf_counter())
     ctx.sync()
     torch.cuda.synchronize()
     barrier(world)
@@ -615,6 +617,7 @@ def sub_stream_line(a, wl, rank, world, local, single, pipe):
                    "points_per_scan": n_pts, "prefill": pre, "timed_scans": [pre + warmup, pre + warmup + steps],
                    "pipelined_extraction": pipe, "parallelism": f"replicas x{world}"},
         "mpts_per_s": round(value * n_pts / 1e6, 3),
+        "ms_per_step_p50": round(float(np.median(np.diff(marks))) * 1e3, 3),
         "roofline": roofline(a, name, d, wl),
         "kernels_ms_per_step": kern_ms,
         "main_stream_busy_frac": round(min(main_ms / ms, 1.0), 4),
@@ -742,8 +745,10 @@ def main():
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    marks = [t0]  # per-scan host marks (register_scan returns with the scan's pose)
     for k in range(pre + a.warmup, pre + a.warmup + a.steps):
         register(ctx, scans, k, pipe)
+        marks.append(time.perf_counter())
     ctx.sync()
     torch.cuda.synchronize()
     barrier(world)
@@ -821,6 +826,8 @@ def main():
                    # timed one's runs inside)
                    "pipelined_extraction": pipe},
         "mpts_per_s": round(value * n_pts / 1e6, 3),
+        # this rank's median per-scan wall time (host noise shows in the mean, not here)
+        "ms_per_step_p50": round(float(np.median(np.diff(marks))) * 1e3, 3),
         "roofline": roof,
         "kernels_ms_per_step": kern_ms,
         "profile_steps": psteps,
