@@ -1452,6 +1452,7 @@ void fmx_destroy(fmx_ctx* c) {
     for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }
     W.meta.release(); if (W.meta_ev) (void)hipEventDestroy(W.meta_ev); W.partials.release(); W.dposes.release();
     W.pticket.release(); W.dticket.release(); W.dflag.release(); W.dbg.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
+    W.hG_spec.release(); W.spec_flag.release();
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
