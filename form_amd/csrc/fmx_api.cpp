@@ -40,7 +40,6 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
   c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K);
-  c->set_gen = ++c->match_gen;  // (a speculative linearization is tied to its match set)
   if (c->match_group != 8) gl::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
   else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
 }
@@ -800,13 +799,7 @@ void swap_match_set(fmx_ctx* c) {
   swap(c->match_nb_pl, S.match_nb_pl); swap(c->match_nb, S.match_nb); swap(c->n_qo, S.n_qo);
   swap(c->match_group, S.match_group); swap(c->ps, S.ps); swap(c->rows_pl, S.rows_pl); swap(c->rows_pt, S.rows_pt);
   swap(c->cnt_pl, S.cnt_pl); swap(c->cnt_pt, S.cnt_pt); swap(c->last_probes, S.last_probes);
-  swap(c->last_cands, S.last_cands); swap(c->ins_tot, S.ins_tot); swap(c->set_gen, S.set_gen);
-}
-
-// FMX_NO_SPEC_LIN (A/B): speculative matches without the speculative linearization
-static bool no_spec_lin() {
-  static const bool v = std::getenv("FMX_NO_SPEC_LIN") != nullptr;
-  return v;
+  swap(c->last_cands, S.last_cands); swap(c->ins_tot, S.ins_tot);
 }
 
 // Speculative match (smoothing-mode ICP): when an LM trial is probably the LM's last
@@ -817,15 +810,11 @@ static bool no_spec_lin() {
 // instead of matching again; results are bit-identical either way.  The speculative
 // set is not read by any queued kernel: it was swapped out at the start of this ICP
 // iteration and every kernel that read it belongs to earlier, completed iterations.
-// lin_table (K + 1 poses, non-null): also queue the next ICP iteration's first window
-// linearization of this match set at that table (win_linearize_spec), behind the match.
-void spec_match(fmx_ctx* c, const double* pose_j, bool first = false, const double* lin_table = nullptr,
-                double sigma = 0.0) {
+void spec_match(fmx_ctx* c, const double* pose_j, bool first = false) {
   const fmx_params& P = c->P;
   swap_match_set(c);
   try {
     run_match(c, pose_j, P.max_dist_matching, P.min_dist_map, true);
-    if (lin_table && !no_spec_lin()) win_linearize_spec(c, lin_table, sigma);
   } catch (...) {
     swap_match_set(c);
     throw;
@@ -865,7 +854,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
   for (auto& p : e.priors) g.priors.push_back(&p);
   for (auto& m : e.margs) g.lins.push_back(&m);
   if (!fast.keys.empty()) g.lins.push_back(&fast);
-  std::vector<double> table, spec_table;
+  std::vector<double> table;
   for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
     ++icp;
     const Pose before = e.values.at(j);
@@ -882,9 +871,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       for (int k = 0; k < K; ++k) std::memcpy(&table[12 * k], x[slot.at(c->map_scans[k])].m, 12 * sizeof(double));
       std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
       HostScope hs(10);
-      // the linearization the previous iteration queued speculatively, if it is this one
-      if (win_adopt_spec(c, table.data())) ++c->spec_lin_hits;
-      else win_linearize_current(c, table.data(), sigma, nullptr);
+      win_linearize_current(c, table.data(), sigma, nullptr);
       // an LM trial the LM will probably stop after (its predicted decrease within the
       // LM's convergence tolerances, rel/abs 1e-5; the actual decrease decides and
       // tracks the prediction closely on this stream, profiles/r2_spec_log.txt): match
@@ -901,14 +888,8 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       }
       static const bool spec_log = std::getenv("FMX_SPEC_LOG") != nullptr;  // diagnostic
       if (spec_log && lc >= 0.0) fprintf(stderr, "spec it %u lin_change %.3e err %.3e rel %.3e\n", it, lc, ce, lc / ce);
-      if (last_likely && it + 1 < P.max_num_rematches && std::memcmp(xj.m, before.m, sizeof(xj.m)) != 0) {
-        // the next iteration starts from the window poses with only X(j) moved to xj
-        // (update_current_pose): its first linearization's table
-        spec_table.resize(12 * ((size_t)K + 1));
-        for (int k = 0; k < K; ++k) std::memcpy(&spec_table[12 * k], e.values.at(c->map_scans[k]).m, 12 * sizeof(double));
-        std::memcpy(&spec_table[12 * (size_t)K], xj.m, 12 * sizeof(double));
-        spec_match(c, xj.m, false, spec_table.data(), sigma);
-      }
+      if (last_likely && it + 1 < P.max_num_rematches && std::memcmp(xj.m, before.m, sizeof(xj.m)) != 0)
+        spec_match(c, xj.m);
     };
     auto lin_end = [&](double* G) {
       HostScope hs(10);
@@ -1169,7 +1150,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
                                       " != " + std::to_string(n));
   const uint64_t j = e.init ? e.scan + 1 : 0;
   const uint64_t waits0 = c->host_waits;
-  const uint64_t spec0 = c->spec_launched, hits0 = c->spec_hits, pf0 = c->pf_used, slin0 = c->spec_lin_hits;
+  const uint64_t spec0 = c->spec_launched, hits0 = c->spec_hits, pf0 = c->pf_used;
   c->spec_valid = false;  // a new map and query set: no speculation carries over
   // Host work that only needs the estimator state runs while this scan's extraction
   // kernels execute: the previous scan's deferred tail (keyscan step +
@@ -1310,7 +1291,6 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[11] = map_spec_used ? 1 : 0;
   c->stats[12] = c->pf_used - pf0;
   c->stats[13] = e.values.size();
-  c->stats[14] = c->spec_lin_hits - slin0;
   if (out) *out = fc;
 }
 
@@ -1452,7 +1432,6 @@ void fmx_destroy(fmx_ctx* c) {
     for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }
     W.meta.release(); if (W.meta_ev) (void)hipEventDestroy(W.meta_ev); W.partials.release(); W.dposes.release();
     W.pticket.release(); W.dticket.release(); W.dflag.release(); W.dbg.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
-    W.hG_spec.release(); W.spec_flag.release();
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);

@@ -237,18 +237,6 @@ struct WinStore {
   int pending_np = 0;
   HBuf<double> hG, hposes;
   HBuf<uint32_t> hmeta;
-  // speculative linearization (register_scan's ICP loop): the next ICP iteration's first
-  // linearization of the current scan's pairs, queued behind the speculative match into
-  // its own host buffer and completion word; adopted by win_adopt_spec when that
-  // iteration starts from exactly this pose table on the speculative match set
-  HBuf<double> hG_spec;
-  HBuf<uint32_t> spec_flag;
-  uint32_t spec_seq = 0;
-  bool spec_launched = false, pending_spec = false;
-  uint64_t spec_set_gen = 0;  // the match set (fmx_ctx::set_gen) it linearized
-  int spec_np = 0;
-  uint32_t spec_grid = 0;
-  std::vector<double> spec_table;
 };
 
 // A second set of match outputs: register_scan launches speculative matches into it
@@ -270,7 +258,6 @@ struct MatchSet {
   uint32_t max_chunks = 0, work_blocks = 0, match_nb_pl = 0, match_nb = 0, n_qo = 0;
   bool work_copied = false;
   int match_group = 8;
-  uint64_t set_gen = 0;
   PairScatter ps;
   uint64_t rows_pl = 0, rows_pt = 0;
   std::vector<uint32_t> cnt_pl, cnt_pt;
@@ -290,7 +277,7 @@ struct ExLaunch {
 
 }  // namespace fmx
 
-constexpr int kStatsN = 15;  // fmx_last_stats entries
+constexpr int kStatsN = 14;  // fmx_last_stats entries
 
 struct fmx_ctx {
   fmx_params P{};
@@ -407,7 +394,6 @@ struct fmx_ctx {
   fmx::DBuf<uint32_t> n_chunks;
   uint32_t max_chunks = 0;
   int match_group = 8;  // lanes per query of the last run_match (voxelmap.hip g8 / gl)
-  uint64_t set_gen = 0, match_gen = 0;  // the current match set's run_match number (swapped with it)
   bool have_corr = false;
   fmx::PairScatter ps;          // the last sorted match's scatter (voxelmap.hip)
   bool scatter_pending = false; // ... not yet launched (deferred by fmx_match)
@@ -464,7 +450,7 @@ struct fmx_ctx {
   bool spec_valid = false;
   bool spec_first = false;  // the speculative set holds the scan's first match (not a speculation)
   double spec_pose[12] = {};
-  uint64_t spec_launched = 0, spec_hits = 0, spec_lin_hits = 0;
+  uint64_t spec_launched = 0, spec_hits = 0;
   uint64_t spec_map_hits = 0, spec_map_misses = 0;  // speculative map builds kept / rebuilt
 
   // ---- multi-GPU exchange (comm.cpp): RCCL communicator, or null
@@ -750,11 +736,7 @@ std::vector<WinPair> win_pairs(fmx_ctx* c);
 void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vector<uint64_t>& keys);
 void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out);
 void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
-void win_finish(fmx_ctx* c, double* G_out);
-// speculative linearization of the current match set (win_linearize_current at the
-// K + 1 pose table `poses`), and its adoption by a later identical request
-void win_linearize_spec(fmx_ctx* c, const double* poses, double sigma);
-bool win_adopt_spec(fmx_ctx* c, const double* poses);  // completes a win_linearize_* called with G_out = null
+void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* called with G_out = null
 // comm.cpp: RCCL communicator of the sharded path, all-reduce on the context stream
 // FORM::map() snapshot (snapshot.hip): world-frame keypoints of feature type t of
 // `scans` at `poses`, grouped by voxel of width w; returns the record count

@@ -372,12 +372,10 @@ void win_timing_collect(fmx_ctx* c, uint32_t grid_chunks) {
 // out (win_finish).  The host assembles the x-dependent non-pair terms in between.
 // out_dev (sharded fmx_linearize): G to this device buffer instead, the completion word
 // to a device scratch word; the caller all-reduces and copies (no win_finish).
-// spec: the speculative linearization (its own host buffer and completion word; a
-// launch in flight stays pending).
 void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double bytes,
-               double* out_dev = nullptr, bool spec = false) {
+               double* out_dev = nullptr) {
   WinStore& W = c->win;
-  if (W.pending && !spec) win_finish(c, nullptr);  // an abandoned one (error path): drain it first
+  if (W.pending) win_finish(c, nullptr);  // an abandoned one (error path): drain it first
   hipStream_t st = c->stream;
   WinPoses wp;
   WinPosesN<kWinSmallArgPoses> wps;
@@ -405,16 +403,6 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
   a.hostG = W.hG.d;
   a.seq = next_flag(c);
   a.flag = c->h_flag.d;
-  if (spec) {
-    W.hG_spec.ensure((size_t)np * kWinG);
-    if (!W.spec_flag.p) {
-      W.spec_flag.ensure(1);
-      W.spec_flag.p[0] = 0;
-    }
-    a.hostG = W.hG_spec.d;
-    a.flag = W.spec_flag.d;
-    a.seq = ++W.spec_seq;
-  }
   if (out_dev) {
     W.dflag.ensure(1);
     a.hostG = out_dev;
@@ -438,14 +426,7 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
       hipLaunchKernelGGL(k_win_linearize<kWinMaxArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
     FMX_HIP(hipGetLastError());
   }
-  if (spec) {
-    W.spec_launched = true;
-    W.spec_np = a.npairs;
-    W.spec_grid = grid_chunks;
-    return;
-  }
   W.pending = out_dev == nullptr;
-  W.pending_spec = false;
   W.pending_seq = a.seq;
   W.pending_np = a.npairs;
   W.pending_grid = grid_chunks;
@@ -459,10 +440,9 @@ void win_finish(fmx_ctx* c, double* G_out) {
   W.pending = false;
   {
     HostScope hs(13);
-    wait_flag(c, W.pending_spec ? W.spec_flag.p : c->h_flag.p, W.pending_seq);
+    wait_flag(c, c->h_flag.p, W.pending_seq);
   }
-  if (G_out) std::memcpy(G_out, (W.pending_spec ? W.hG_spec : W.hG).p, (size_t)W.pending_np * kWinG * sizeof(double));
-  W.pending_spec = false;
+  if (G_out) std::memcpy(G_out, W.hG.p, (size_t)W.pending_np * kWinG * sizeof(double));
   if (win_timing_on()) win_timing_collect(c, W.pending_grid);
 }
 
@@ -667,52 +647,6 @@ void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double
   // exact row counts arrive with the match counts; the byte model uses the last known
   win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K);
   if (G_out) win_finish(c, G_out);
-}
-
-// The speculative form of win_linearize_current (no wait; W.pending untouched): the
-// pose table is kept for win_adopt_spec.
-void win_linearize_spec(fmx_ctx* c, const double* poses, double sigma) {
-  if (!c->have_corr) throw StatusError(FMX_E_STATE, "win_linearize_spec: no sorted match");
-  WinStore& W = c->win;
-  W.spec_launched = false;
-  if ((int)c->K + 1 > kWinMaxArgPoses) return;  // (a device pose table would share hposes with the pending launch)
-  run_pair_scatter(c);
-  WinArgs a{};
-  a.chunks = c->chunks.p;
-  a.n_chunks = c->n_chunks.p;
-  a.chunk_range = c->chunk_range.p;
-  a.npairs = (int)c->K;
-  a.c_pl = c->c_pl.p;
-  a.ld_pl = c->ld_pl;
-  a.c_pt = c->c_pt.p;
-  a.ld_pt = c->ld_pt;
-  a.implicit_j = (int)c->K;
-  a.inv = 1.0 / sigma;
-  W.spec_table.assign(poses, poses + 12 * ((size_t)c->K + 1));
-  W.spec_set_gen = c->set_gen;
-  win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K,
-            nullptr, true);
-}
-
-// A request for win_linearize_current at `poses` that the speculative launch already
-// made (same match set — the caller's responsibility — and bit-identical poses): it
-// becomes the pending linearization, finished by win_finish.  Any other request drops
-// the speculative one.
-bool win_adopt_spec(fmx_ctx* c, const double* poses) {
-  WinStore& W = c->win;
-  if (!W.spec_launched) return false;
-  W.spec_launched = false;
-  const size_t n = 12 * ((size_t)c->K + 1);
-  if (W.spec_set_gen != c->set_gen || W.spec_np != (int)c->K || W.spec_table.size() != n ||
-      std::memcmp(W.spec_table.data(), poses, n * sizeof(double)) != 0)
-    return false;
-  if (W.pending) win_finish(c, nullptr);
-  W.pending = true;
-  W.pending_spec = true;
-  W.pending_seq = W.spec_seq;
-  W.pending_np = W.spec_np;
-  W.pending_grid = W.spec_grid;
-  return true;
 }
 
 // fmx_linearize / fmx_error — the GTSAM seam, DenseFactor::linearize of every pair's

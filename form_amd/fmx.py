@@ -393,7 +393,7 @@ class Context:
     def last_stats(self) -> dict:
         keys = ["icp_iters", "lm_iters", "matched_planar", "matched_point", "map_planar", "map_point",
                 "linearizations", "map_scans", "host_waits", "spec_matches", "spec_hits", "spec_map",
-                "pipelined", "window_poses", "spec_lins"]
+                "pipelined", "window_poses"]
         s = np.zeros(len(keys), np.uint64)
         self._chk(self._L.fmx_last_stats(self.h, _p(s), C.c_int(len(keys))))
         return {k: int(v) for k, v in zip(keys, s)}

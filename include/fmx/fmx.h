@@ -270,9 +270,7 @@ fmx_status fmx_map_download(fmx_ctx* ctx, double voxel_width, double* planar, ui
  * the one built speculatively during the previous scan's final LM, 0 when built at
  * the start of this scan), pipelined (1 when the scan's features were extracted
  * during the previous registration, fmx_next_scan), window_poses (poses in the
- * smoother's window after the scan: the host LM's system is 6 x window_poses),
- * spec_lins (ICP iterations whose first linearization was the one queued behind the
- * speculative match)};
+ * smoother's window after the scan: the host LM's system is 6 x window_poses)};
  * entries past the known ones read 0. */
 fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t* stats, int n);
 /* Work of the last fmx_match (counted by the kernel, available while profiling is

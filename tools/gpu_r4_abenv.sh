@@ -12,6 +12,6 @@ for rep in $(seq 1 $N); do
   for tag in env default; do
     if [ $tag = env ]; then E="env $ENVSET"; else E=""; fi
     timeout -k 10 300 $E $B > gpurun_out/r4ab/env_$tag$rep.json 2> gpurun_out/r4ab/env_$tag$rep.err || { tail -20 gpurun_out/r4ab/env_$tag$rep.err; exit 1; }
-    python -c "import json; d=json.load(open('gpurun_out/r4ab/env_$tag$rep.json')); k=d['kernels_ms_per_step']; k2=d['c2']['kernels_ms_per_step']; print('%-8s C4 %7.1f ms %.3f p50 %.3f match %.4f win %.4f rt %.1f slin %.2f | C2 %6.1f ms %.3f p50 %.3f match %.4f win %.4f' % ('$tag', d['value'], d['ms_per_step'], d['ms_per_step_p50'], k['match'], k['window'], d['host_round_trips_per_scan'], d['counters'].get('spec_lins', -1), d['c2']['value'], d['c2']['ms_per_step'], d['c2']['ms_per_step_p50'], k2['match'], k2['window']))"
+    python -c "import json; d=json.load(open('gpurun_out/r4ab/env_$tag$rep.json')); k=d['kernels_ms_per_step']; k2=d['c2']['kernels_ms_per_step']; print('%-8s C4 %7.1f ms %.3f p50 %.3f match %.4f win %.4f rt %.1f | C2 %6.1f ms %.3f p50 %.3f match %.4f win %.4f' % ('$tag', d['value'], d['ms_per_step'], d['ms_per_step_p50'], k['match'], k['window'], d['host_round_trips_per_scan'], d['c2']['value'], d['c2']['ms_per_step'], d['c2']['ms_per_step_p50'], k2['match'], k2['window']))"
   done
 done
