@@ -628,6 +628,17 @@ def sub_stream_line(a, wl, rank, world, local, single, pipe):
     return line, (host, params, k0)
 
 
+# What a launch's algorithmic bytes count: the work the launch
+# did, from the kernel's own probe / candidate counters.
+ALG_BYTES_MODEL = {
+    "match": "per query 16 B read + 45 B result (+32 B planar normal) + warm state 20 B written, 52 B read; "
+             "64 B per brick probe, 32 B per candidate record tested; a query the warm certificate settles "
+             "probes and tests nothing (round 4: 87-92 % of warm queries)",
+    "match_linearize": "per query 16 B read (+32 B planar normal of the winner); 64 B per brick probe, 32 B per "
+                       "candidate record; 256 B of block partials per block",
+}
+
+
 def roofline(a, name, d, workload):
     """The roofline block of the dominant kernel class `name` (profile entry d): the §8(d)
     algorithmic bytes per launch over the HIP-event average launch time (frac), and the
@@ -640,6 +651,8 @@ def roofline(a, name, d, workload):
     roof = dict(bound="hbm", kernel=name, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 6), traffic=traffic, avg_launch_us=round(avg_ms * 1e3, 3),
                 alg_bytes_per_launch=bytes_per)
+    if name in ALG_BYTES_MODEL:
+        roof["alg_bytes_model"] = ALG_BYTES_MODEL[name]
     if tsrc:
         roof["traffic_source"] = tsrc
     if traffic and avg_ms > 0:

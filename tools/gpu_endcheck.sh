@@ -13,7 +13,7 @@ tail -1 $D/smoke.log
 timeout -k 10 900 python bench.py > $D/bench.json 2> $D/bench.err || { tail -20 $D/bench.err; exit 1; }
 head -c 800 $D/bench.json; echo
 rm -rf $D/prof
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --streams "" > $D/bench_prof.json 2> $D/prof.err || { tail -20 $D/prof.err; exit 1; }
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --streams "" --sub-workloads= --no-host-input --no-c5 --no-ablation > $D/bench_prof.json 2> $D/prof.err || { tail -20 $D/prof.err; exit 1; }
 python tools/critical_path.py $(find $D/prof -name "*kernel_trace.csv" | head -1) 40 $D/critical_path_c4.json 40 > /dev/null || exit 1
 find $D/prof -name "*kernel_trace.csv" -delete
 python tools/stats_fmx.py $(find $D/prof -name "*kernel_stats.csv" | head -1) > $D/kernel_stats_fmx.csv
