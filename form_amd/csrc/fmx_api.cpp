@@ -39,13 +39,11 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
 }
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
-  HostScope hs(16);
   c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K);
   if (c->match_group != 8) gl::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
   else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
 }
 void run_pair_scatter(fmx_ctx* c) {
-  HostScope hs(17);
   if (c->match_group != 8) gl::run_pair_scatter(c);
   else g8::run_pair_scatter(c);
 }
@@ -180,15 +178,11 @@ void drop_match(fmx_ctx* c) { c->lazy.pending = false; }
 // SETTLE: run a deferred fmx_match first — every entry point but fmx_match itself,
 // fmx_linearize_matched (which may consume it fused) and those that read no match
 // state (pose, stats, profile counters, fmx_sync: a deferred match is no queued work)
-void early_undo(fmx_ctx* c);
-// KEEP_EARLY: an entry point that leaves an early first match in place (register_scan,
-// next_scan and the read-only / profiling calls); every other one undoes it first.
-template <bool SETTLE = true, bool KEEP_EARLY = false, class F>
+template <bool SETTLE = true, class F>
 fmx_status guard(fmx_ctx* c, F&& f) {
   if (!c) return FMX_E_INVAL;
   try {
     FMX_HIP(hipSetDevice(c->device));
-    if constexpr (!KEEP_EARLY) early_undo(c);
     if constexpr (SETTLE) settle_match(c);
     f();
     c->err.clear();
@@ -482,27 +476,6 @@ void swap_query_set(fmx_ctx* c) {
   using std::swap;
   swap(c->q_pl_pos, c->nq_pl_pos); swap(c->q_pl_nrm, c->nq_pl_nrm); swap(c->q_pt_pos, c->nq_pt_pos);
   swap(c->q_pl_idx, c->nq_pl_idx); swap(c->q_pt_idx, c->nq_pt_idx); swap(c->planar_mask, c->n_planar_mask);
-}
-// Undo an early first match (fmx_ctx::Early): the previous query set back, the
-// announced scan's extraction pending again, no speculation carried over.
-void early_undo(fmx_ctx* c) {
-  auto& E = c->early;
-  if (!E.valid) return;
-  E.valid = false;
-  swap_query_set(c);
-  c->q_scan = E.q_scan;
-  c->n_qpl = E.n_qpl;
-  c->n_qpt = E.n_qpt;
-  c->n_sel = E.n_sel;
-  c->have_queries = E.have_queries;
-  c->have_match = E.have_match;
-  c->have_qo = E.have_qo;
-  ++c->warm_gen;
-  c->spec_valid = false;
-  c->pf_launched = true;  // pf_L still holds its launch (its completion word stays published)
-  c->pf_ptr = E.ptr;
-  c->pf_n = E.n;
-  c->pf_host = E.host;
 }
 // Discard a queued extraction of an announced scan (its buffers are then free again).
 void pf_drop(fmx_ctx* c) {
@@ -1152,7 +1125,6 @@ void finish_tail(fmx_ctx* c) {
   if (c->est) finish_tail(c, *c->est);
 }
 
-void early_first_match(fmx_ctx* c, fmx_ctx::Est& e);
 void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
   HostScope hs_all(0);
   // host time spent outside register_scan since the previous call returned (diagnostic)
@@ -1179,11 +1151,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   const uint64_t j = e.init ? e.scan + 1 : 0;
   const uint64_t waits0 = c->host_waits;
   const uint64_t spec0 = c->spec_launched, hits0 = c->spec_hits, pf0 = c->pf_used;
-  // the early first match of this scan (queued by the previous call), if this is its scan
-  const bool early = c->early.valid && (on_dev != 0) != c->early.host && xyzw == c->early.ptr && n == c->early.n;
-  if (c->early.valid && !early) early_undo(c);  // another scan: as if nothing had been taken
-  c->early.valid = false;
-  if (!early) c->spec_valid = false;  // a new map and query set: no speculation carries over
+  c->spec_valid = false;  // a new map and query set: no speculation carries over
   // Host work that only needs the estimator state runs while this scan's extraction
   // kernels execute: the previous scan's deferred tail (keyscan step +
   // marginalization), then step(prediction) (constraints.cpp:206-223) and the map
@@ -1240,20 +1208,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   };
   {
     HostScope hs_ex(2);
-    if (early) {
-      // taken at the end of the previous call: the query set is current, the first match
-      // queued at the prediction on the speculative map — if the map inputs and the
-      // prediction computed now are exactly those, else match again here
-      fc = c->early.fc;
-      ++c->pf_used;
-      map_inputs();
-      FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
-      if (!map_spec_used || std::memcmp(e.values.at(j).m, c->early.pred, sizeof(c->early.pred)) != 0) {
-        c->spec_valid = false;
-        if (!P.disable_smoothing) spec_match(c, e.values.at(j).m, true);
-      }
-      finish();
-    } else if (pf_take(c, xyzw, n, on_dev, j, &fc)) {
+    if (pf_take(c, xyzw, n, on_dev, j, &fc)) {
       // pipelined: the features were extracted during the previous registration.  The
       // first ICP match (at the prediction) is queued before the host's finish() work,
       // which then overlaps it; the ICP loop takes it as a speculative match.
@@ -1337,65 +1292,6 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   c->stats[12] = c->pf_used - pf0;
   c->stats[13] = e.values.size();
   if (out) *out = fc;
-  early_first_match(c, e);
-}
-
-// FMX_NO_EARLY (A/B): no early first match
-bool no_early() {
-  static const bool v = std::getenv("FMX_NO_EARLY") != nullptr;
-  return v;
-}
-
-// At the end of register_scan (smoothing mode): when the announced next scan's
-// extraction has finished and the speculative map built during the final LM is exactly
-// the map the next call will want, take that scan's query set now and queue its first
-// (speculative) match at the prediction — the computation register_scan(j + 1) starts
-// with — so it runs while the caller is between the two calls.  fmx_ctx::Early keeps
-// what the take replaced; any entry point other than register_scan of that scan undoes
-// it (early_undo).
-void early_first_match(fmx_ctx* c, fmx_ctx::Est& e) {
-  const fmx_params& P = c->P;
-  if (P.disable_smoothing || no_early() || !c->pf_launched || !e.spec_map || !e.init) return;
-  if (*c->pf_L.flag != c->pf_L.seq) return;  // still extracting: the next call takes it as usual
-  std::set<uint64_t> sset;
-  for (int t = 0; t < 2; ++t)
-    for (auto& [s, r] : c->pool[t].ranges) sset.insert(s);
-  const std::vector<uint64_t> scans(sset.begin(), sset.end());
-  if (scans != e.spec_map_scans || scans.empty()) return;
-  for (size_t k = 0; k < scans.size(); ++k)
-    if (std::memcmp(&e.spec_map_poses[12 * k], e.values.at(scans[k]).m, 12 * sizeof(double)) != 0) return;
-  const Pose pred = predict_next(e, e.tail_pending ? e.tail_marg : std::vector<uint64_t>{});
-  auto& E = c->early;
-  E.q_scan = c->q_scan;
-  E.n_qpl = c->n_qpl;
-  E.n_qpt = c->n_qpt;
-  E.n_sel = c->n_sel;
-  E.have_queries = c->have_queries;
-  E.have_match = c->have_match;
-  E.have_qo = c->have_qo;
-  E.ptr = c->pf_ptr;
-  E.n = c->pf_n;
-  E.host = c->pf_host;
-  // pf_take's steps (its stats count comes with the next call)
-  c->pf_launched = false;
-  c->pf_ptr = nullptr;
-  swap_query_set(c);
-  FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_pf, 0));
-  extract_collect(c, c->pf_L, &E.fc);  // published: no wait
-  c->q_scan = e.scan + 1;
-  c->have_queries = true;
-  ++c->warm_gen;
-  c->have_match = false;
-  c->have_qo = false;
-  E.valid = true;  // (early_undo restores the above if anything below throws)
-  try {
-    FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the speculative map
-    spec_match(c, pred.m, true);
-  } catch (...) {
-    early_undo(c);
-    throw;
-  }
-  std::memcpy(E.pred, pred.m, sizeof(E.pred));
 }
 
 }  // namespace
@@ -1823,7 +1719,7 @@ fmx_status fmx_comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank
 }
 
 fmx_status fmx_next_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev) {
-  return guard<false, true>(c, [&] {
+  return guard<false>(c, [&] {
     if (!xyzw) {  // withdraw the announcement
       c->ann_ptr = nullptr;
       return;
@@ -1853,7 +1749,7 @@ fmx_status fmx_next_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev) {
 }
 
 fmx_status fmx_scan_buffer(fmx_ctx* c, size_t n, float** out) {
-  return guard<false, true>(c, [&] {
+  return guard<false>(c, [&] {
     if (!out || !n) throw StatusError(FMX_E_INVAL, "null output / zero points");
     auto& B = c->scanbuf[c->scanbuf_next];
     if (B.cap < n) {
@@ -1871,14 +1767,14 @@ fmx_status fmx_scan_buffer(fmx_ctx* c, size_t n, float** out) {
 }
 
 fmx_status fmx_register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feature_counts* out) {
-  return guard<false, true>(c, [&] {
+  return guard<false>(c, [&] {
     drop_match(c);
     register_scan(c, xyzw, n, on_dev, out);
   });
 }
 
 fmx_status fmx_current_pose(fmx_ctx* c, double pose[12]) {
-  return guard<false, true>(c, [&] {
+  return guard<false>(c, [&] {
     if (!c->est || !c->est->init) {
       const Pose I = identity();
       std::memcpy(pose, I.m, sizeof(I.m));
@@ -1939,14 +1835,14 @@ fmx_status fmx_map_download(fmx_ctx* c, double voxel_width, double* planar, uint
 }
 
 fmx_status fmx_last_stats(fmx_ctx* c, uint64_t* stats, int n) {
-  return guard<false, true>(c, [&] {
+  return guard<false>(c, [&] {
     if (!stats || n < 0) throw StatusError(FMX_E_INVAL, "null stats");
     for (int k = 0; k < n; ++k) stats[k] = k < kStatsN ? c->stats[k] : 0;
   });
 }
 
 fmx_status fmx_match_work(fmx_ctx* c, double work[3]) {
-  return guard<false, true>(c, [&] {  // the last launched match (a fused one counts too)
+  return guard<false>(c, [&] {  // the last launched match (a fused one counts too)
     match_counts_fetch(c);
     work[0] = (double)c->n_qpl + (double)c->n_qpt;
     work[1] = c->last_probes;
@@ -1955,10 +1851,10 @@ fmx_status fmx_match_work(fmx_ctx* c, double work[3]) {
 }
 
 fmx_status fmx_profile_enable(fmx_ctx* c, int on) {
-  return guard<false, true>(c, [&] { c->prof.on = on != 0; });
+  return guard<false>(c, [&] { c->prof.on = on != 0; });
 }
 fmx_status fmx_profile_reset(fmx_ctx* c) {
-  return guard<false, true>(c, [&] {
+  return guard<false>(c, [&] {
     prof_collect(c);
     for (int i = 0; i < PROF_COUNT; ++i) {
       c->prof.ms[i] = 0;
@@ -1970,7 +1866,7 @@ fmx_status fmx_profile_reset(fmx_ctx* c) {
 int fmx_profile_count(void) { return PROF_COUNT; }
 const char* fmx_profile_name(int k) { return (k >= 0 && k < PROF_COUNT) ? kProfNames[k] : ""; }
 fmx_status fmx_profile_read(fmx_ctx* c, double* ms, uint64_t* launches, double* bytes, int n) {
-  return guard<false, true>(c, [&] {
+  return guard<false>(c, [&] {
     prof_collect(c);
     for (int i = 0; i < std::min(n, (int)PROF_COUNT); ++i) {
       if (ms) ms[i] = c->prof.ms[i];
@@ -1980,7 +1876,7 @@ fmx_status fmx_profile_read(fmx_ctx* c, double* ms, uint64_t* launches, double* 
   });
 }
 fmx_status fmx_sync(fmx_ctx* c) {
-  return guard<false, true>(c, [&] { sync_all(c); });
+  return guard<false>(c, [&] { sync_all(c); });
 }
 
 }  // extern "C"

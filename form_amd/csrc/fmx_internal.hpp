@@ -323,22 +323,6 @@ struct fmx_ctx {
   fmx::HBuf<uint32_t> h_pf;         // pinned: [0..2] its totals, [4] its completion word
   hipEvent_t ev_pf = nullptr, ev_pf_fork = nullptr;
   uint64_t pf_used = 0, pf_dropped = 0;
-  // early first match (register_scan's end, smoothing mode): the announced scan's query
-  // set already taken and its first (speculative) match queued at the prediction on the
-  // speculative map; the next register_scan of that scan continues from here, any other
-  // entry point undoes it (early_undo)
-  struct Early {
-    bool valid = false;
-    const float* ptr = nullptr;
-    size_t n = 0;
-    bool host = false;
-    fmx_feature_counts fc{};
-    double pred[12] = {};
-    // the state the take replaced
-    uint64_t q_scan = 0;
-    uint32_t n_qpl = 0, n_qpt = 0, n_sel = 0;
-    bool have_queries = false, have_match = false, have_qo = false;
-  } early;
 
   // ---- host-resident scans (stage.hpp): the reference passes the scan as a host
   // std::vector<PointXYZf> (form.hpp:82-83).  Copied into pinned memory by helper
@@ -488,15 +472,15 @@ namespace fmx {
 // printed to stderr at exit.  Diagnostic only.
 struct HostTiming {
   bool on = std::getenv("FMX_HOST_TIMING") != nullptr;
-  double t[18] = {0};
-  uint64_t n[18] = {0};
+  double t[16] = {0};
+  uint64_t n[16] = {0};
   ~HostTiming() {
     if (!on) return;
-    static const char* names[18] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop",
+    static const char* names[16] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop",
                                     "insert+tail", "map_host_prep", "map_launches", "fast_lm", "full_lm",
                                     "lin_callback", "marginalize", "win_launch_call", "win_wait",
-                                    "pf_launch", "between_calls", "match_call", "scatter_call"};
-    for (int i = 0; i < 18; ++i)
+                                    "pf_launch", "between_calls"};
+    for (int i = 0; i < 16; ++i)
       if (n[i]) fprintf(stderr, "host %-14s %10.1f us total %8llu calls %8.2f us/call\n", names[i], t[i] * 1e6,
                         (unsigned long long)n[i], t[i] * 1e6 / n[i]);
     fprintf(stderr, "host device-buffer reallocations %llu\n", (unsigned long long)dbuf_reallocs().load());
