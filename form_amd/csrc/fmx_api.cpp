@@ -39,11 +39,13 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
 }
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
+  HostScope hs(16);
   c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K);
   if (c->match_group != 8) gl::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
   else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
 }
 void run_pair_scatter(fmx_ctx* c) {
+  HostScope hs(17);
   if (c->match_group != 8) gl::run_pair_scatter(c);
   else g8::run_pair_scatter(c);
 }

@@ -472,15 +472,15 @@ namespace fmx {
 // printed to stderr at exit.  Diagnostic only.
 struct HostTiming {
   bool on = std::getenv("FMX_HOST_TIMING") != nullptr;
-  double t[16] = {0};
-  uint64_t n[16] = {0};
+  double t[18] = {0};
+  uint64_t n[18] = {0};
   ~HostTiming() {
     if (!on) return;
-    static const char* names[16] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop",
+    static const char* names[18] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop",
                                     "insert+tail", "map_host_prep", "map_launches", "fast_lm", "full_lm",
                                     "lin_callback", "marginalize", "win_launch_call", "win_wait",
-                                    "pf_launch", "between_calls"};
-    for (int i = 0; i < 16; ++i)
+                                    "pf_launch", "between_calls", "match_call", "scatter_call"};
+    for (int i = 0; i < 18; ++i)
       if (n[i]) fprintf(stderr, "host %-14s %10.1f us total %8llu calls %8.2f us/call\n", names[i], t[i] * 1e6,
                         (unsigned long long)n[i], t[i] * 1e6 / n[i]);
     fprintf(stderr, "host device-buffer reallocations %llu\n", (unsigned long long)dbuf_reallocs().load());
