@@ -306,6 +306,7 @@ def host_input_block(a, new_ctx, dscans, single, start, steps):
         # timed: the fmx calls only (a pinned scan's assembly is the caller's own copy, as
         # the pageable arrays' is: bindings.cpp:150-156 builds its vector either way)
         dt = 0.0
+        per = []
         for k in range(start, start + steps):
             nxt = get(k + 1) if pipe else None
             cur = get(k)
@@ -313,12 +314,14 @@ def host_input_block(a, new_ctx, dscans, single, start, steps):
             if pipe:
                 ctx.next_scan(nxt)
             ctx.register_scan(cur)
-            dt += time.perf_counter() - t0
+            per.append(time.perf_counter() - t0)
+            dt += per[-1]
             bufs.pop(k - 1, None)
         t0 = time.perf_counter()
         ctx.sync()
         dt += time.perf_counter() - t0
         out[mode] = {"scans_per_s": round(steps / dt, 3), "ms_per_step": round(dt / steps * 1e3, 3),
+                     "ms_per_step_p50": round(float(np.median(per)) * 1e3, 3),
                      "pipelined_scans": ctx.last_stats()["pipelined"]}
         ctx.close()
     # raw copies of one scan (median of 10): what the staging has to hide
@@ -737,12 +740,15 @@ def main():
             register(actx, scans, k, pipeline)
         actx.sync()
         ta = time.perf_counter()
+        mk = [ta]
         for k in range(pre + a.warmup, pre + a.warmup + a.steps):
             register(actx, scans, k, pipeline)
+            mk.append(time.perf_counter())
         actx.sync()
         ta = time.perf_counter() - ta
         actx.close()
-        return {"scans_per_s": round(a.steps / ta, 3), "ms_per_step": round(ta / a.steps * 1e3, 3)}
+        return {"scans_per_s": round(a.steps / ta, 3), "ms_per_step": round(ta / a.steps * 1e3, 3),
+                "ms_per_step_p50": round(float(np.median(np.diff(mk))) * 1e3, 3)}
 
     ablation = None
     if not a.no_ablation:
@@ -872,6 +878,16 @@ def main():
             "pinned_pipelined": round(host_in["pinned_pipelined"]["scans_per_s"] / value, 4),
             "pinned_sequential": round(host_in["pinned_sequential"]["scans_per_s"] / sequential["scans_per_s"], 4)
             if sequential else None}
+        # the same ratios from median scan times (robust to the host hiccups that move
+        # the means between runs on one box): device median / host-input median
+        p50_dev = out.get("ms_per_step_p50")
+        p50_seq = sequential.get("ms_per_step_p50") if sequential else None
+        out["host_input"]["vs_device_p50"] = {
+            "pipelined": round(p50_dev / host_in["pageable_pipelined"]["ms_per_step_p50"], 4) if p50_dev else None,
+            "sequential": round(p50_seq / host_in["pageable_sequential"]["ms_per_step_p50"], 4) if p50_seq else None,
+            "pinned_pipelined": round(p50_dev / host_in["pinned_pipelined"]["ms_per_step_p50"], 4) if p50_dev else None,
+            "pinned_sequential": round(p50_seq / host_in["pinned_sequential"]["ms_per_step_p50"], 4)
+            if p50_seq else None}
     if c5 is not None:
         out["sharded_c5"] = c5
         out["sharded_c5_wholemap"] = c5_whole
