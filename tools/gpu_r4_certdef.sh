@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the A side: make -C form_amd/csrc BUILD=build_nocert OUT=../ab/libfmx_nocert.so EXTRA=-DFMX_WARM_CERT=0)
 # The warm certificate as the default build: the whole GPU suite, then an interleaved
 # A/B against the build without it (libfmx_nocert, FMX_WARM_CERT=0), C4 + C2.
 set -o pipefail
