@@ -639,6 +639,7 @@ ALG_BYTES_MODEL = {
              "probes and tests nothing (round 4: 87-92 % of warm queries)",
     "match_linearize": "per query 16 B read (+32 B planar normal of the winner); 64 B per brick probe, 32 B per "
                        "candidate record; 256 B of block partials per block",
+    "window": "72 B per plane row (p_i, n_i, p_j as fp64) + 48 B per point pair + 92 doubles of G per pair",
 }
 
 
@@ -816,6 +817,10 @@ def main():
     # dominant kernel by device time in the timed region
     name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
     roof = roofline(a, name, d, a.workload)
+    # the runner-up kernel class too (C4: match and the window linearization are within a
+    # few % of each other per scan)
+    ranked = sorted(prof.items(), key=lambda kv: -kv[1]["ms"])
+    roof_next = roofline(a, ranked[1][0], ranked[1][1], a.workload) if len(ranked) > 1 and ranked[1][1]["ms"] > 0 else None
     st_mean = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]} if stats else {}
     kern_ms = {k: round(v["ms"] / max(psteps, 1), 4) for k, v in prof.items()}
     kern_sum = sum(kern_ms.values())
@@ -848,6 +853,7 @@ def main():
         # this rank's median per-scan wall time (host noise shows in the mean, not here)
         "ms_per_step_p50": round(float(np.median(np.diff(marks))) * 1e3, 3),
         "roofline": roof,
+        "roofline_next": roof_next,
         "kernels_ms_per_step": kern_ms,
         "profile_steps": psteps,
         # the context (critical-path) stream's kernel time per scan (profile pass, HIP
