@@ -163,6 +163,10 @@ def sum_over_ranks(x, world, local):
     return _over_ranks(x, world, local, dist.ReduceOp.SUM)
 
 
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import provenance  # noqa: E402  (source hashes of the committed profiles: tools/provenance.py)
+
+
 def pmc_traffic(a, name, workload=None, with_source=False):
     """HBM bytes per launch of kernel class `name` from the committed PMC summary of this
     workload (tools/gpu_pmc.sh, tools/gpu_c5pmc.sh), or None; with_source: also
@@ -176,7 +180,8 @@ def pmc_traffic(a, name, workload=None, with_source=False):
             tj = json.load(f)
         if tj.get("workload") == workload and name in tj.get("kernels", {}):
             val = tj["kernels"][name]["hbm_bytes_per_launch"]
-            src = {"file": os.path.relpath(path, ROOT), "measured_at": tj.get("measured_at")}
+            src = {"file": os.path.relpath(path, ROOT), "measured_at": tj.get("measured_at"),
+                   **provenance.staleness(tj, "kernels")}
     except (OSError, ValueError, KeyError):
         pass
     return (val, src) if with_source else val
@@ -595,7 +600,7 @@ def sub_stream_line(a, wl, rank, world, local, single, pipe):
         stats.append(ctx.last_stats())
     ctx.sync()
     prof = ctx.profile_read()
-    work = ctx.match_work()
+    mwork = ctx.profile_match_work()
     ctx.close()
     t_max = max_over_ranks(t_local, world, local)
     scans_total = sum_over_ranks(float(steps), world, local)
@@ -626,7 +631,7 @@ def sub_stream_line(a, wl, rank, world, local, single, pipe):
         "main_stream_busy_frac": round(min(main_ms / ms, 1.0), 4),
         "host_round_trips_per_scan": round(st_mean.get("host_waits", 0.0), 2),
         "counters": st_mean,
-        "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
+        "match_work_per_query": match_work_split(mwork),
     }
     return line, (host, params, k0)
 
@@ -640,7 +645,21 @@ ALG_BYTES_MODEL = {
     "match_linearize": "per query 16 B read (+32 B planar normal of the winner); 64 B per brick probe, 32 B per "
                        "candidate record; 256 B of block partials per block",
     "window": "72 B per plane row (p_i, n_i, p_j as fp64) + 48 B per point pair + 92 doubles of G per pair",
+    "moments": "72 B per plane row (p_i, n_i, p_j as fp64) + 48 B per point pair + 2 x 136 doubles of moments "
+               "per pair",
 }
+
+
+def match_work_split(mw):
+    """fmx_profile_match_work -> per class: launches, and per query probes / candidates /
+    certified (the fraction of the class's queries)."""
+    out = {}
+    for k, v in mw.items():
+        q = max(v["queries"], 1.0)
+        out[k] = {"launches": int(v["launches"]), "queries_per_launch": round(v["queries"] / max(v["launches"], 1), 1),
+                  "probes": round(v["probes"] / q, 3), "candidates": round(v["candidates"] / q, 3),
+                  "certified": round(v["certified"] / q, 3), "warm": round(v["warm"] / q, 3)}
+    return out
 
 
 def roofline(a, name, d, workload):
@@ -668,13 +687,14 @@ def roofline(a, name, d, workload):
     # a chain of dependent memory rounds with the VALU issue sharing the SIMD
     sq = os.path.join(ROOT, "profiles", f"sq_wavestate_{workload}.json")
     try:
-        c = json.load(open(sq))["kernels"][name]["counters_per_launch"]
+        sqd = json.load(open(sq))
+        c = sqd["kernels"][name]["counters_per_launch"]
         wc = max(c["SQ_WAVE_CYCLES"], 1.0)
         roof["wave_cycles"] = dict(valu_active=round(c["SQ_ACTIVE_INST_VALU"] / wc, 3),
                                    memory_wait=round(c["SQ_WAIT_ANY"] / wc, 3),
                                    issue_wait=round(c["SQ_WAIT_INST_ANY"] / wc, 3),
                                    source=os.path.relpath(sq, ROOT),
-                                   measured_at=json.load(open(sq)).get("measured_at"))
+                                   measured_at=sqd.get("measured_at"), **provenance.staleness(sqd, "kernels"))
     except (OSError, KeyError, ValueError):
         pass
     return roof
@@ -784,6 +804,7 @@ def main():
     ctx.sync()
     prof = ctx.profile_read()
     work = ctx.match_work()
+    mwork = ctx.profile_match_work()
     ctx.profile(False)
     ctx.close()
     multi = {}
@@ -864,7 +885,10 @@ def main():
         "all_streams_kernel_ms_per_step": round(kern_sum, 4),
         "host_round_trips_per_scan": round(st_mean.get("host_waits", 0.0), 2),
         "counters": st_mean,
-        "match_work_per_query": {k: round(v / max(work["queries"], 1), 3) for k, v in work.items() if k != "queries"},
+        # every profiled match launch, each charged its own counters, cold (a scan's first
+        # match on its map) and warm (the ICP iterations after it) apart; certified: the
+        # warm queries the certificate settled without a search (fmx_match_cert)
+        "match_work_per_query": match_work_split(mwork),
     }
     if multi:
         # S independent streams on one GPU (per rank), each its own context, stream and
@@ -902,6 +926,7 @@ def main():
         with open(cp) as f:
             out["critical_path_trace"] = json.load(f)
         out["critical_path_trace"]["source"] = os.path.relpath(cp, ROOT)
+        out["critical_path_trace"].update(provenance.staleness(out["critical_path_trace"], "all"))
     if prev_aff is not None:
         os.sched_setaffinity(0, prev_aff)  # the CPU baseline's threads use every host core
     if host is not None:

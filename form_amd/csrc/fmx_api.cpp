@@ -40,6 +40,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
   HostScope hs(16);
+  ++c->corr_gen;
   c->match_group = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K);
   if (c->match_group != 8) gl::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
   else g8::run_match(c, pose_j34, max_dist, min_dist_map, sorted, defer_scatter);
@@ -67,7 +68,7 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
 // ============================================================================ profiling
 static const char* kProfNames[PROF_COUNT] = {"extract_rows", "closest",   "fit",       "compact", "map_build",
                                              "match",        "pair_sort", "linearize", "insert",  "window",
-                                             "match_linearize", "unpack"};
+                                             "match_linearize", "unpack", "moments"};
 
 ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), bytes(by), st(s) {
   if (!pr.on) return;
@@ -88,8 +89,15 @@ ProfScope::ProfScope(Prof& p, int i, double by, hipStream_t s) : pr(p), id(i), b
 ProfScope::~ProfScope() {
   if (!a) return;
   (void)hipEventRecord(b, st);
-  pr.pending.push_back({id, {a, b}});
-  pr.pending_bytes.push_back(bytes);
+  ProfPending e;
+  e.id = id;
+  e.a = a;
+  e.b = b;
+  e.bytes = bytes;
+  e.ring = ring;
+  e.warm = warm;
+  e.queries = queries;
+  pr.pending.push_back(e);
 }
 // every stream of the context: main, side (map build), side2 (pipelined extraction)
 static void sync_all(fmx_ctx* c) {
@@ -97,25 +105,50 @@ static void sync_all(fmx_ctx* c) {
   if (c->side) FMX_HIP(hipStreamSynchronize(c->side));
   if (c->side2) FMX_HIP(hipStreamSynchronize(c->side2));
 }
+// A match launch's algorithmic bytes: the per-launch part known at
+// launch time + 64 B per hash probe and 32 B per candidate record, the counts the launch
+// itself published to its ring slot.
 static void prof_collect(fmx_ctx* c) {
   Prof& pr = c->prof;
   if (pr.pending.empty()) return;
   sync_all(c);  // profiled launches run on all three streams
-  for (size_t i = 0; i < pr.pending.size(); ++i) {
-    auto& [id, ev] = pr.pending[i];
+  for (ProfPending& e : pr.pending) {
     float ms = 0.f;
-    FMX_HIP(hipEventElapsedTime(&ms, ev.first, ev.second));
-    pr.ms[id] += ms;
-    pr.launches[id] += 1;
-    pr.bytes[id] += pr.pending_bytes[i];
-    pr.free_events.push_back(ev.first);
-    pr.free_events.push_back(ev.second);
+    FMX_HIP(hipEventElapsedTime(&ms, e.a, e.b));
+    double bytes = e.bytes;
+    if (e.ring >= 0) {
+      const uint32_t* w = pr.wring.p + 4 * (size_t)e.ring;
+      const double probes = w[0], cands = w[1];
+      bytes += 64.0 * probes + 32.0 * cands;
+      double* m = pr.mwork[e.warm ? 1 : 0];
+      m[0] += 1;
+      m[1] += e.queries;
+      m[2] += probes;
+      m[3] += cands;
+      m[4] += w[2];
+      m[5] += w[3];
+    }
+    pr.ms[e.id] += ms;
+    pr.launches[e.id] += 1;
+    pr.bytes[e.id] += bytes;
+    pr.free_events.push_back(e.a);
+    pr.free_events.push_back(e.b);
   }
   pr.pending.clear();
-  pr.pending_bytes.clear();
+  pr.wnext = 0;
+}
+int prof_ring_slot(fmx_ctx* c) {
+  Prof& pr = c->prof;
+  if (!pr.on) return -1;
+  if (!pr.wring.p) pr.wring.ensure(4 * (size_t)kProfRing);
+  if (pr.wnext >= kProfRing) prof_collect(c);  // every slot pending: collect (syncs) and reuse
+  const int s = (int)pr.wnext++;
+  std::memset(pr.wring.p + 4 * (size_t)s, 0, 4 * sizeof(uint32_t));
+  return s;
 }
 }  // namespace fmx
 
+#include "moments.hpp"
 #include "pose.hpp"
 #include "smoother.hpp"
 using namespace fmxh;
@@ -175,7 +208,16 @@ void settle_match(fmx_ctx* c) {
 }
 // Entry points that discard the match results (a new query set, an extraction,
 // register_scan) drop a deferred match instead of launching it: nothing could read it.
-void drop_match(fmx_ctx* c) { c->lazy.pending = false; }
+// The results of any earlier match are gone with it (the deferred match replaced them),
+// also when the dropping call then fails its own checks: no later reader may take an
+// older match's outputs for the dropped one's.
+void drop_match(fmx_ctx* c) {
+  if (!c->lazy.pending) return;
+  c->lazy.pending = false;
+  c->have_match = false;
+  c->have_qo = false;
+  c->have_corr = false;
+}
 
 // SETTLE: run a deferred fmx_match first — every entry point but fmx_match itself,
 // fmx_linearize_matched (which may consume it fused) and those that read no match
@@ -582,6 +624,14 @@ struct fmx_ctx::Est {
   // every stored pair's linearization at `values` (the last full LM's final state),
   // keyed (j, i): m_fast_linear and marginalize reuse it
   std::map<std::pair<uint64_t, uint64_t>, std::vector<double>> gcache;
+  // pair moments (moments.hpp) of every stored pair, keyed (j, i): the rows of scan j's
+  // last match, taken at reference poses; the LMs linearize the pairs from them on the
+  // host (FMX_LIN_ROWS=1: the per-row device linearization over the window store instead)
+  struct Mom {
+    Pose ref_i, ref_j;
+    std::vector<double> phi;  // kMomPairD
+  };
+  std::map<std::pair<uint64_t, uint64_t>, Mom> moms;
   // marginalization of the scans the last keyscan step dropped, deferred to the next
   // register_scan where it runs while that scan's extraction kernels execute
   bool tail_pending = false;
@@ -788,6 +838,7 @@ void set_lin(WinGraph& g, B begin, E end) {
 void swap_match_set(fmx_ctx* c) {
   MatchSet& S = c->spec;
   using std::swap;
+  ++c->corr_gen;
   swap(c->m_pair, S.m_pair); swap(c->m_d2, S.m_d2); swap(c->m_pi, S.m_pi); swap(c->m_ni, S.m_ni);
   swap(c->m_ins, S.m_ins); swap(c->hist, S.hist); swap(c->hist_off, S.hist_off); swap(c->thist, S.thist);
   swap(c->c_pl, S.c_pl); swap(c->c_pt, S.c_pt); swap(c->pair_counts, S.pair_counts);
@@ -801,7 +852,7 @@ void swap_match_set(fmx_ctx* c) {
   swap(c->match_nb_pl, S.match_nb_pl); swap(c->match_nb, S.match_nb); swap(c->n_qo, S.n_qo);
   swap(c->match_group, S.match_group); swap(c->ps, S.ps); swap(c->rows_pl, S.rows_pl); swap(c->rows_pt, S.rows_pt);
   swap(c->cnt_pl, S.cnt_pl); swap(c->cnt_pt, S.cnt_pt); swap(c->last_probes, S.last_probes);
-  swap(c->last_cands, S.last_cands); swap(c->ins_tot, S.ins_tot);
+  swap(c->last_cands, S.last_cands); swap(c->ins_tot, S.ins_tot); swap(c->cert_tot, S.cert_tot);
 }
 
 // Speculative match (smoothing-mode ICP): when an LM trial is probably the LM's last
@@ -839,6 +890,20 @@ bool use_spec_match(fmx_ctx* c, const double* pose_j) {
 void keyscan_step(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat);
 void record_cons(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j);
 
+// FMX_LIN_ROWS=1 (A/B): the smoother's LMs linearize every trial on the device from the
+// rows (k_win_linearize over the sorted match / the window store), as before round 5;
+// default: from the pair moments (k_win_moments once per ICP iteration, moments.cpp)
+bool lin_rows() {
+  static const bool v = std::getenv("FMX_LIN_ROWS") != nullptr;
+  return v;
+}
+// FMX_FULL_ROWS=1 (A/B): the final LM (every stored pair) linearizes on the device from
+// the window store's rows even when the ICP loop uses moments
+bool full_rows() {
+  static const bool v = std::getenv("FMX_FULL_ROWS") != nullptr;
+  return v;
+}
+
 // ICP loop (form.cpp:67-89) + optimize(false) (form.cpp:92-93) in smoothing mode:
 // every LM runs over all window poses; the current scan's FeatureFactors linearize
 // from the sorted match, the stored pairs from the window store (window.hip).
@@ -857,6 +922,13 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
   for (auto& m : e.margs) g.lins.push_back(&m);
   if (!fast.keys.empty()) g.lins.push_back(&fast);
   std::vector<double> table;
+  const bool mom = !lin_rows();
+  const bool mom_full = mom && !full_rows();  // the final LM from the stored pairs' moments too
+  std::vector<double> momv;                  // the current scan's pair moments (K x kMomPairD)
+  std::vector<Pose> mref;                    // ... their reference poses: [k] pair k's X(i), [K] X(j)
+  std::vector<const double*> mp;             // contraction arguments (moments.hpp)
+  std::vector<const Pose*> mri, mrj, mxi, mxj;
+  MomBatch mbatch;
   for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
     ++icp;
     const Pose before = e.values.at(j);
@@ -867,18 +939,12 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     g.pairs.clear();
     for (uint32_t k = 0; k < c->K; ++k) g.pairs.push_back({slot.at(c->map_scans[k]), slot.at(j)});
     const int K = (int)c->K;
-    // split form: launch, the host assembles the non-pair terms, then wait (smoother.hpp)
-    auto lin_begin = [&](const std::vector<Pose>& x) {
-      table.resize(12 * ((size_t)K + 1));
-      for (int k = 0; k < K; ++k) std::memcpy(&table[12 * k], x[slot.at(c->map_scans[k])].m, 12 * sizeof(double));
-      std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
-      HostScope hs(10);
-      win_linearize_current(c, table.data(), sigma, nullptr);
-      // an LM trial the LM will probably stop after (its predicted decrease within the
-      // LM's convergence tolerances, rel/abs 1e-5; the actual decrease decides and
-      // tracks the prediction closely on this stream, profiles/r2_spec_log.txt): match
-      // its X(j) speculatively — the next ICP iteration starts from the LM's final
-      // X(j).  A trial predicted to decrease more is followed by another.
+    // an LM trial the LM will probably stop after (its predicted decrease within the
+    // LM's convergence tolerances, rel/abs 1e-5; the actual decrease decides and tracks
+    // the prediction closely on this stream, profiles/r2_spec_log.txt): match its X(j)
+    // speculatively — the next ICP iteration starts from the LM's final X(j).  A trial
+    // predicted to decrease more is followed by another.
+    auto maybe_spec = [&](const std::vector<Pose>& x) {
       const Pose& xj = x[slot.at(j)];
       const double lc = g.trial_lin_change, ce = g.trial_err;
       bool last_likely = lc >= 0.0 && (lc <= 1e-5 * ce || lc <= 1e-5);
@@ -893,14 +959,63 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       if (last_likely && it + 1 < P.max_num_rematches && std::memcmp(xj.m, before.m, sizeof(xj.m)) != 0)
         spec_match(c, xj.m);
     };
-    auto lin_end = [&](double* G) {
-      HostScope hs(10);
-      win_finish(c, G);
-      match_counts_fetch(c, false);  // the match finished before the linearization
-      for (int k = 0; k < K; ++k)
-        if (c->cnt_pl[k] + c->cnt_pt[k] == 0) std::fill(G + (size_t)k * kPairG, G + (size_t)(k + 1) * kPairG, 0.0);
-    };
-    set_lin(g, lin_begin, lin_end);
+    if (mom) {
+      // the pairs' moments at the LM's starting values (one launch, one wait); every
+      // linearization of this LM is then a host contraction (moments.hpp)
+      const std::vector<Pose> x0 = window_poses(e);
+      mref.resize((size_t)K + 1);
+      table.resize(12 * ((size_t)K + 1));
+      for (int k = 0; k < K; ++k) mref[k] = x0[slot.at(c->map_scans[k])];
+      mref[K] = x0[slot.at(j)];
+      for (int k = 0; k <= K; ++k) std::memcpy(&table[12 * k], mref[k].m, 12 * sizeof(double));
+      momv.resize((size_t)std::max(K, 1) * kMomPairD);
+      {
+        HostScope hs(10);
+        win_moments_current(c, table.data(), momv.data());
+        match_counts_fetch(c, false);  // the match finished before the moments
+      }
+      for (int k = 0; k < K; ++k)  // pairs without rows are never written by the kernel
+        if (c->cnt_pl[k] + c->cnt_pt[k] == 0) std::fill(&momv[(size_t)k * kMomPairD], &momv[(size_t)(k + 1) * kMomPairD], 0.0);
+      mp.resize(K);
+      mri.resize(K);
+      mrj.assign(K, &mref[K]);
+      mxi.resize(K);
+      mxj.resize(K);
+      for (int k = 0; k < K; ++k) {
+        mp[k] = &momv[(size_t)k * kMomPairD];
+        mri[k] = &mref[k];
+      }
+      mom_prepare(mbatch, K, mp.data(), mri.data(), mrj.data());
+      g.lin_begin = nullptr;
+      g.lin_end = nullptr;
+      g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
+        HostScope hs(10);
+        maybe_spec(x);
+        for (int k = 0; k < K; ++k) {
+          mxi[k] = &x[slot.at(c->map_scans[k])];
+          mxj[k] = &x[slot.at(j)];
+        }
+        mom_eval(mbatch, mxi.data(), mxj.data(), 1.0 / sigma, G);
+      };
+    } else {
+      // split form: launch, the host assembles the non-pair terms, then wait (smoother.hpp)
+      auto lin_begin = [&](const std::vector<Pose>& x) {
+        table.resize(12 * ((size_t)K + 1));
+        for (int k = 0; k < K; ++k) std::memcpy(&table[12 * k], x[slot.at(c->map_scans[k])].m, 12 * sizeof(double));
+        std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
+        HostScope hs(10);
+        win_linearize_current(c, table.data(), sigma, nullptr);
+        maybe_spec(x);
+      };
+      auto lin_end = [&](double* G) {
+        HostScope hs(10);
+        win_finish(c, G);
+        match_counts_fetch(c, false);  // the match finished before the linearization
+        for (int k = 0; k < K; ++k)
+          if (c->cnt_pl[k] + c->cnt_pt[k] == 0) std::fill(G + (size_t)k * kPairG, G + (size_t)(k + 1) * kPairG, 0.0);
+      };
+      set_lin(g, lin_begin, lin_end);
+    }
     HostScope* hs_lm = new HostScope(8);
     const WinLMResult R = window_lm(g, window_poses(e));
     delete hs_lm;
@@ -918,9 +1033,20 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     if (std::sqrt(dn) < P.new_pose_threshold) break;
     e.values[j] = after;  // update_current_pose
   }
-  // the last match is the scan's constraint set: into the window store
+  // the last match is the scan's constraint set: into the window store (its pair
+  // moments, or its rows for FMX_LIN_ROWS)
   record_cons(c, e, j);
-  win_persist(c, j);
+  if (mom_full) {
+    for (uint32_t k = 0; k < c->K; ++k)
+      if (c->cnt_pl[k] + c->cnt_pt[k] > 0) {
+        fmx_ctx::Est::Mom& m = e.moms[{j, c->map_scans[k]}];
+        m.ref_i = mref[k];
+        m.ref_j = mref[c->K];
+        m.phi.assign(momv.begin() + (size_t)k * kMomPairD, momv.begin() + (size_t)(k + 1) * kMomPairD);
+      }
+  } else {
+    win_persist(c, j);
+  }
   // insert_matches (form.cpp:98-100) reads only the last match (local keypoints and
   // their NN distances), not the poses optimize(false) moves: its kernel goes ahead of
   // the full LM, off the scan's tail
@@ -942,41 +1068,76 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
   int spec_builds = 0;
   pf_launch(c, false);  // a host-announced next scan staged by now
   // optimize(false): every stored pair's FeatureFactor (constraints.cpp:294-305)
-  const std::vector<WinPair> prs = win_pairs(c);
+  std::vector<WinPair> prs;
+  if (mom_full) {  // (j ascending, i ascending: the window store's order)
+    for (auto& [ji, m] : e.moms) prs.push_back(WinPair{ji.second, ji.first, 0, 0, 0, 0});
+  } else {
+    prs = win_pairs(c);
+  }
   g.lins.clear();
   for (auto& m : e.margs) g.lins.push_back(&m);
   g.pairs.clear();
   for (auto& p : prs) g.pairs.push_back({slot.at(p.i), slot.at(p.j)});
-  if (!prs.empty()) win_set_pairs(c, prs, keys);
-  auto lin_begin = [&](const std::vector<Pose>& x) {
-    table.resize(12 * keys.size());
-    for (size_t k = 0; k < keys.size(); ++k) std::memcpy(&table[12 * k], x[k].m, 12 * sizeof(double));
-    HostScope hs(10);
-    win_linearize_stored(c, table.data(), (int)keys.size(), sigma, nullptr);
-    // Speculative map build: a trial the LM will probably stop after (predicted decrease
-    // within its 1e-5 tolerances, as for the speculative match) gives the poses the
-    // next scan's map is built from; build it now on the side stream, behind the insert,
-    // while this LM and the next scan's extraction run.  register_scan(j+1) keeps it
-    // only if its map inputs are exactly these.
+  if (!prs.empty() && !mom_full) win_set_pairs(c, prs, keys);
+  // Speculative map build: a trial the LM will probably stop after (predicted decrease
+  // within its 1e-5 tolerances, as for the speculative match) gives the poses the next
+  // scan's map is built from; build it now on the side stream, behind the insert, while
+  // this LM and the next scan's extraction run.  register_scan(j+1) keeps it only if its
+  // map inputs are exactly these.
+  auto maybe_spec_map = [&](const std::vector<Pose>& x) {
     const double lc = g.trial_lin_change, ce = g.trial_err;
     if (lc >= 0.0 && (lc <= 1e-5 * ce || lc <= 1e-5) && spec_builds < 2 && !map_scans.empty()) {
       ++spec_builds;
-      std::vector<double> mp(12 * map_scans.size());
-      for (size_t k = 0; k < map_scans.size(); ++k) std::memcpy(&mp[12 * k], x[slot.at(map_scans[k])].m, 12 * sizeof(double));
+      std::vector<double> mpo(12 * map_scans.size());
+      for (size_t k = 0; k < map_scans.size(); ++k) std::memcpy(&mpo[12 * k], x[slot.at(map_scans[k])].m, 12 * sizeof(double));
       if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));  // pinned staging reuse (see register_scan)
       FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      run_map_build(c, map_scans, mp.data(), P.max_dist_matching, c->side);
+      run_map_build(c, map_scans, mpo.data(), P.max_dist_matching, c->side);
       FMX_HIP(hipEventRecord(c->ev_join, c->side));
       e.spec_map = true;
       e.spec_map_scans = map_scans;
-      e.spec_map_poses = std::move(mp);
+      e.spec_map_poses = std::move(mpo);
     }
   };
-  auto lin_end = [&](double* G) {
-    HostScope hs(10);
-    win_finish(c, G);
-  };
-  set_lin(g, lin_begin, lin_end);
+  if (mom_full) {
+    const size_t np = prs.size();
+    mp.resize(np);
+    mri.resize(np);
+    mrj.resize(np);
+    mxi.resize(np);
+    mxj.resize(np);
+    for (size_t p = 0; p < np; ++p) {
+      const fmx_ctx::Est::Mom& m = e.moms.at({prs[p].j, prs[p].i});
+      mp[p] = m.phi.data();
+      mri[p] = &m.ref_i;
+      mrj[p] = &m.ref_j;
+    }
+    mom_prepare(mbatch, (int)np, mp.data(), mri.data(), mrj.data());
+    g.lin_begin = nullptr;
+    g.lin_end = nullptr;
+    g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
+      HostScope hs(10);
+      maybe_spec_map(x);
+      for (size_t p = 0; p < np; ++p) {
+        mxi[p] = &x[g.pairs[p].first];
+        mxj[p] = &x[g.pairs[p].second];
+      }
+      mom_eval(mbatch, mxi.data(), mxj.data(), 1.0 / sigma, G);
+    };
+  } else {
+    auto lin_begin = [&](const std::vector<Pose>& x) {
+      table.resize(12 * keys.size());
+      for (size_t k = 0; k < keys.size(); ++k) std::memcpy(&table[12 * k], x[k].m, 12 * sizeof(double));
+      HostScope hs(10);
+      win_linearize_stored(c, table.data(), (int)keys.size(), sigma, nullptr);
+      maybe_spec_map(x);
+    };
+    auto lin_end = [&](double* G) {
+      HostScope hs(10);
+      win_finish(c, G);
+    };
+    set_lin(g, lin_begin, lin_end);
+  }
   HostScope* hs_lm = new HostScope(9);
   const WinLMResult R = window_lm(g, window_poses(e));
   delete hs_lm;
@@ -1118,6 +1279,8 @@ void finish_tail(fmx_ctx* c, fmx_ctx::Est& e) {
   if (!P.disable_smoothing) smooth_marginalize(e, marg);
   for (uint64_t m : marg) {
     if (!P.disable_smoothing) win_remove(c, m);
+    for (auto it = e.moms.begin(); it != e.moms.end();)  // pairs (m, j) and (i, m)
+      it = it->first.first == m || it->first.second == m ? e.moms.erase(it) : std::next(it);
     e.values.erase(m);
     e.cons.erase(m);
     for (auto& [jj, mm] : e.cons) mm.erase(m);
@@ -1379,12 +1542,14 @@ void fmx_destroy(fmx_ctx* c) {
   if (c->side2) (void)hipStreamSynchronize(c->side2);
   for (auto& e : c->prof.free_events) (void)hipEventDestroy(e);
   for (auto& pe : c->prof.pending) {
-    (void)hipEventDestroy(pe.second.first);
-    (void)hipEventDestroy(pe.second.second);
+    (void)hipEventDestroy(pe.a);
+    (void)hipEventDestroy(pe.b);
   }
+  c->prof.wring.release();
   delete c->est;
   comm_destroy(c);
   c->d_sum.release();
+  c->h_hold.release();
   // DBuf/HBuf members do not free in their destructors: release explicitly.
   c->scan.release(); c->planar_mask.release(); c->sel_slots.release(); c->pt_slots.release();
   c->row_counts.release(); c->row_ok.release(); c->row_off.release(); c->closest.release();
@@ -1419,7 +1584,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
-  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release();
+  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release(); c->mcert.release(); c->mprof.release();
   c->cert_b2.release();
   {
     auto& S = c->spec;
@@ -1433,7 +1598,7 @@ void fmx_destroy(fmx_ctx* c) {
     auto& W = c->win;
     for (int b = 0; b < 2; ++b) { W.pl[b].release(); W.pt[b].release(); }
     W.meta.release(); if (W.meta_ev) (void)hipEventDestroy(W.meta_ev); W.partials.release(); W.dposes.release();
-    W.pticket.release(); W.dticket.release(); W.dflag.release(); W.dbg.release(); W.hG.release(); W.hposes.release(); W.hmeta.release();
+    W.pticket.release(); W.dticket.release(); W.dflag.release(); W.dbg.release(); W.hG.release(); W.hM.release(); W.hposes.release(); W.hmeta.release();
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -1540,6 +1705,7 @@ fmx_status fmx_map_build(fmx_ctx* c, const uint64_t* scans, const double* poses,
 fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint32_t* cpl, uint32_t* cpt) {
   return guard<false>(c, [&] {
     c->lazy.pending = false;  // a newer match replaces a deferred one
+    ++c->corr_gen;
     if (!c->have_map) throw StatusError(FMX_E_STATE, "fmx_map_build first");
     if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
     if (!(max_dist > 0)) throw StatusError(FMX_E_INVAL, "max_dist must be > 0");
@@ -1618,6 +1784,7 @@ fmx_status fmx_corr_set(fmx_ctx* c, uint32_t K, const uint32_t* np, const double
                         const double* ppj, const uint32_t* nt, const double* tpi, const double* tpj) {
   return guard(c, [&] {
     if (K && (!np || !nt)) throw StatusError(FMX_E_INVAL, "null counts");
+    ++c->corr_gen;
     upload_corr(c, K, np, ppi, pni, ppj, nt, tpi, tpj);
   });
 }
@@ -1629,6 +1796,41 @@ fmx_status fmx_linearize(fmx_ctx* c, const double* pi, const double* pj, double 
     if (c->K && (!pi || !pj)) throw StatusError(FMX_E_INVAL, "null poses");
     win_linearize_pairs(c, pi, pj, sigma, single ? 1 : 0, G, err);
   });
+}
+
+fmx_status fmx_moments(fmx_ctx* c, const double* pi, const double* pj, double* mom) {
+  return guard(c, [&] {
+    if (c->K && (!pi || !pj || !mom)) throw StatusError(FMX_E_INVAL, "null poses / output");
+    win_moments_pairs(c, pi, pj, mom);
+  });
+}
+
+fmx_status fmx_moments_contract(uint32_t K, const double* mom, const double* ri, const double* rj, const double* pi,
+                                const double* pj, double sigma, double* G, double* err) {
+  if (K == 0) return FMX_OK;
+  if (!mom || !ri || !rj || !pi || !pj || !(sigma > 0)) return FMX_E_INVAL;
+  try {
+    std::vector<const double*> m(K);
+    std::vector<const Pose*> a(K), b(K), x(K), y(K);
+    for (uint32_t k = 0; k < K; ++k) {
+      m[k] = mom + (size_t)kMomPairD * k;
+      a[k] = reinterpret_cast<const Pose*>(ri + 12 * (size_t)k);
+      b[k] = reinterpret_cast<const Pose*>(rj + 12 * (size_t)k);
+      x[k] = reinterpret_cast<const Pose*>(pi + 12 * (size_t)k);
+      y[k] = reinterpret_cast<const Pose*>(pj + 12 * (size_t)k);
+    }
+    std::vector<double> g((size_t)K * 92);
+    MomBatch mb;
+    mom_prepare(mb, (int)K, m.data(), a.data(), b.data());
+    mom_eval(mb, x.data(), y.data(), 1.0 / sigma, g.data());
+    for (uint32_t k = 0; k < K; ++k) {
+      if (G) std::memcpy(G + 91 * (size_t)k, &g[92 * (size_t)k], 91 * sizeof(double));
+      if (err) err[k] = g[92 * (size_t)k + 91];
+    }
+    return FMX_OK;
+  } catch (const std::bad_alloc&) {
+    return FMX_E_OOM;
+  }
 }
 
 fmx_status fmx_error(fmx_ctx* c, const double* pi, const double* pj, double sigma, double* err) {
@@ -1722,7 +1924,14 @@ fmx_status fmx_comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank
 
 fmx_status fmx_next_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev) {
   return guard<false>(c, [&] {
+    // a pageable announcement being withdrawn or replaced: its staging copy still reads
+    // the caller's array on the helper threads — finish it before returning, so the
+    // caller may free or reuse that memory once this call is back
+    auto retire_announced = [&] {
+      if (c->ann_ptr && c->ann_host && !c->ann_pinned) c->stager.retire(&c->st_pf[c->ann_slot]);
+    };
     if (!xyzw) {  // withdraw the announcement
+      retire_announced();
       c->ann_ptr = nullptr;
       return;
     }
@@ -1730,6 +1939,7 @@ fmx_status fmx_next_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev) {
     if (n != (size_t)E.num_rows * (size_t)E.num_columns)
       throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " +
                                         std::to_string((size_t)E.num_rows * E.num_columns) + " != " + std::to_string(n));
+    retire_announced();
     c->ann_pinned = !on_dev && host_pinned(xyzw, n * sizeof(float4));
     if (!on_dev && !c->ann_pinned) {
       // a pageable host scan: its staging copy into a pinned slot starts now, in the
@@ -1757,6 +1967,14 @@ fmx_status fmx_scan_buffer(fmx_ctx* c, size_t n, float** out) {
     if (B.cap < n) {
       // the buffer may feed a queued DMA (a registered or announced scan): drain first
       sync_all(c);
+      if (B.p) {
+        // an announcement or a queued extraction of a scan in this buffer would otherwise
+        // outlive it (a new buffer may even come back at the same address)
+        const float* b0 = reinterpret_cast<const float*>(B.p);
+        const float* b1 = reinterpret_cast<const float*>(B.p + B.cap);
+        if (c->ann_ptr >= b0 && c->ann_ptr < b1) c->ann_ptr = nullptr;
+        if (c->pf_launched && c->pf_ptr >= b0 && c->pf_ptr < b1) pf_drop(c);
+      }
       if (B.p) (void)hipHostFree(B.p);
       B.p = nullptr;
       B.cap = 0;
@@ -1852,6 +2070,39 @@ fmx_status fmx_match_work(fmx_ctx* c, double work[3]) {
   });
 }
 
+fmx_status fmx_match_cert(fmx_ctx* c, uint64_t counts[2], uint8_t* certified) {
+  return guard(c, [&] {
+    if (!c->have_match) throw StatusError(FMX_E_STATE, "no match results");
+    match_counts_fetch(c);
+    if (counts) {
+      counts[0] = c->cert_tot[0];
+      counts[1] = c->cert_tot[1];
+    }
+    if (certified) {
+      const uint32_t nq = c->n_qpl + c->n_qpt;
+      std::vector<uint8_t> f(nq);
+      if (nq) FMX_HIP(hipMemcpy(f.data(), c->m_ins.p, nq, hipMemcpyDeviceToHost));
+      for (uint32_t q = 0; q < nq; ++q) certified[q] = (f[q] >> 1) & 1;
+    }
+  });
+}
+
+fmx_status fmx_profile_match_work(fmx_ctx* c, double out[12]) {
+  return guard<false>(c, [&] {
+    if (!out) throw StatusError(FMX_E_INVAL, "null output");
+    prof_collect(c);
+    for (int k = 0; k < 2; ++k)
+      for (int i = 0; i < 6; ++i) out[6 * k + i] = c->prof.mwork[k][i];
+  });
+}
+
+fmx_status fmx_corr_generation(fmx_ctx* c, uint64_t* gen) {
+  return guard<false>(c, [&] {
+    if (!gen) throw StatusError(FMX_E_INVAL, "null output");
+    *gen = c->corr_gen;
+  });
+}
+
 fmx_status fmx_profile_enable(fmx_ctx* c, int on) {
   return guard<false>(c, [&] { c->prof.on = on != 0; });
 }
@@ -1863,6 +2114,7 @@ fmx_status fmx_profile_reset(fmx_ctx* c) {
       c->prof.launches[i] = 0;
       c->prof.bytes[i] = 0;
     }
+    std::memset(c->prof.mwork, 0, sizeof(c->prof.mwork));
   });
 }
 int fmx_profile_count(void) { return PROF_COUNT; }

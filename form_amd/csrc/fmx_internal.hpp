@@ -108,17 +108,34 @@ enum ProfId {
   PROF_WINDOW,
   PROF_MATCH_LIN,
   PROF_UNPACK,
+  PROF_MOMENTS,
   PROF_COUNT
 };
 
+// Per-launch work words of a profiled match (probes, candidates), written by the
+// launch's last block to pinned memory: each launch's byte model uses its OWN counts
+// (fmx_api.cpp prof_collect), no launch is charged another's.
+constexpr uint32_t kProfRing = 8192;
+struct ProfPending {
+  int id;
+  hipEvent_t a, b;
+  double bytes;
+  int ring = -1;    // match launches: slot in Prof::wring, else -1
+  int warm = 0;     // ... 1: a warm-started launch (an earlier match on this map and query set)
+  double queries = 0;
+};
 struct Prof {
   bool on = false;
   double ms[PROF_COUNT] = {};
   uint64_t launches[PROF_COUNT] = {};
   double bytes[PROF_COUNT] = {};
-  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
-  std::vector<double> pending_bytes;
+  // match work since the last reset, [cold, warm] x {launches, queries, probes, candidates,
+  // certified queries, warm queries}
+  double mwork[2][6] = {};
+  std::vector<ProfPending> pending;
   std::vector<hipEvent_t> free_events;
+  HBuf<uint32_t> wring;  // [kProfRing][4]: probes, candidates, certified, warm (pinned, mapped)
+  uint32_t wnext = 0;    // next slot; slots in use = pending entries with ring >= 0
 };
 
 // Scoped kernel timer: HIP events on the context stream around one launch group.
@@ -128,6 +145,8 @@ struct ProfScope {
   double bytes;
   hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
+  int ring = -1, warm = 0;  // a match launch's work slot (prof_ring_slot) and class
+  double queries = 0;
   ProfScope(Prof& p, int i, double by, hipStream_t s);
   ~ProfScope();
 };
@@ -233,9 +252,10 @@ struct WinStore {
   DBuf<uint64_t> dbg;  // FMX_WIN_TIMING stamps
   DBuf<uint32_t> pticket, dticket, dflag;  // dflag: the completion word of a sharded launch
   bool pending = false;  // a k_win_linearize launched by win_start, not yet finished
+  bool pending_mom = false;  // ... a k_win_moments (its results in hM)
   uint32_t pending_seq = 0, pending_grid = 0;
   int pending_np = 0;
-  HBuf<double> hG, hposes;
+  HBuf<double> hG, hM, hposes;  // hM: per pair 2 x 136 moments (k_win_moments)
   HBuf<uint32_t> hmeta;
 };
 
@@ -263,6 +283,7 @@ struct MatchSet {
   std::vector<uint32_t> cnt_pl, cnt_pt;
   double last_probes = 0, last_cands = 0;
   uint32_t ins_tot[2] = {0, 0};
+  uint32_t cert_tot[2] = {0, 0};
 };
 
 // An extraction launched on stream `st`: its totals and completion word go to mapped
@@ -386,6 +407,7 @@ struct fmx_ctx {
 
   // ---- sorted correspondences (pair-major SoA) + chunk table
   uint32_t K = 0;
+  uint64_t corr_gen = 0;         // bumped by every call that replaces the correspondences (fmx_corr_generation)
   fmx::DBuf<double> c_pl, c_pt;  // [9][cap_pl], [6][cap_pt]
   size_t ld_pl = 0, ld_pt = 0;
   fmx::DBuf<uint32_t> pair_counts;  // [2][K] plane rows, point pairs
@@ -422,6 +444,9 @@ struct fmx_ctx {
   uint32_t fz_work_blocks = 0;
   fmx::DBuf<uint32_t> ins_blk, ins_off;           // per match block insert counts / offsets
   uint32_t ins_tot[2] = {0, 0};                   // insert totals of the last match
+  uint32_t cert_tot[2] = {0, 0};                  // ... its certified / warm query counts
+  fmx::DBuf<uint32_t> mcert;                      // the match launches' certified / warm sums (self-resetting)
+  fmx::DBuf<uint32_t> mprof;                      // profiled match launches' probe / candidate sums (self-resetting)
   uint32_t match_nb_pl = 0, match_nb = 0;         // blocks of the last match
   uint32_t n_qo = 0;                              // queries of the last query-order match
   fmx::HBuf<uint32_t> h_flag;                     // mapped completion word (wait_flag)
@@ -457,6 +482,7 @@ struct fmx_ctx {
   void* comm = nullptr;
   int comm_size = 1, comm_rank = 0;
   fmx::DBuf<double> d_sum;  // device-side linearization sums all-reduced in place
+  fmx::HBuf<uint32_t> h_hold;  // FMX_TEST_WITHHOLD_FLAG: the word that releases a withheld publish
 
   // ---- host estimator state (register_scan)
   struct Est;
@@ -697,6 +723,9 @@ constexpr uint32_t kMatchTileMaxPairs = 256;
 namespace g8 { FMX_VM_DECLS }
 namespace gl { FMX_VM_DECLS }
 #undef FMX_VM_DECLS
+// A free slot of the profiler's work ring for a match launch about to be profiled
+// (collects pending results first when every slot is taken); -1 when not profiling.
+int prof_ring_slot(fmx_ctx* c);
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
                         uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq);
@@ -736,7 +765,11 @@ std::vector<WinPair> win_pairs(fmx_ctx* c);
 void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vector<uint64_t>& keys);
 void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out);
 void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
-void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* called with G_out = null
+void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* / win_moments_* called with G_out = null
+// pair moments (k_win_moments): per pair 2 x 136 doubles (plane, point; packed upper 16 x 16)
+constexpr int kMomPair = 272;
+void win_moments_current(fmx_ctx* c, const double* poses, double* out);
+void win_moments_pairs(fmx_ctx* c, const double* poses_i, const double* poses_j, double* out);
 // comm.cpp: RCCL communicator of the sharded path, all-reduce on the context stream
 // FORM::map() snapshot (snapshot.hip): world-frame keypoints of feature type t of
 // `scans` at `poses`, grouped by voxel of width w; returns the record count

@@ -521,6 +521,14 @@ struct MatchArgs {
   int cert_ok;  // cert_b2 holds the bounds of the match that wrote the warm records
                 // (an 8-lane match on this map and query set; the one-lane build keeps none)
 #endif
+  // per launch: [0] certified queries, [1] warm queries (agent-scope sums of the
+  // blocks' counts, published by the last block to host_counts[2K + 2 ..] and zeroed)
+  uint32_t* cert_cnt;
+  // profiled launches only (else null): the launch's total probes / candidates, summed
+  // in prof_acc (agent scope, self-resetting) and stored by the last block to prof_work
+  // (its pinned slot of the profiler's work ring: the byte model of THIS launch)
+  uint32_t* prof_acc;
+  uint32_t* prof_work;
 };
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
@@ -1432,7 +1440,7 @@ __device__ __forceinline__ bool match_result(const MatchArgs& a, const MapView& 
                                              uint32_t best_i, uint32_t sg, const double* __restrict__ inv_poses,
                                              int32_t* __restrict__ m_pair, double* __restrict__ m_d2,
                                              double4* __restrict__ m_pi, double4* __restrict__ m_ni,
-                                             uint8_t* __restrict__ m_ins, int32_t& pair_out) {
+                                             uint8_t* __restrict__ m_ins, int32_t& pair_out, bool cert = false) {
   const bool found = best_i != 0xFFFFFFFFu;
   int32_t pair = -1;
   double4 pi = make_double4(0, 0, 0, 0), ni = make_double4(0, 0, 0, 0);
@@ -1457,7 +1465,7 @@ __device__ __forceinline__ bool match_result(const MatchArgs& a, const MapView& 
   m_pi[gq] = pi;
   if (planar) m_ni[q] = ni;
   const bool ins = !found || best > a.min_d2;
-  m_ins[gq] = ins ? 1 : 0;
+  m_ins[gq] = (ins ? 1 : 0) | (cert ? 2 : 0);  // bit 0: insert (k_insert); bit 1: settled by the warm certificate
   if (a.rec) a.rec[gq] = best_i;  // the next match's warm start
   pair_out = pair;
   return ins;
@@ -1575,9 +1583,10 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     const float4 lq = planar ? q_pl[q] : q_pt[q];
     d_xform(Tj, (double)lq.x, (double)lq.y, (double)lq.z, wq);  // kp->transform(init), matcher.hpp:89
   };
-  auto emit = [&](uint32_t q, double best, uint32_t best_i, uint32_t sg) {
+  auto emit = [&](uint32_t q, double best, uint32_t best_i, uint32_t sg, bool cert) {
     int32_t pair;
-    const bool ins = match_result(a, M, planar, q, best, best_i, sg, inv_poses, m_pair, m_d2, m_pi, m_ni, m_ins, pair);
+    const bool ins =
+        match_result(a, M, planar, q, best, best_i, sg, inv_poses, m_pair, m_d2, m_pi, m_ni, m_ins, pair, cert);
     if (ins) atomicAdd(&s_ins, 1u);
     if (pair >= 0) atomicAdd(&s_hist[pair], 1u);
   };
@@ -1745,10 +1754,18 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
 #endif
     w4[0] = make_uint4(tp, tc, mq, d0);
     w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), d1, d2);
+    if (a.prof_work) {  // this launch's totals (byte model), drained with the ticket's vmcnt(0)
+      __hip_atomic_fetch_add(a.prof_acc, tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(a.prof_acc + 1, tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 
   if constexpr (!FUSED) {
-    if (qi < nq && g == 0) emit(qi, best, best_i, best_sg);
+#if FMX_WARM_CERT
+    if (qi < nq && g == 0) emit(qi, best, best_i, best_sg, cert_q);
+#else
+    if (qi < nq && g == 0) emit(qi, best, best_i, best_sg, false);
+#endif
   } else {
     static_assert(kGroup == 1, "the fused match + linearization runs one lane per query");
     // this lane's accepted match in its map scan's frame, then its row(s)
@@ -1852,6 +1869,10 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
       if (tid == 27) host_store(fz.out + 28, 0.5 * tot);  // error = 0.5 ||r / sigma||^2
     }
     if (tid == 0) {
+      if (a.prof_work) {  // the launch's probes / candidates -> its profiler slot
+        host_store(a.prof_work, __hip_atomic_exchange(a.prof_acc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        host_store(a.prof_work + 1, __hip_atomic_exchange(a.prof_acc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
       __hip_atomic_store(fz.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (fz.flag) publish_flag(fz.flag, fz.seq);  // fz.out was stored by this wave (threads 0..27)
     }
@@ -1860,6 +1881,12 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   __syncthreads();  // every emit's LDS counts are in
   if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
     __hip_atomic_store(ins_blk + blockIdx.x, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if FMX_CERT_ANY
+  if (threadIdx.x == 0 && a.cert_cnt) {  // the launch's certified / warm totals (a warm launch only)
+    if (s_cert[0]) __hip_atomic_fetch_add(a.cert_cnt, s_cert[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s_cert[2]) __hip_atomic_fetch_add(a.cert_cnt + 1, s_cert[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
   const int t = planar ? 0 : 1;
   if (a.sorted && a.tiles) {
     // per-(type, pair, tile) counts: agent-scope adds, scanned by the last block
@@ -1893,6 +1920,21 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     s_last = __hip_atomic_fetch_add(mticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
+  if (threadIdx.x == 0) {  // certified / warm queries of this launch -> host, counters zeroed
+    uint32_t nc = 0, nw = 0;
+    if (a.cert_cnt) {
+      nc = __hip_atomic_exchange(a.cert_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nw = __hip_atomic_exchange(a.cert_cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    host_store(host_counts + 2 * a.K + 2, nc);
+    host_store(host_counts + 2 * a.K + 3, nw);
+    if (a.prof_work) {  // the launch's probes / candidates / certified / warm -> its profiler slot
+      host_store(a.prof_work, __hip_atomic_exchange(a.prof_acc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      host_store(a.prof_work + 1, __hip_atomic_exchange(a.prof_acc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      host_store(a.prof_work + 2, nc);
+      host_store(a.prof_work + 3, nw);
+    }
+  }
   match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2129,7 +2171,7 @@ __global__ __launch_bounds__(kQPB) void k_insert(InsArgs a) {
   const bool planar = b < a.nb_pl;
   const uint32_t qi = (planar ? b : b - a.nb_pl) * kQPB + threadIdx.x;
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
-  const bool f = qi < nq && a.ins[planar ? qi : a.nq_pl + qi] != 0;
+  const bool f = qi < nq && (a.ins[planar ? qi : a.nq_pl + qi] & 1) != 0;
   const uint64_t m = __ballot(f);
   // a match block of several waves (large-set build): earlier waves' counts first
   constexpr int kW = (kQPB + kWave - 1) / kWave;
@@ -2423,6 +2465,8 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->work_blocks = nb;
   ensure_zeroed(c->mcnt, 2 * (size_t)K, st);
   ensure_zeroed(c->mticket, 1, st);
+  ensure_zeroed(c->mcert, 2, st);
+  a.cert_cnt = c->mcert.p;
   c->ins_blk.ensure(nb + 1);
   c->ins_off.ensure(nb + 1);
   ensure_zeroed(c->thist, (size_t)K * (a.ntl_pl + a.ntl_pt) + 1, st);
@@ -2435,14 +2479,17 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
                    M.pos.p, M.nrm_p, M.epoch, M.rsh};
   };
   // Algorithmic bytes of a match launch: query read (16 B) +
-  // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + one 64-B line per
-  // hash probe (a brick; a dense cell's 256-B header counts as 4 probes) + 32 B per
-  // candidate record tested (double4: position + build order/segment), using the
-  // probe/candidate counts of the previous launch (counted by the kernel), + the warm
-  // state: NN record index and own-cell entry written (4 + 16 B), and on a warm launch
-  // also read, with the warm record itself (4 + 16 + 32 B).
-  const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + 64.0 * c->last_probes + 32.0 * c->last_cands +
-                       (a.rec ? 20.0 * nq : 0.0) + (a.warm ? 52.0 * nq : 0.0);
+  // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + the warm state: NN
+  // record index and own-cell entry written (4 + 16 B), and on a warm launch also read,
+  // with the warm record itself (4 + 16 + 32 B); + one 64-B line per hash probe (a brick;
+  // a dense cell's 256-B header counts as 4 probes) + 32 B per candidate record tested
+  // (double4: position + build order/segment) — those two from the counts THIS launch
+  // publishes to its profiler slot (prof_collect adds them)
+  const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + (a.rec ? 20.0 * nq : 0.0) + (a.warm ? 52.0 * nq : 0.0);
+  const int pslot = nb > 0 ? prof_ring_slot(c) : -1;
+  ensure_zeroed(c->mprof, 2, st);
+  a.prof_acc = c->mprof.p;
+  a.prof_work = pslot >= 0 ? c->prof.wring.d + 4 * (size_t)pslot : nullptr;
   // the sub-cell walk only when the map may hold dense cells: the build's pinned info
   // word (written by k_map_dense) says "none" for this very build (same epoch)
   bool dense = c->map.n[0] + c->map.n[1] > 0;
@@ -2452,6 +2499,9 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   }
   if (nb > 0) {
     ProfScope ps(c->prof, PROF_MATCH, bytes, st);
+    ps.ring = pslot;
+    ps.warm = a.warm ? 1 : 0;
+    ps.queries = nq;
     {
       auto kern = dense ? k_match<true> : k_match<false>;
       hipLaunchKernelGGL(kern, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a,
@@ -2462,7 +2512,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     }
   }
   // no queries: no launch, so zero the counts and insert totals the kernel would write
-  if (nb == 0) FMX_HIP(hipMemsetAsync(c->h_counts.d, 0, (2 * (size_t)c->K + 2) * sizeof(uint32_t), st));
+  if (nb == 0) FMX_HIP(hipMemsetAsync(c->h_counts.d, 0, (2 * (size_t)c->K + 4) * sizeof(uint32_t), st));
   c->match_nb_pl = a.nb_pl;
   c->match_nb = nb;
   c->n_qo = nq;  // query-order rows (k_linearize_total) in both modes
@@ -2531,6 +2581,7 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
 #if FMX_CERT_ANY
   a.cert_b2 = nullptr;
 #endif
+  a.cert_cnt = nullptr;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
@@ -2565,11 +2616,18 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   const FusedArgs fz{c->map_poses_p, 1.0 / sigma, c->bpart.p, c->bpart.p + (size_t)nb * kFzLd, c->fz_tickets.p,
                      c->ticket.p, dst, flag, seq};
   const SortOut so{};
-  // bytes: query read (16 B) + 64 B per probe + 32 B per candidate + the accepted
-  // match's normal (32 B, planar) + 32 * 8 B block partials
+  // bytes: query read (16 B) + the accepted match's normal (32 B, planar) + 32 * 8 B
+  // block partials + 64 B per probe and 32 B per candidate (this launch's own counts,
+  // added by prof_collect from its profiler slot)
   const double nq = (double)c->n_qpl + c->n_qpt;
-  const double bytes = 16.0 * nq + 32.0 * c->n_qpl + 64.0 * c->last_probes + 32.0 * c->last_cands + 256.0 * nb;
+  const double bytes = 16.0 * nq + 32.0 * c->n_qpl + 256.0 * nb;
+  const int pslot = prof_ring_slot(c);
+  ensure_zeroed(c->mprof, 2, st);
+  a.prof_acc = c->mprof.p;
+  a.prof_work = pslot >= 0 ? c->prof.wring.d + 4 * (size_t)pslot : nullptr;
   ProfScope ps(c->prof, PROF_MATCH_LIN, bytes, st);
+  ps.ring = pslot;
+  ps.queries = nq;
 #if FMX_MATCH_GROUP == 1
   {
     auto kern = dense ? k_match<true, true> : k_match<false, true>;
@@ -2617,6 +2675,8 @@ void match_counts_fetch(fmx_ctx* c, bool wait) {
   c->cnt_pt.assign(c->h_counts.p + c->K, c->h_counts.p + 2 * c->K);
   c->ins_tot[0] = c->h_counts.p[2 * c->K];
   c->ins_tot[1] = c->h_counts.p[2 * c->K + 1];
+  c->cert_tot[0] = c->h_counts.p[2 * c->K + 2];
+  c->cert_tot[1] = c->h_counts.p[2 * c->K + 3];
   c->rows_pl = c->rows_pt = 0;
   for (uint32_t k = 0; k < c->K; ++k) {
     c->rows_pl += c->cnt_pl[k];

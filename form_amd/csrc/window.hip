@@ -301,6 +301,224 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
   WSTAMP(6);
 }
 
+// ---------------------------------------------------------------- pair moments
+// The ICP loop's LM relinearizes the current scan's pairs at every trial (fast mode,
+// constraints.cpp:257-266) and the final LM every stored pair (:294-305).  Each row's
+// whitened a = [H_i H_j -r] / sigma is LINEAR in 16 per-row features taken once at
+// reference poses (T_i0, T_j0), with coefficients that depend only on the pair's poses:
+//   plane rows (factor.cpp:37-77), q0 = R_i0^T (R_j0 p_j + t_j0 - t_i0) (p_j in frame i):
+//     phi = [ r0 = n.(q0 - p_i), n x q0 (3), n (3), n_b p_j,d (9) ]
+//     since H_i = [n x q, -n], H_j = [p_j x M^T n, M^T n], r = n.(q - p_i) with
+//     q = M p_j + v, M = R_i^T R_j, v = R_i^T (t_j - t_i) = q0 + dM p_j + dv;
+//   point rows (factor.cpp:87-124), e0 = (R_j0 p_j + t_j0) - (R_i0 p_i + t_i0):
+//     phi = [ e0 (3), p_i (3), p_j (3), 1, 0 x 6 ] (the three axes share it).
+// So a pair's DenseFactor::linearize (gtsam.hpp:67-86) at ANY poses is C Phi C^T with
+// Phi = sum_rows phi phi^T (16 x 16) — contracted on the host (moments.cpp) without a
+// device round trip.  The residual enters through r0 / e0 (taken per row), not as a
+// difference of large moments, so the contraction keeps full precision.
+// k_win_moments: the same launch geometry as k_win_linearize (one block per <= 256-row
+// chunk of one pair, fp64 MFMA sums, per-pair ticket + ordered finisher); out: per pair
+// Phi_plane then Phi_point, packed upper 16 x 16 (136 each), to pinned host memory.
+constexpr int kMomF = 16;                // features per row
+constexpr int kMomP = 136;               // packed upper 16 x 16
+constexpr int kMomLd = 144;              // doubles per chunk partial (136 used)
+constexpr int kMomStride = 17;           // doubles per staged row (odd: no LDS bank conflicts)
+
+__device__ __forceinline__ void stage_and_mfma16(double* __restrict__ rows, const double (&f)[kMomF], bool valid,
+                                                 f64x4 (&acc)[4]) {
+  const int lane = lane_id();
+  double* mine = rows + lane * kMomStride;
+#pragma unroll
+  for (int i = 0; i < kMomF; ++i) mine[i] = valid ? f[i] : 0.0;
+  __builtin_amdgcn_wave_barrier();
+  const double* src = rows + (lane >> 4) * kMomStride + (lane & 15);
+  double v[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) v[t] = src[4 * t * kMomStride];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[t], v[t], acc[t & 3], 0, 0, 0);
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int NP>
+__global__ __launch_bounds__(kWinWaves * kWave) void k_win_moments(WinArgs a, WinPosesN<NP> wp) {
+  __shared__ double s_rows[kWinWaves][kWave * kMomStride];
+  __shared__ double s_g[kWinWaves][2 * kMomP];
+  __shared__ uint32_t s_t;
+  const int w = threadIdx.x / kWave, lane = lane_id(), tid = threadIdx.x;
+  const uint32_t ch = blockIdx.x;
+  const uint32_t nch = a.n_chunks ? *a.n_chunks : a.n_chunks_host;
+  Chunk d{};
+  if (a.n_chunks || ch < a.n_chunks_host) d = a.chunks[ch];
+  if (nch == 0) {
+    if (blockIdx.x == 0 && tid == 0) publish_flag(a.flag, a.seq);
+    return;
+  }
+  if (ch >= nch) return;
+  const uint32_t type = d.type & 0xFFu;
+  const int slot = (int)d.pair;
+  const uint32_t cb = a.chunk_range[slot], ce = a.chunk_range[slot + 1];
+  int pi, pj;
+  if (a.implicit_j >= 0) {
+    pi = slot;
+    pj = a.implicit_j;
+  } else if (a.implicit_j == kPairedPoses) {
+    pi = 2 * slot;
+    pj = 2 * slot + 1;
+  } else {
+    pi = (int)((d.type >> 8) & 0xFFFu);
+    pj = (int)(d.type >> 20);
+  }
+  const double* Ti = a.dposes ? a.dposes + 12 * pi : wp.m[pi];
+  const double* Tj = a.dposes ? a.dposes + 12 * pj : wp.m[pj];
+  f64x4 accs[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) accs[i] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const uint32_t row = d.begin + w * kWave + lane;
+  if (d.begin + w * kWave < d.end) {  // wave-uniform
+    const bool valid = row < d.end;
+    double f[kMomF];
+#pragma unroll
+    for (int i = 0; i < kMomF; ++i) f[i] = 0.0;
+    if (valid) {
+      if (type == 0) {
+        double c[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) c[q] = a.c_pl[row + q * a.ld_pl];
+        double wj[3], q0[3];
+        d_xform(Tj, c[6], c[7], c[8], wj);
+        d_rotT(Ti, wj[0] - Ti[3], wj[1] - Ti[7], wj[2] - Ti[11], q0);
+        const double n0 = c[3], n1 = c[4], n2 = c[5];
+        f[0] = (n0 * (q0[0] - c[0]) + n1 * (q0[1] - c[1])) + n2 * (q0[2] - c[2]);
+        f[1] = n1 * q0[2] - n2 * q0[1];
+        f[2] = n2 * q0[0] - n0 * q0[2];
+        f[3] = n0 * q0[1] - n1 * q0[0];
+        f[4] = n0;
+        f[5] = n1;
+        f[6] = n2;
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+#pragma unroll
+          for (int e = 0; e < 3; ++e) f[7 + 3 * b + e] = c[3 + b] * c[6 + e];
+      } else {
+        double c[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) c[q] = a.c_pt[row + q * a.ld_pt];
+        double wi[3], wj[3];
+        d_xform(Ti, c[0], c[1], c[2], wi);
+        d_xform(Tj, c[3], c[4], c[5], wj);
+        f[0] = wj[0] - wi[0];
+        f[1] = wj[1] - wi[1];
+        f[2] = wj[2] - wi[2];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) f[3 + q] = c[q];
+        f[9] = 1.0;
+      }
+    }
+    stage_and_mfma16(s_rows[w], f, valid, accs);
+  }
+  // wave sums (packed upper 16 x 16) -> LDS; block sum in wave order
+  const f64x4 acc = (accs[0] + accs[1]) + (accs[2] + accs[3]);
+  {
+    const int col = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = (lane >> 4) + 4 * r;
+      if (rr <= col) s_g[w][rr * 16 - rr * (rr - 1) / 2 + (col - rr)] = acc[r];
+    }
+  }
+  __syncthreads();
+  double bsum = 0.0;
+  if (tid < kMomP) {
+    bsum = s_g[0][tid];
+#pragma unroll
+    for (int i = 1; i < kWinWaves; ++i) bsum += s_g[i][tid];
+  }
+  // this pair's sums by type (entry tid < 136): plane rows, point pairs
+  double out_pl = 0.0, out_pt = 0.0;
+  if (ce - cb > 1) {
+    if (tid < kMomP) agent_store(a.partials + (size_t)ch * kMomLd + tid, bsum);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_t = __hip_atomic_fetch_add(a.pair_ticket + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_t != ce - cb - 1) return;
+    // the pair's last chunk sums the partials by type, in chunk order: wave w takes
+    // chunks cb + w, cb + w + W, ...; lane holds entries lane, lane + 64, lane + 128
+    // (< 136) of each type; the wave sums meet in LDS in wave order
+    {
+      double sp[3] = {0.0, 0.0, 0.0}, st[3] = {0.0, 0.0, 0.0};
+      for (uint32_t c0 = cb + w; c0 < ce; c0 += kFinBatch * kWinWaves) {
+        double x[kFinBatch][3];
+        uint32_t ty[kFinBatch];
+#pragma unroll
+        for (int u = 0; u < kFinBatch; ++u) {
+          const uint32_t cc = c0 + u * kWinWaves;
+          const double* src = a.partials + (size_t)cc * kMomLd;
+          ty[u] = cc < ce ? (a.chunks[cc].type & 0xFFu) : 2u;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const int e = lane + 64 * k;
+            x[u][k] = cc < ce && e < kMomP ? agent_load(src + e) : 0.0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kFinBatch; ++u)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            sp[k] += ty[u] == 0u ? x[u][k] : 0.0;
+            st[k] += ty[u] == 1u ? x[u][k] : 0.0;
+          }
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e = lane + 64 * k;
+        if (e < kMomP) {
+          s_g[w][e] = sp[k];
+          s_g[w][kMomP + e] = st[k];
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < kMomP) {
+      out_pl = s_g[0][tid];
+      out_pt = s_g[0][kMomP + tid];
+#pragma unroll
+      for (int i = 1; i < kWinWaves; ++i) {
+        out_pl += s_g[i][tid];
+        out_pt += s_g[i][kMomP + tid];
+      }
+    }
+    if (tid == 0) __hip_atomic_store(a.pair_ticket + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    out_pl = type == 0 ? bsum : 0.0;
+    out_pt = type == 1 ? bsum : 0.0;
+  }
+  // this pair's Phi (both types) straight to pinned host memory (write-through)
+  double* G = a.hostG + (size_t)slot * (2 * kMomP);
+  if (tid < kMomP) {
+    host_store(G + tid, out_pl);
+    host_store(G + kMomP + tid, out_pt);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (w != 0) return;
+  uint32_t n_ne = 0;
+  for (int k0 = 0; k0 < a.npairs; k0 += kWave) {
+    const int k = k0 + lane;
+    const bool ne = k < a.npairs && a.chunk_range[k + 1] > a.chunk_range[k];
+    n_ne += (uint32_t)__popcll(__ballot(ne));
+  }
+  uint32_t t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(a.done_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, 0, 64);
+  if (t != n_ne - 1) return;
+  if (lane == 0) {  // every finisher's host stores were acknowledged before its ticket (as k_win_linearize)
+    __hip_atomic_store(a.done_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    publish_flag(a.flag, a.seq);
+  }
+}
+
 // Copy n_pl plane rows (9 comps) and n_pt point pairs (6 comps) between SoA buffers.
 __global__ void k_rows_copy(const double* __restrict__ spl, size_t lds_pl, uint64_t so_pl, double* __restrict__ dpl,
                             size_t ldd_pl, uint64_t do_pl, uint32_t n_pl, const double* __restrict__ spt, size_t lds_pt,
@@ -372,8 +590,9 @@ void win_timing_collect(fmx_ctx* c, uint32_t grid_chunks) {
 // out (win_finish).  The host assembles the x-dependent non-pair terms in between.
 // out_dev (sharded fmx_linearize): G to this device buffer instead, the completion word
 // to a device scratch word; the caller all-reduces and copies (no win_finish).
+// mom: k_win_moments instead (per pair 2 x 136 doubles of moments, to W.hM)
 void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double bytes,
-               double* out_dev = nullptr) {
+               double* out_dev = nullptr, bool mom = false) {
   WinStore& W = c->win;
   if (W.pending) win_finish(c, nullptr);  // an abandoned one (error path): drain it first
   hipStream_t st = c->stream;
@@ -393,14 +612,15 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
     a.dposes = W.dposes.p;
   }
   const int np = std::max(a.npairs, 1);
-  W.partials.ensure((size_t)std::max<uint32_t>(grid_chunks, 1) * kWinLd);
+  W.partials.ensure((size_t)std::max<uint32_t>(grid_chunks, 1) * (mom ? kMomLd : kWinLd));
   ensure_zeroed(W.pticket, (size_t)np, st);
   ensure_zeroed(W.dticket, 1, st);
   W.hG.ensure((size_t)np * kWinG);
+  if (mom) W.hM.ensure((size_t)np * 2 * kMomP);
   a.partials = W.partials.p;
   a.pair_ticket = W.pticket.p;
   a.done_ticket = W.dticket.p;
-  a.hostG = W.hG.d;
+  a.hostG = mom ? W.hM.d : W.hG.d;
   a.seq = next_flag(c);
   a.flag = c->h_flag.d;
   if (out_dev) {
@@ -419,16 +639,23 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
   const uint32_t blocks = std::max<uint32_t>(grid_chunks, 1);
   {
     HostScope hs(12);
-    ProfScope ps(c->prof, PROF_WINDOW, bytes, st);
-    if (nposes <= kWinSmallArgPoses)
+    ProfScope ps(c->prof, mom ? PROF_MOMENTS : PROF_WINDOW, bytes, st);
+    if (mom) {
+      if (nposes <= kWinSmallArgPoses)
+        hipLaunchKernelGGL(k_win_moments<kWinSmallArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wps);
+      else
+        hipLaunchKernelGGL(k_win_moments<kWinMaxArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
+    } else if (nposes <= kWinSmallArgPoses) {
       hipLaunchKernelGGL(k_win_linearize<kWinSmallArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wps);
-    else
+    } else {
       hipLaunchKernelGGL(k_win_linearize<kWinMaxArgPoses>, dim3(blocks), dim3(kWinWaves * kWave), 0, st, a, wp);
+    }
     FMX_HIP(hipGetLastError());
   }
   W.pending = out_dev == nullptr;
   W.pending_seq = a.seq;
   W.pending_np = a.npairs;
+  W.pending_mom = mom;
   W.pending_grid = grid_chunks;
 }
 
@@ -442,8 +669,11 @@ void win_finish(fmx_ctx* c, double* G_out) {
     HostScope hs(13);
     wait_flag(c, c->h_flag.p, W.pending_seq);
   }
-  if (G_out) std::memcpy(G_out, W.hG.p, (size_t)W.pending_np * kWinG * sizeof(double));
-  if (win_timing_on()) win_timing_collect(c, W.pending_grid);
+  if (G_out) {
+    if (W.pending_mom) std::memcpy(G_out, W.hM.p, (size_t)W.pending_np * 2 * kMomP * sizeof(double));
+    else std::memcpy(G_out, W.hG.p, (size_t)W.pending_np * kWinG * sizeof(double));
+  }
+  if (win_timing_on() && !W.pending_mom) win_timing_collect(c, W.pending_grid);
 }
 
 namespace {
@@ -647,6 +877,66 @@ void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double
   // exact row counts arrive with the match counts; the byte model uses the last known
   win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K);
   if (G_out) win_finish(c, G_out);
+}
+
+// The moments (k_win_moments) of the current scan's K pairs from the sorted match at the
+// reference poses poses[k] (pose of map_scans[k]) and poses[K] (the current pose): out
+// (null: launch only, win_finish(c, out) later) = K x 272 doubles, per pair the packed
+// upper 16 x 16 plane moments then the point moments.
+void win_moments_current(fmx_ctx* c, const double* poses, double* out) {
+  if (!c->have_corr) throw StatusError(FMX_E_STATE, "win_moments_current: no sorted match");
+  run_pair_scatter(c);
+  WinArgs a{};
+  a.chunks = c->chunks.p;
+  a.n_chunks = c->n_chunks.p;
+  a.chunk_range = c->chunk_range.p;
+  a.npairs = (int)c->K;
+  a.c_pl = c->c_pl.p;
+  a.ld_pl = c->ld_pl;
+  a.c_pt = c->c_pt.p;
+  a.ld_pt = c->ld_pt;
+  a.implicit_j = (int)c->K;
+  a.inv = 1.0;
+  // bytes: rows read (72 B per plane row, 48 B per point pair) + 2 x 136 doubles per pair
+  win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * 2 * kMomP * c->K,
+            nullptr, true);
+  if (out) win_finish(c, out);
+}
+
+// fmx_moments: the same for the context's correspondences (fmx_match / fmx_corr_set),
+// pair k at the reference poses poses_i[k], poses_j[k] (the GTSAM seam's "linearize once,
+// evaluate anywhere" form; fmx_moments_contract).  out: K x 272.
+void win_moments_pairs(fmx_ctx* c, const double* poses_i, const double* poses_j, double* out) {
+  if (!c->have_corr) throw StatusError(FMX_E_STATE, "no correspondences (call fmx_match or fmx_corr_set)");
+  run_pair_scatter(c);
+  const int K = (int)c->K;
+  if (K == 0) return;
+  if (c->comm) throw StatusError(FMX_E_STATE, "fmx_moments is not sharded (no communicator)");
+  if (2 * (size_t)K > 0xFFFFFFu) throw StatusError(FMX_E_INVAL, "too many pairs");
+  WinStore& W = c->win;
+  if (W.pending) win_finish(c, nullptr);
+  std::vector<double> table(24 * (size_t)K);
+  for (int k = 0; k < K; ++k) {
+    std::memcpy(&table[24 * (size_t)k], poses_i + 12 * (size_t)k, 12 * sizeof(double));
+    std::memcpy(&table[24 * (size_t)k + 12], poses_j + 12 * (size_t)k, 12 * sizeof(double));
+  }
+  if (c->counts_pending) match_counts_fetch(c);
+  W.hM.ensure((size_t)K * 2 * kMomP);
+  std::memset(W.hM.p, 0, (size_t)K * 2 * kMomP * sizeof(double));  // pairs without rows are never written
+  WinArgs a{};
+  a.chunks = c->chunks.p;
+  a.n_chunks = c->n_chunks.p;
+  a.chunk_range = c->chunk_range.p;
+  a.npairs = K;
+  a.c_pl = c->c_pl.p;
+  a.ld_pl = c->ld_pl;
+  a.c_pt = c->c_pt.p;
+  a.ld_pt = c->ld_pt;
+  a.implicit_j = kPairedPoses;
+  a.inv = 1.0;
+  win_start(c, a, c->max_chunks, table.data(), 2 * K, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * 2 * kMomP * K,
+            nullptr, true);
+  win_finish(c, out);
 }
 
 // fmx_linearize / fmx_error — the GTSAM seam, DenseFactor::linearize of every pair's

@@ -82,7 +82,8 @@ EXPORTED = [
     "fmx_current_pose",
     "fmx_last_stats", "fmx_match_work", "fmx_profile_enable", "fmx_profile_reset", "fmx_profile_count",
     "fmx_profile_name", "fmx_profile_read", "fmx_sync", "fmx_comm_unique_id", "fmx_comm_init",
-    "fmx_map_download", "fmx_register_points", "fmx_scan_buffer",
+    "fmx_map_download", "fmx_register_points", "fmx_scan_buffer", "fmx_match_cert", "fmx_profile_match_work",
+    "fmx_corr_generation", "fmx_moments", "fmx_moments_contract",
 ]
 
 
@@ -349,7 +350,11 @@ class Context:
         n = n or e.num_rows * e.num_columns
         p = C.c_void_p()
         self._chk(self._L.fmx_scan_buffer(self.h, C.c_size_t(n), C.byref(p)))
-        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n, 4))
+        a = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n, 4))
+        # the memory belongs to the context: the array keeps the Context alive (a view
+        # whose base holds it).  It is invalid after close() and after a later
+        # scan_buffer call that asks for more points than this buffer holds.
+        return np.asarray(_CtxBuffer(a, self))
 
     def next_scan(self, scan):
         """fmx_next_scan: announce the scan that follows the one the next register_scan
@@ -404,6 +409,42 @@ class Context:
         return dict(queries=float(w[0]), probes=float(w[1]), candidates=float(w[2]))
 
     # ---------------------------------------------------------------- profiling
+    def moments(self, ref_i, ref_j) -> np.ndarray:
+        """fmx_moments: the (K, 272) pair moments of the context's correspondences at
+        reference poses ref_i[k], ref_j[k] (K x 3 x 4); evaluate them at any poses with
+        moments_contract (no device round trip)."""
+        ri = np.ascontiguousarray(ref_i, np.float64).reshape(-1, 12)
+        rj = np.ascontiguousarray(ref_j, np.float64).reshape(-1, 12)
+        out = np.zeros((max(self.K, 1), 272))
+        self._chk(self._L.fmx_moments(self.h, _p(ri), _p(rj), _p(out)))
+        return out[:self.K]
+
+    def match_cert(self, per_query: bool = False):
+        """fmx_match_cert: the warm certificate of the last match — (certified, warm)
+        query counts, and with per_query a uint8 array (planar then point queries, 1 =
+        settled by the certificate without a search)."""
+        cnt = np.zeros(2, np.uint64)
+        flags = np.zeros(self.n_planar + self.n_point if per_query else 0, np.uint8)
+        self._chk(self._L.fmx_match_cert(self.h, _p(cnt), _p(flags) if per_query else None))
+        out = dict(certified=int(cnt[0]), warm=int(cnt[1]))
+        if per_query:
+            out["flags"] = flags
+        return out
+
+    def profile_match_work(self) -> dict:
+        """fmx_profile_match_work: the profiled match launches' work since the last
+        reset, split into cold (first match on a map / query set) and warm launches."""
+        w = np.zeros(12)
+        self._chk(self._L.fmx_profile_match_work(self.h, _p(w)))
+        return {k: dict(launches=w[6 * i], queries=w[6 * i + 1], probes=w[6 * i + 2], candidates=w[6 * i + 3],
+                        certified=w[6 * i + 4], warm=w[6 * i + 5])
+                for i, k in enumerate(("cold", "warm"))}
+
+    def corr_generation(self) -> int:
+        g = C.c_uint64()
+        self._chk(self._L.fmx_corr_generation(self.h, C.byref(g)))
+        return int(g.value)
+
     def profile(self, on: bool = True):
         self._chk(self._L.fmx_profile_enable(self.h, C.c_int(int(on))))
 
@@ -423,6 +464,15 @@ class Context:
         self._chk(self._L.fmx_sync(self.h))
 
 
+class _CtxBuffer:
+    """Buffer protocol over a context-owned pinned array that also holds the context."""
+
+    def __init__(self, arr, ctx):
+        self._arr = arr
+        self._ctx = ctx
+        self.__array_interface__ = arr.__array_interface__
+
+
 def _scan_ptr(scan):
     """(on_device, pointer, n_points, keepalive) for a numpy array or torch tensor."""
     try:
@@ -438,6 +488,21 @@ def _scan_ptr(scan):
     if a.ndim != 2 or a.shape[1] != 4:
         raise ValueError("scan must be (N, 4) float32 (PointXYZf layout)")
     return 0, _p(a), a.shape[0], a
+
+
+def moments_contract(mom, ref_i, ref_j, poses_i, poses_j, sigma: float):
+    """fmx_moments_contract (host only): packed 13 x 13 G (K, 91) and errors (K,) of K
+    pairs at poses (poses_i[k], poses_j[k]) from their moments taken at (ref_i, ref_j)."""
+    m = np.ascontiguousarray(mom, np.float64).reshape(-1, 272)
+    K = m.shape[0]
+    a = [np.ascontiguousarray(x, np.float64).reshape(K, 12) for x in (ref_i, ref_j, poses_i, poses_j)]
+    G = np.zeros((max(K, 1), 91))
+    err = np.zeros(max(K, 1))
+    st = lib().fmx_moments_contract(C.c_uint32(K), _p(m), _p(a[0]), _p(a[1]), _p(a[2]), _p(a[3]),
+                                    C.c_double(sigma), _p(G), _p(err))
+    if st != FMX_OK:
+        raise FmxError(st, "fmx_moments_contract failed")
+    return G[:K], err[:K]
 
 
 def comm_unique_id() -> bytes:

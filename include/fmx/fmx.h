@@ -112,7 +112,9 @@ fmx_status fmx_extract(fmx_ctx* ctx, const float* xyzw, size_t n_points, uint64_
  * directly: passed as a host scan (src_on_device = 0) it is DMA'd with no staging copy.
  * Three buffers are handed out in turn: the one returned here is returned again by the
  * third next call, so a caller may fill scan k+1 while scan k registers.  Valid until
- * fmx_destroy. */
+ * fmx_destroy, or until a later call asks for more points than that buffer holds: the
+ * buffer is then reallocated (after draining every queued DMA from it), and an
+ * announcement of a scan in the old buffer is withdrawn. */
 fmx_status fmx_scan_buffer(fmx_ctx* ctx, size_t n_points, float** out);
 /* Copy the last extraction to host (any pointer may be NULL):
  * planar[6*planar], planar_index[planar] (scan point index), point[3*point],
@@ -182,11 +184,31 @@ fmx_status fmx_map_insert(fmx_ctx* ctx, double min_dist_map, uint32_t* n_inserte
 fmx_status fmx_corr_set(fmx_ctx* ctx, uint32_t K, const uint32_t* n_plane,
                         const double* plane_pi, const double* plane_ni, const double* plane_pj,
                         const uint32_t* n_point, const double* point_pi, const double* point_pj);
+/* A counter that changes whenever the context's correspondences may have been replaced
+ * (fmx_match, fmx_corr_set, fmx_register_scan): a caller caching fmx_linearize results per
+ * set of poses (fmx_seam.hpp's FmxBatch) keys its cache on it as well. */
+fmx_status fmx_corr_generation(fmx_ctx* ctx, uint64_t* gen);
 /* DenseFactor::linearize of every pair's FeatureFactor (gtsam.hpp:67-86,
  * factor.cpp:142-186): poses_i / poses_j are K x 12.  G: K x 91 (single_pose=0)
  * or K x 28 (single_pose=1); err: K x 1 = 0.5*||r/sigma||^2 (may be NULL). */
 fmx_status fmx_linearize(fmx_ctx* ctx, const double* poses_i34, const double* poses_j34,
                          double sigma, int single_pose, double* G, double* err);
+/* Pair moments: DenseFactor::linearize "once, evaluated anywhere".  Every row's whitened
+ * [H_i H_j -r] is linear in 16 per-row features taken at reference poses (plane rows:
+ * r0 = n.(q0 - p_i), n x q0, n, n (x) p_j with q0 = p_j in frame i; point rows: the world
+ * residual e0, p_i, p_j, 1), so a pair's 13 x 13 information at ANY poses is C Phi C^T
+ * with Phi = sum over its rows of phi phi^T.  fmx_moments: Phi of every pair of the
+ * context's correspondences (fmx_match / fmx_corr_set) at reference poses
+ * poses_i[k], poses_j[k] (K x 12 each), on the device (one launch).  mom: K x 272 =
+ * per pair the packed upper 16 x 16 of the plane rows, then of the point rows. */
+fmx_status fmx_moments(fmx_ctx* ctx, const double* ref_i34, const double* ref_j34, double* mom);
+/* Host only (no context, no device): the packed 13 x 13 G (K x 91, may be NULL) and
+ * errors 0.5 ||r/sigma||^2 (K, may be NULL) of K pairs at poses (poses_i[k],
+ * poses_j[k]) from their moments mom (K x 272) taken at (ref_i[k], ref_j[k]) — equal to
+ * fmx_linearize at the same poses up to rounding (gtsam.hpp:67-86, factor.cpp:30-128). */
+fmx_status fmx_moments_contract(uint32_t K, const double* mom, const double* ref_i34, const double* ref_j34,
+                                const double* poses_i34, const double* poses_j34, double sigma, double* G,
+                                double* err);
 /* NoiseModelFactor::error of every pair (FeatureFactor::evaluateError without
  * Jacobians), err: K x 1. */
 fmx_status fmx_error(fmx_ctx* ctx, const double* poses_i34, const double* poses_j34,
@@ -245,7 +267,9 @@ fmx_status fmx_register_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, i
  * DMA'd and extracted on the side stream as soon as that copy has finished); it must
  * stay unchanged until its own fmx_register_scan returns.  That call must pass the
  * same pointer with the same src_on_device, else the queued extraction is discarded
- * and the scan extracted in the call.  xyzw = NULL withdraws the announcement. */
+ * and the scan extracted in the call.  xyzw = NULL withdraws the announcement.  A
+ * withdrawing or replacing call returns only once the staging copy of a withdrawn or
+ * replaced pageable scan has finished: from then on its memory is no longer read. */
 fmx_status fmx_next_scan(fmx_ctx* ctx, const float* xyzw, size_t n_points, int src_on_device);
 /* Estimator::current_lidar_estimate (form/form.hpp:79). */
 fmx_status fmx_current_pose(fmx_ctx* ctx, double pose34[12]);
@@ -276,6 +300,14 @@ fmx_status fmx_last_stats(fmx_ctx* ctx, uint64_t* stats, int n);
 /* Work of the last fmx_match (counted by the kernel, available while profiling is
  * enabled): queries, hash probes, candidate records distance-tested. */
 fmx_status fmx_match_work(fmx_ctx* ctx, double work[3]);
+/* The warm certificate of the last fmx_match (no profiling needed).  A match on the same
+ * map and query set as the previous one starts warm; a warm query whose previous nearest
+ * record provably stays nearest after the pose step (it kept its cell, and every other
+ * record was farther than that record by more than twice the step) skips the search —
+ * the result is identical to a search (VoxelMap::find_closest, map.tpp:70-91).
+ * counts[0] = certified queries, counts[1] = warm queries (either may be 0);
+ * certified (may be NULL): per query (planar then point) 1 if it was certified. */
+fmx_status fmx_match_cert(fmx_ctx* ctx, uint64_t counts[2], uint8_t* certified);
 
 /* ---------------- profiling (bench.py roofline) ----------------------------
  * When enabled, each kernel launch is bracketed by HIP events on the context
@@ -286,6 +318,10 @@ fmx_status fmx_profile_reset(fmx_ctx* ctx);
 int fmx_profile_count(void);
 const char* fmx_profile_name(int k);
 fmx_status fmx_profile_read(fmx_ctx* ctx, double* ms, uint64_t* launches, double* bytes, int n);
+/* Match work of the profiled match launches since the last reset, cold (the first match
+ * on a map / query set) then warm: {launches, queries, probes, candidates, certified
+ * queries, warm queries} each (fmx_match_cert's counts, summed). */
+fmx_status fmx_profile_match_work(fmx_ctx* ctx, double out[12]);
 
 /* Wait for all of the context's device work (its stream and the side streams of the
  * map build and the pipelined extraction). */

@@ -17,7 +17,9 @@
 //   * FmxBatch: one fmx_linearize for ALL pairs of a graph per set of poses.  GTSAM
 //     linearizes every factor of a NonlinearFactorGraph against the same Values, so
 //     the first factor's linearize() launches the batch and the others read its cached
-//     result; the cache key is the exact bits of the K pose pairs.
+//     result; the cache key is the exact bits of the K pose pairs plus the context's
+//     correspondence generation (fmx_corr_generation: a re-match or fmx_corr_set at
+//     unchanged poses is a new system).
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -104,13 +106,16 @@ class FmxBatch {
       pose_of(ki_[k], &pi_[12 * k]);
       pose_of(kj_[k], &pj_[12 * k]);
     }
-    if (valid_ && pi_ == ci_ && pj_ == cj_) return G_.data();  // doubles compared exactly
+    uint64_t gen = 0;
+    if (fmx_corr_generation(ctx_, &gen) != FMX_OK) throw std::runtime_error("fmx_corr_generation failed");
+    if (valid_ && gen == gen_ && pi_ == ci_ && pj_ == cj_) return G_.data();  // doubles compared exactly
     G_.assign((K ? K : 1) * (size_t)stride(), 0.0);
     err_.assign(K ? K : 1, 0.0);
     const fmx_status st = fmx_linearize(ctx_, pi_.data(), pj_.data(), sigma_, single_ ? 1 : 0, G_.data(), err_.data());
     if (st != FMX_OK) throw std::runtime_error(std::string("fmx_linearize: ") + fmx_last_error(ctx_));
     ci_ = pi_;
     cj_ = pj_;
+    gen_ = gen;
     valid_ = true;
     ++launches_;
     return G_.data();
@@ -130,6 +135,7 @@ class FmxBatch {
   std::vector<uint64_t> ki_, kj_;
   std::vector<double> pi_, pj_, ci_, cj_, G_, err_;
   bool valid_ = false;
+  uint64_t gen_ = 0;
   uint64_t launches_ = 0;
 };
 

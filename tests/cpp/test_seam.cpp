@@ -120,6 +120,12 @@ int main() {
     batch.linearize_all(pose_of);
     batch.linearize_all(pose_of);  // same Values: served from the cache
     check(batch.launches() == 1, "cache hit", 0, (double)batch.launches(), 1.0);
+    // the correspondences replaced (here: set again) at unchanged poses: a new
+    // generation (fmx_corr_generation), so the batch relaunches instead of serving the cache
+    if (fmx_corr_set(ctx, K, np.data(), ppi.data(), pni.data(), ppj.data(), nt.data(), tpi.data(), tpj.data()) != FMX_OK)
+      return 1;
+    batch.linearize_all(pose_of);
+    check(batch.launches() == 2, "relaunch on new correspondences", 0, (double)batch.launches(), 2.0);
     // the oracle's packed G and errors at the same poses
     std::vector<double> Pi(12 * K), Pj(12 * K);
     for (uint32_t k = 0; k < K; ++k) {
@@ -181,7 +187,7 @@ int main() {
     const double before = batch.error(0);
     pose[100][3] += 0.01;
     batch.linearize_all(pose_of);
-    check(batch.launches() == 2, "relaunch on new poses", 0, (double)batch.launches(), 2.0);
+    check(batch.launches() == 3, "relaunch on new poses", 0, (double)batch.launches(), 3.0);
     check(batch.error(0) != before, "new poses change the error", 0, batch.error(0), before);
     pose[100][3] -= 0.01;
   }

@@ -213,14 +213,28 @@ def test_warm_matches_c4_icp_sequence(fmx_mod, oracle):
     ctx.set_queries(q["planar"], q["point"], 5)
     rng = np.random.default_rng(23)
     T = perturb(q["pose"], rng, 0.01, 0.1)
-    scale = 1.0
+    log = []
     for it in range(8):
+        # ICP-like: each pose is the previous one moved by a step 4x smaller than the last
+        # (~0.5 mrad / 5 mm first, down to ~0.03 urad / 0.3 um), as an ICP loop converging
+        # on the 1e-4 break (form.cpp:83-88) moves X(j)
+        if it > 0:
+            T = perturb(T, rng, 0.002 * 0.25 ** it, 0.02 * 0.25 ** it)
         _warm_check(ctx, built, q, T, w)
-        scale *= 0.25
-        T = perturb(q["pose"], rng, 0.01 * scale, 0.1 * scale)
+        cc = ctx.match_cert()  # the warm certificate fired (and every match above is bit-exact)
+        log.append((it, cc["certified"], cc["warm"]))
+        if it == 0:
+            assert cc["warm"] == 0 and cc["certified"] == 0
+        else:  # (queries whose last match found no record have no warm record)
+            assert 0.9 * (len(q["planar"]) + len(q["point"])) < cc["warm"] <= len(q["planar"]) + len(q["point"])
+        if it >= 3:  # steps <= ~30 urad / 0.3 mm: VERDICT r4's bar, certified / warm >= 0.8
+            assert cc["certified"] >= 0.8 * cc["warm"], log
+    print("C4 ICP sequence, warm certificate (iteration, certified, warm):", log)
     built = _warm_build(ctx, oracle, feats, [0, 2, 3, 4], w)
-    for rot, trans in [(0.002, 0.02), (0.0005, 0.005)]:
+    for k, (rot, trans) in enumerate([(0.002, 0.02), (0.0005, 0.005)]):
         _warm_check(ctx, built, q, perturb(q["pose"], rng, rot, trans), w)
+        cc = ctx.match_cert()
+        assert (cc["warm"] == 0) == (k == 0) and (k > 0 or cc["certified"] == 0), cc
 
 
 def test_match_large_query_set_matches_oracle(fmx_mod, oracle):
@@ -413,3 +427,97 @@ def test_match_sort_then_linearize(fmx_mod, oracle, K):
     scale = np.abs(Gr).max(axis=1, keepdims=True) + 1e-300
     assert np.all(np.abs(G - Gr) <= 1e-10 * scale)
     assert np.allclose(err, er, rtol=1e-10, atol=0)
+
+
+def _cert_fixture():
+    """Planar map records (scan 0, identity pose) and planar queries (local frame) in
+    isolated 0.8 m cells (x cell index 10 g), for a pose step of +DELTA along x:
+      pos   — NN at 0.05, competitor at 0.35: margin >> 2 DELTA, must certify;
+      tie   — NN at 0.10 (+x side), competitor at 0.115 (-x side): the step moves away
+              from the competitor, the NN is unchanged, but the margin 0.015 < 2 DELTA:
+              must refuse;
+      flip  — NN at 0.10 (-x side), competitor at 0.115 (+x side): the step keeps the
+              own cell and moves toward the competitor, which becomes the NN: must refuse;
+      face  — the query 5 mm below a cell face, NN 0.05 away inside the cell, the next
+              record 0.6 away: the step crosses the face (other 27 cells): must refuse."""
+    w, c = 0.8, 0.4
+    recs, qs, kind = [], [], []
+    nrm = (0.0, 0.0, 1.0)
+
+    def cell(g):
+        return np.array([0.8 * 10 * g, 0.0, 0.0])
+
+    g = 0
+    for k, n in (("pos", 48), ("tie", 4), ("flip", 4), ("face", 4)):
+        for _ in range(n):
+            o = cell(g)
+            if k == "face":
+                q = o + np.array([w - 0.005, c, c])
+                recs += [q + [-0.05, 0, 0], q + [-0.6, 0, 0]]
+            else:
+                q = o + np.array([c, c, c])
+                a, b = {"pos": ((0.05, 0, 0), (-0.35, 0, 0)), "tie": ((0.10, 0, 0), (-0.115, 0, 0)),
+                        "flip": ((-0.10, 0, 0), (0.115, 0, 0))}[k]
+                recs += [q + a, q + b]
+            qs.append(q)
+            kind.append(k)
+            g += 1
+    mk = lambda P: np.hstack([np.asarray(P, np.float32), np.tile(np.float32(nrm), (len(P), 1))])
+    return mk(recs), mk(qs), np.array(kind)
+
+
+def test_warm_certificate_refuses_adversarial_steps(fmx_mod, oracle):
+    """the warm certificate (voxelmap.hip, k_match) skips the
+    search the reference always runs (VoxelMap::find_closest, map.tpp:70-91) only when it
+    provably returns the same record.  On the fixture above, per query (fmx_match_cert's
+    flags): the isolated queries are certified, every near tie (< 2 delta), the step
+    toward a competitor (the NN flips) and the cell-face crossing are searched; a rebuilt
+    map with the same query set starts cold.  Every match bit-exact to the oracle."""
+    w, delta = 0.8, 0.01
+    recs, qs, kind = _cert_fixture()
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams())
+    ctx.keypoints_add(0, recs, np.zeros((0, 3), np.float32))
+    I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
+    empty = np.zeros((0, 3), np.float32)
+    q = {"planar": qs, "point": empty}
+    built = _warm_build(ctx, oracle, {0: {"pose": I34, "planar": recs, "point": empty}}, [0], w)
+    ctx.set_queries(qs, empty, 1)
+    step = lambda k: np.hstack([np.eye(3), np.array([[k * delta], [0.0], [0.0]])])
+    log = []
+
+    def run(T, label):
+        _warm_check(ctx, built, q, T, w)
+        got = ctx.match_download()
+        ref = built[0][0].match(qs, T)
+        assert np.array_equal(got["pi"][ref["found"]], ref["pi"][ref["found"]])  # the same record
+        cc = ctx.match_cert(per_query=True)
+        log.append((label, cc["certified"], cc["warm"]))
+        return cc
+
+    cc = run(I34, "cold")
+    assert cc["warm"] == 0 and cc["certified"] == 0 and not cc["flags"].any()
+    # step 1 is the adversarial one: only the isolated queries may certify
+    cc = run(step(1), "step 1")
+    f = cc["flags"].astype(bool)
+    assert cc["warm"] == len(qs)
+    assert f[kind == "pos"].all() and not f[kind != "pos"].any(), (log, kind[f])
+    assert cc["certified"] == int((kind == "pos").sum())
+    # the flip queries' NN did change (the certificate had something to refuse), the
+    # tie queries' did not
+    before = built[0][0].match(qs, I34)["pi"]
+    after = built[0][0].match(qs, step(1))["pi"]
+    moved = np.any(before != after, axis=1)
+    assert moved[kind == "flip"].all() and not moved[kind == "tie"].any()
+    # step 2 continues in +x: the tie queries now move away from their competitor
+    # (margin 0.125 - 0.09 > 2 delta) and the face queries stay in their new cell — both
+    # certify; the flipped queries' margin (0.11 - 0.105 + ...) is still < 2 delta
+    cc = run(step(2), "step 2")
+    f = cc["flags"].astype(bool)
+    assert f[kind != "flip"].all() and not f[kind == "flip"].any(), (log, kind[f])
+    # a rebuilt map (same inputs) with the unchanged query set: cold, then warm again
+    built = _warm_build(ctx, oracle, {0: {"pose": I34, "planar": recs, "point": empty}}, [0], w)
+    cc = run(step(2), "rebuilt: cold")
+    assert cc["warm"] == 0 and cc["certified"] == 0 and not cc["flags"].any()
+    cc = run(step(3), "rebuilt: warm")  # (every query's margin now exceeds 2 delta)
+    assert cc["warm"] == len(qs) and cc["flags"].astype(bool).all(), log
+    print("warm certificate (label, certified, warm):", log)

@@ -15,10 +15,14 @@ Streams come from the trace's Stream_Id column when present, else from kernel na
 (extraction and map-build kernels are the side streams' in the pipelined bench).
 """
 import csv
+import os
 import json
 import re
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import provenance  # noqa: E402
 
 SIDE = re.compile(r"k_extract_rows|k_normals|k_row_blocks|k_closest|k_fit|k_write_features|k_row_scan|k_scan_|k_map_")
 
@@ -72,6 +76,7 @@ def main():
            "main_stream_kernels_us_per_scan": {k: round(v, 2) for k, v in sorted(per.items(), key=lambda x: -x[1])}}
     print(json.dumps(out, indent=1))
     out["skipped_trailing_scans"] = skip
+    provenance.stamp(out)  # the sources this run measured (bench.py marks stale profiles)
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as f:
             json.dump(out, f, indent=1)

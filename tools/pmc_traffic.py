@@ -28,6 +28,9 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import provenance  # noqa: E402
+
 # fmx kernel symbol fragment -> bench.py profile id
 KMAP = {
     "k_match<false, true>": "match_linearize",  # C5: match + single-pose linearization fused
@@ -94,6 +97,7 @@ def main():
            "correction": "per kernel (see 'correction'): coalesced 2 x FETCH_SIZE, random 64-B lines 1 x FETCH_SIZE "
                          "(calibrated, profiles/r2_pmc_calibration.txt), + WRITE_SIZE; KiB -> bytes",
            "kernels": kernels}
+    provenance.stamp(res)  # the sources this run measured (bench.py marks stale profiles)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
