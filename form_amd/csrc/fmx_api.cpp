@@ -8,7 +8,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <execinfo.h>
 #include <functional>
+#include <csignal>
+#include <unistd.h>
 #include <map>
 #include <new>
 #include <set>
@@ -551,8 +554,8 @@ void pf_launch(fmx_ctx* c, bool force = true) {
   const float4* d = reinterpret_cast<const float4*>(c->ann_ptr);
   c->h_pf.ensure(8);
   if (c->pf_seq == 0) c->h_pf.p[4] = 0;
-  FMX_HIP(hipEventRecord(c->ev_pf_fork, c->stream));
-  FMX_HIP(hipStreamWaitEvent(c->side2, c->ev_pf_fork, 0));
+  c->ev_pf_fork.record(c->stream);
+  FMX_HIP(hipStreamWaitEvent(c->side2, c->ev_pf_fork.last(), 0));
   if (c->ann_host) {  // the staged copy -> the device (side2: behind the previous queued extraction's reads)
     c->pf_scan.ensure(c->ann_n);
     if (c->ann_pinned) {
@@ -577,7 +580,7 @@ void pf_launch(fmx_ctx* c, bool force = true) {
     throw;
   }
   swap_query_set(c);
-  FMX_HIP(hipEventRecord(c->ev_pf, c->side2));
+  c->ev_pf.record(c->side2);
   c->pf_launched = true;
   c->pf_ptr = c->ann_ptr;
   c->pf_n = c->ann_n;
@@ -597,7 +600,7 @@ bool pf_take(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, uint64_t scan,
   c->pf_launched = false;
   c->pf_ptr = nullptr;
   swap_query_set(c);
-  FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_pf, 0));
+  FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_pf.last(), 0));
   extract_collect(c, c->pf_L, out);
   ++c->pf_used;
   c->q_scan = scan;
@@ -863,16 +866,23 @@ void swap_match_set(fmx_ctx* c) {
 // instead of matching again; results are bit-identical either way.  The speculative
 // set is not read by any queued kernel: it was swapped out at the start of this ICP
 // iteration and every kernel that read it belongs to earlier, completed iterations.
-void spec_match(fmx_ctx* c, const double* pose_j, bool first = false) {
+// mom_ref (moments mode, else null): K + 1 reference poses (the map scans', then X(j) =
+// pose_j): the speculative set's pair moments are queued right behind its match and
+// scatter (win_moments_current, left pending in the window machinery), so an ICP
+// iteration that takes this match finds its moments under way (c->spec_mom).
+void spec_match(fmx_ctx* c, const double* pose_j, bool first = false, const double* mom_ref = nullptr) {
   const fmx_params& P = c->P;
   swap_match_set(c);
   try {
     run_match(c, pose_j, P.max_dist_matching, P.min_dist_map, true);
+    if (mom_ref) win_moments_current(c, mom_ref, nullptr);
   } catch (...) {
     swap_match_set(c);
     throw;
   }
   swap_match_set(c);
+  c->spec_mom = mom_ref != nullptr;
+  if (mom_ref) c->spec_mom_ref.assign(mom_ref, mom_ref + 12 * ((size_t)c->K + 1));
   std::memcpy(c->spec_pose, pose_j, sizeof(c->spec_pose));
   c->spec_valid = true;
   c->spec_first = first;
@@ -890,11 +900,32 @@ bool use_spec_match(fmx_ctx* c, const double* pose_j) {
 void keyscan_step(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat);
 void record_cons(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j);
 
-// FMX_LIN_ROWS=1 (A/B): the smoother's LMs linearize every trial on the device from the
-// rows (k_win_linearize over the sorted match / the window store), as before round 5;
-// default: from the pair moments (k_win_moments once per ICP iteration, moments.cpp)
+// FMX_TRACE (diagnostic): one stderr line per step of the smoothing-mode registration
+bool trace_on() {
+  static const bool v = std::getenv("FMX_TRACE") != nullptr;
+  return v;
+}
+#define FMX_TRACE_(...)                   \
+  do {                                    \
+    if (trace_on()) {                     \
+      fprintf(stderr, __VA_ARGS__);       \
+      fflush(stderr);                     \
+    }                                     \
+  } while (0)
+
+// The smoother's LMs linearize either every trial on the device from the rows
+// (k_win_linearize over the sorted match / the window store) or from the pair moments
+// (k_win_moments once per ICP iteration, host contractions, moments.cpp).
+// FMX_LIN_ROWS=1 / FMX_MOMENTS=1 choose (A/B); the default is kLinRowsDefault.
+constexpr bool kLinRowsDefault = true;
 bool lin_rows() {
-  static const bool v = std::getenv("FMX_LIN_ROWS") != nullptr;
+  static const bool v = std::getenv("FMX_MOMENTS") ? false : std::getenv("FMX_LIN_ROWS") ? true : kLinRowsDefault;
+  return v;
+}
+// FMX_NO_SPEC_MOMENTS=1 (A/B): a speculative match's pair moments are launched by the ICP
+// iteration that takes it instead of right behind the match
+bool spec_moments() {
+  static const bool v = std::getenv("FMX_NO_SPEC_MOMENTS") == nullptr;
   return v;
 }
 // FMX_FULL_ROWS=1 (A/B): the final LM (every stored pair) linearizes on the device from
@@ -932,8 +963,13 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
   for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
     ++icp;
     const Pose before = e.values.at(j);
-    if (!use_spec_match(c, before.m)) run_match(c, before.m, P.max_dist_matching, P.min_dist_map, true);  // pair-major
+    const bool spec_hit = use_spec_match(c, before.m);
+    if (!spec_hit) run_match(c, before.m, P.max_dist_matching, P.min_dist_map, true);  // pair-major
     c->spec_valid = false;
+    // the taken speculative match's moments are pending (spec_match); a missed one's are
+    // drained by the next window launch
+    const bool mom_queued = spec_hit && c->spec_mom;
+    c->spec_mom = false;
     pf_launch(c, false);  // the announced next scan's extraction, behind this match (host: once staged)
     // get_graph(true): the current scan's K pairs (empty ones linearize to zero)
     g.pairs.clear();
@@ -956,47 +992,89 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       }
       static const bool spec_log = std::getenv("FMX_SPEC_LOG") != nullptr;  // diagnostic
       if (spec_log && lc >= 0.0) fprintf(stderr, "spec it %u lin_change %.3e err %.3e rel %.3e\n", it, lc, ce, lc / ce);
-      if (last_likely && it + 1 < P.max_num_rematches && std::memcmp(xj.m, before.m, sizeof(xj.m)) != 0)
-        spec_match(c, xj.m);
+      if (last_likely && it + 1 < P.max_num_rematches && std::memcmp(xj.m, before.m, sizeof(xj.m)) != 0) {
+        FMX_TRACE_("  spec match\n");
+        if (mom && spec_moments()) {
+          // the next iteration's reference: its LM starts from the window values with
+          // X(j) = this trial's (fast mode keeps only X(j), constraints.cpp:257-266)
+          std::vector<double> ref(12 * ((size_t)K + 1));
+          for (int k = 0; k < K; ++k) std::memcpy(&ref[12 * k], e.values.at(c->map_scans[k]).m, 12 * sizeof(double));
+          std::memcpy(&ref[12 * (size_t)K], xj.m, 12 * sizeof(double));
+          spec_match(c, xj.m, false, ref.data());
+        } else {
+          spec_match(c, xj.m);
+        }
+      }
     };
+    bool launched = false, ready = false, already = false;  // (moments: captured by the LM's callbacks below)
     if (mom) {
-      // the pairs' moments at the LM's starting values (one launch, one wait); every
-      // linearization of this LM is then a host contraction (moments.hpp)
-      const std::vector<Pose> x0 = window_poses(e);
-      mref.resize((size_t)K + 1);
-      table.resize(12 * ((size_t)K + 1));
-      for (int k = 0; k < K; ++k) mref[k] = x0[slot.at(c->map_scans[k])];
-      mref[K] = x0[slot.at(j)];
-      for (int k = 0; k <= K; ++k) std::memcpy(&table[12 * k], mref[k].m, 12 * sizeof(double));
-      momv.resize((size_t)std::max(K, 1) * kMomPairD);
-      {
+      // The pairs' moments at the LM's starting values: launched by the LM's first
+      // linearization (split form: the host builds the base system and the non-pair
+      // terms while the moments kernel runs) and waited for in its lin_end; from then on
+      // every linearization of this LM is a host contraction (moments.hpp), no launch.
+      auto lin_begin = [&](const std::vector<Pose>& x) {
         HostScope hs(10);
-        win_moments_current(c, table.data(), momv.data());
-        match_counts_fetch(c, false);  // the match finished before the moments
-      }
-      for (int k = 0; k < K; ++k)  // pairs without rows are never written by the kernel
-        if (c->cnt_pl[k] + c->cnt_pt[k] == 0) std::fill(&momv[(size_t)k * kMomPairD], &momv[(size_t)(k + 1) * kMomPairD], 0.0);
-      mp.resize(K);
-      mri.resize(K);
-      mrj.assign(K, &mref[K]);
-      mxi.resize(K);
-      mxj.resize(K);
-      for (int k = 0; k < K; ++k) {
-        mp[k] = &momv[(size_t)k * kMomPairD];
-        mri[k] = &mref[k];
-      }
-      mom_prepare(mbatch, K, mp.data(), mri.data(), mrj.data());
-      g.lin_begin = nullptr;
-      g.lin_end = nullptr;
-      g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
-        HostScope hs(10);
+        if (!launched && mom_queued) {  // queued behind the speculative match (spec_match)
+          mref.resize((size_t)K + 1);
+          for (int k = 0; k <= K; ++k) std::memcpy(mref[k].m, &c->spec_mom_ref[12 * (size_t)k], 12 * sizeof(double));
+          momv.resize((size_t)std::max(K, 1) * kMomPairD);
+          launched = true;
+          FMX_TRACE_("scan %llu it %u: moments queued with the spec match\n", (unsigned long long)j, it);
+        }
+        if (!launched) {
+          mref.resize((size_t)K + 1);
+          table.resize(12 * ((size_t)K + 1));
+          for (int k = 0; k < K; ++k) mref[k] = x[slot.at(c->map_scans[k])];
+          mref[K] = x[slot.at(j)];
+          for (int k = 0; k <= K; ++k) std::memcpy(&table[12 * k], mref[k].m, 12 * sizeof(double));
+          momv.resize((size_t)std::max(K, 1) * kMomPairD);
+          static const bool eager = std::getenv("FMX_MOM_EAGER") != nullptr;  // diagnostic
+          FMX_TRACE_("scan %llu it %u: moments launch K %d chunks %u\n", (unsigned long long)j, it, K, c->max_chunks);
+          win_moments_current(c, table.data(), eager ? momv.data() : nullptr);  // launch only; win_finish in lin_end
+          FMX_TRACE_("  launched\n");
+          launched = true;
+          if (eager) already = true;
+        }
         maybe_spec(x);
-        for (int k = 0; k < K; ++k) {
+        mxi.resize(K);
+        mxj.resize(K);
+        for (int k = 0; k < K; ++k) {  // (x outlives the lin_end of this linearization)
           mxi[k] = &x[slot.at(c->map_scans[k])];
           mxj[k] = &x[slot.at(j)];
         }
-        mom_eval(mbatch, mxi.data(), mxj.data(), 1.0 / sigma, G);
       };
+      auto lin_end = [&](double* G) {
+        HostScope hs(10);
+        if (!ready) {
+          FMX_TRACE_("  wait\n");
+          if (!already) win_finish(c, momv.data());
+          FMX_TRACE_("  moments in\n");
+          match_counts_fetch(c, false);  // the match finished before the moments
+          for (int k = 0; k < K; ++k)  // pairs without rows are never written by the kernel
+            if (c->cnt_pl[k] + c->cnt_pt[k] == 0)
+              std::fill(&momv[(size_t)k * kMomPairD], &momv[(size_t)(k + 1) * kMomPairD], 0.0);
+          mp.resize(K);
+          mri.resize(K);
+          mrj.assign(K, &mref[K]);
+          for (int k = 0; k < K; ++k) {
+            mp[k] = &momv[(size_t)k * kMomPairD];
+            mri[k] = &mref[k];
+          }
+          HostScope hp(19);
+          mom_prepare(mbatch, K, mp.data(), mri.data(), mrj.data());
+          FMX_TRACE_("  prepared\n");
+          ready = true;
+        }
+        HostScope he(18);
+        mom_eval(mbatch, mxi.data(), mxj.data(), 1.0 / sigma, G);
+        FMX_TRACE_("  eval\n");
+      };
+      set_lin(g, lin_begin, lin_end);
+      static const bool nosplit = std::getenv("FMX_MOM_NOSPLIT") != nullptr;  // diagnostic
+      if (nosplit) {
+        g.lin_begin = nullptr;
+        g.lin_end = nullptr;
+      }
     } else {
       // split form: launch, the host assembles the non-pair terms, then wait (smoother.hpp)
       auto lin_begin = [&](const std::vector<Pose>& x) {
@@ -1017,7 +1095,9 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       set_lin(g, lin_begin, lin_end);
     }
     HostScope* hs_lm = new HostScope(8);
+    FMX_TRACE_("scan %llu it %u: lm\n", (unsigned long long)j, it);
     const WinLMResult R = window_lm(g, window_poses(e));
+    FMX_TRACE_("scan %llu it %u: lm done\n", (unsigned long long)j, it);
     delete hs_lm;
     lm_it += R.iters;
     lins += R.lins;
@@ -1057,7 +1137,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
   // keyscan step (form.cpp:104-111): it reads only the constraint counts, so it runs
   // before optimize(false); the next map's scans are known from here on
   keyscan_step(c, e, j, nfeat);
-  FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the insert: the pool is final
+  c->ev_fork.record(c->stream);  // after the insert: the pool is final
   std::vector<uint64_t> map_scans;
   {
     std::set<uint64_t> sset;
@@ -1091,9 +1171,11 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       std::vector<double> mpo(12 * map_scans.size());
       for (size_t k = 0; k < map_scans.size(); ++k) std::memcpy(&mpo[12 * k], x[slot.at(map_scans[k])].m, 12 * sizeof(double));
       if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));  // pinned staging reuse (see register_scan)
-      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork.last(), 0));
+      FMX_TRACE_("  spec map build\n");
       run_map_build(c, map_scans, mpo.data(), P.max_dist_matching, c->side);
-      FMX_HIP(hipEventRecord(c->ev_join, c->side));
+      c->ev_join.record(c->side);
+      FMX_TRACE_("  spec map queued\n");
       e.spec_map = true;
       e.spec_map_scans = map_scans;
       e.spec_map_poses = std::move(mpo);
@@ -1112,7 +1194,10 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       mri[p] = &m.ref_i;
       mrj[p] = &m.ref_j;
     }
-    mom_prepare(mbatch, (int)np, mp.data(), mri.data(), mrj.data());
+    {
+      HostScope hp(19);
+      mom_prepare(mbatch, (int)np, mp.data(), mri.data(), mrj.data());
+    }
     g.lin_begin = nullptr;
     g.lin_end = nullptr;
     g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
@@ -1122,6 +1207,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
         mxi[p] = &x[g.pairs[p].first];
         mxj[p] = &x[g.pairs[p].second];
       }
+      HostScope he(18);
       mom_eval(mbatch, mxi.data(), mxj.data(), 1.0 / sigma, G);
     };
   } else {
@@ -1138,9 +1224,11 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     };
     set_lin(g, lin_begin, lin_end);
   }
+  FMX_TRACE_("scan %llu: full lm, %zu pairs\n", (unsigned long long)j, prs.size());
   HostScope* hs_lm = new HostScope(9);
   const WinLMResult R = window_lm(g, window_poses(e));
   delete hs_lm;
+  FMX_TRACE_("scan %llu: full lm done, %d spec maps\n", (unsigned long long)j, spec_builds);
   lm_it += R.iters;
   lins += R.lins;
   for (size_t k = 0; k < keys.size(); ++k) e.values[keys[k]] = R.x[k];  // update_values
@@ -1314,6 +1402,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     throw StatusError(FMX_E_SIZE, "Provided scan does not match the expected size " + std::to_string(RC) +
                                       " != " + std::to_string(n));
   const uint64_t j = e.init ? e.scan + 1 : 0;
+  FMX_TRACE_("scan %llu: register_scan\n", (unsigned long long)j);
   const uint64_t waits0 = c->host_waits;
   const uint64_t spec0 = c->spec_launched, hits0 = c->spec_hits, pf0 = c->pf_used;
   c->spec_valid = false;  // a new map and query set: no speculation carries over
@@ -1353,7 +1442,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
   // run (extraction occupies one CU per scan line, so the build's kernels take the
   // idle CUs, and its host launch cost hides behind the extraction wait).
   fmx_feature_counts fc{};
-  FMX_HIP(hipEventRecord(c->ev_fork, c->stream));  // after the previous scan's insert
+  c->ev_fork.record(c->stream);  // after the previous scan's insert
   auto map_inputs = [&] {
     prepare();
     const bool spec_ok = e.spec_map && e.spec_map_scans == scans && e.spec_map_poses.size() == poses.size() &&
@@ -1365,9 +1454,9 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       // a discarded speculative build may still be reading the pinned pose staging
       // buffer this build rewrites: drain it first (misses are rare)
       if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));
-      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork.last(), 0));
       run_map_build(c, scans, poses.data(), P.max_dist_matching, c->side);
-      FMX_HIP(hipEventRecord(c->ev_join, c->side));
+      c->ev_join.record(c->side);
     }
     e.spec_map = false;
   };
@@ -1378,8 +1467,17 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       // first ICP match (at the prediction) is queued before the host's finish() work,
       // which then overlaps it; the ICP loop takes it as a speculative match.
       map_inputs();
-      FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
-      if (!P.disable_smoothing) spec_match(c, e.values.at(j).m, true);
+      FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join.last(), 0));
+      if (!P.disable_smoothing) {
+        if (!lin_rows() && spec_moments()) {  // + the first ICP iteration's moments (its x0: the window values)
+          std::vector<double> ref(12 * ((size_t)c->K + 1));
+          for (uint32_t k = 0; k < c->K; ++k) std::memcpy(&ref[12 * k], e.values.at(c->map_scans[k]).m, 12 * sizeof(double));
+          std::memcpy(&ref[12 * (size_t)c->K], e.values.at(j).m, 12 * sizeof(double));
+          spec_match(c, e.values.at(j).m, true, ref.data());
+        } else {
+          spec_match(c, e.values.at(j).m, true);
+        }
+      }
       finish();
     } else {
       do_extract(c, xyzw, n, j, on_dev, &fc, [&] {
@@ -1388,7 +1486,8 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       });
     }
   }
-  FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+  FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join.last(), 0));
+  FMX_TRACE_("scan %llu: extracted %u + %u, map queued\n", (unsigned long long)j, fc.planar, fc.point);
   HostScope* hs_icp = new HostScope(4);
   uint64_t icp = 0, lm_it = 0, lins = 0;
   bool inserted = false;
@@ -1442,6 +1541,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
     run_insert(c, j, nullptr);
     keyscan_step(c, e, j, fc.planar + fc.point);  // marginalization: deferred (finish_tail)
   }
+  FMX_TRACE_("scan %llu: done\n", (unsigned long long)j);
   c->stats[0] = icp;
   c->stats[1] = lm_it;
   c->stats[2] = e.last_mpl;
@@ -1496,8 +1596,23 @@ void fmx_default_params(fmx_params* p) {
   p->voxel_subdivision = 1;
 }
 
+// FMX_SEGV_TRACE (diagnostic): a native backtrace on SIGSEGV / SIGABRT, then the default action
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "fmx: native backtrace\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
   if (!p || !out) return FMX_E_INVAL;
+  if (std::getenv("FMX_SEGV_TRACE")) {
+    signal(SIGSEGV, segv_trace);
+    signal(SIGABRT, segv_trace);
+  }
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return FMX_E_HIP;
@@ -1515,10 +1630,10 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     FMX_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
     FMX_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_lo));
     FMX_HIP(hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, prio_lo));
-    FMX_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    FMX_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-    FMX_HIP(hipEventCreateWithFlags(&c->ev_pf, hipEventDisableTiming));
-    FMX_HIP(hipEventCreateWithFlags(&c->ev_pf_fork, hipEventDisableTiming));
+    c->ev_fork.create();
+    c->ev_join.create();
+    c->ev_pf.create();
+    c->ev_pf_fork.create();
     const uint64_t cap = p->keypoint_pool_capacity ? p->keypoint_pool_capacity : (4u << 20);
     c->pool[0].planar = true;
     c->pool[1].planar = false;
@@ -1584,7 +1699,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
-  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release(); c->mcert.release(); c->mprof.release();
+  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release(); c->mcert.release(); c->mprof.release(); c->mord.release(); c->mcost.release();
   c->cert_b2.release();
   {
     auto& S = c->spec;
@@ -1603,10 +1718,10 @@ void fmx_destroy(fmx_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->side2) (void)hipStreamDestroy(c->side2);
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-  if (c->ev_pf) (void)hipEventDestroy(c->ev_pf);
-  if (c->ev_pf_fork) (void)hipEventDestroy(c->ev_pf_fork);
+  c->ev_fork.destroy();
+  c->ev_join.destroy();
+  c->ev_pf.destroy();
+  c->ev_pf_fork.destroy();
   delete c;
 }
 

@@ -94,6 +94,29 @@ struct HBuf {  // pinned host memory, also mapped into the device address space
   }
 };
 
+// A ring of events (fmx_ctx's cross-stream ordering): record() takes the next event,
+// last() is the most recently recorded one.
+struct EvRing {
+  static constexpr int kN = 8;
+  hipEvent_t e[kN] = {};
+  int cur = 0;
+  void create() {
+    for (auto& x : e)
+      if (!x) FMX_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  }
+  void destroy() {
+    for (auto& x : e)
+      if (x) (void)hipEventDestroy(x);
+    for (auto& x : e) x = nullptr;
+  }
+  hipEvent_t record(hipStream_t st) {
+    cur = (cur + 1) % kN;
+    FMX_HIP(hipEventRecord(e[cur], st));
+    return e[cur];
+  }
+  hipEvent_t last() const { return e[cur]; }
+};
+
 // Profiled kernel classes (bench.py roofline).
 enum ProfId {
   PROF_EXTRACT_ROWS = 0,
@@ -306,7 +329,12 @@ struct fmx_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;                    // map build, overlapped with extraction
   hipStream_t side2 = nullptr;                   // pipelined extraction of the announced next scan
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // stream -> side -> stream ordering
+  // stream -> side -> stream ordering.  Rings of events: each record takes the next one
+  // and a wait uses the last recorded, so an event is never re-recorded while an earlier
+  // cross-stream wait on it may still be pending in the runtime (a re-record right after
+  // a hipStreamWaitEvent was seen to corrupt the HIP runtime's state when the host moved
+  // fast between them)
+  fmx::EvRing ev_fork, ev_join;
   std::string err;
   fmx::Prof prof;
 
@@ -342,7 +370,7 @@ struct fmx_ctx {
   fmx::ExLaunch pf_L;
   uint32_t pf_seq = 0;              // its completion word's sequence number
   fmx::HBuf<uint32_t> h_pf;         // pinned: [0..2] its totals, [4] its completion word
-  hipEvent_t ev_pf = nullptr, ev_pf_fork = nullptr;
+  fmx::EvRing ev_pf, ev_pf_fork;
   uint64_t pf_used = 0, pf_dropped = 0;
 
   // ---- host-resident scans (stage.hpp): the reference passes the scan as a host
@@ -447,6 +475,9 @@ struct fmx_ctx {
   uint32_t cert_tot[2] = {0, 0};                  // ... its certified / warm query counts
   fmx::DBuf<uint32_t> mcert;                      // the match launches' certified / warm sums (self-resetting)
   fmx::DBuf<uint32_t> mprof;                      // profiled match launches' probe / candidate sums (self-resetting)
+  fmx::DBuf<uint32_t> mord, mcost;                // heaviest-first query-block order + per-block durations (k_match)
+  uint64_t ord_gen = 0;                           // warm_gen when mord was written (0: none)
+  uint32_t ord_nb = 0;                            // ... for this many query blocks
   uint32_t match_nb_pl = 0, match_nb = 0;         // blocks of the last match
   uint32_t n_qo = 0;                              // queries of the last query-order match
   fmx::HBuf<uint32_t> h_flag;                     // mapped completion word (wait_flag)
@@ -474,6 +505,8 @@ struct fmx_ctx {
   hipStream_t match_stream = nullptr;  // run_match / run_pair_scatter stream override
   bool spec_valid = false;
   bool spec_first = false;  // the speculative set holds the scan's first match (not a speculation)
+  bool spec_mom = false;    // ... and its pair moments are pending in the window machinery (win_moments_current)
+  std::vector<double> spec_mom_ref;  // ... taken at these K + 1 reference poses
   double spec_pose[12] = {};
   uint64_t spec_launched = 0, spec_hits = 0;
   uint64_t spec_map_hits = 0, spec_map_misses = 0;  // speculative map builds kept / rebuilt
@@ -498,15 +531,16 @@ namespace fmx {
 // printed to stderr at exit.  Diagnostic only.
 struct HostTiming {
   bool on = std::getenv("FMX_HOST_TIMING") != nullptr;
-  double t[18] = {0};
-  uint64_t n[18] = {0};
+  double t[20] = {0};
+  uint64_t n[20] = {0};
   ~HostTiming() {
     if (!on) return;
-    static const char* names[18] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop",
+    static const char* names[20] = {"register_scan", "stream_wait", "extract", "map_build", "icp_loop",
                                     "insert+tail", "map_host_prep", "map_launches", "fast_lm", "full_lm",
                                     "lin_callback", "marginalize", "win_launch_call", "win_wait",
-                                    "pf_launch", "between_calls", "match_call", "scatter_call"};
-    for (int i = 0; i < 18; ++i)
+                                    "pf_launch", "between_calls", "match_call", "scatter_call", "mom_eval",
+                                    "mom_prepare"};
+    for (int i = 0; i < 20; ++i)
       if (n[i]) fprintf(stderr, "host %-14s %10.1f us total %8llu calls %8.2f us/call\n", names[i], t[i] * 1e6,
                         (unsigned long long)n[i], t[i] * 1e6 / n[i]);
     fprintf(stderr, "host device-buffer reallocations %llu\n", (unsigned long long)dbuf_reallocs().load());

@@ -464,13 +464,34 @@ struct Assembler {
       }
     }
   }
+  // S back to the base system.  A linearization changes only the entries the pairs'
+  // 6 x 6 blocks ((i,i), (i,j), (j,i), (j,j)) and the rhs row / column cover (the prior
+  // and linear factors' information is in the base; their rhs terms go to the last
+  // row / column), so only those are copied back from the base — the same values a
+  // full copy would give, at a fraction of the D^2 doubles.
+  void reset(DenseSys& S) const {
+    const int D = base.D, ld = D + 1;
+    auto blk = [&](int si, int sj) {
+      for (int r = 0; r < 6; ++r)
+        std::memcpy(&S.A[(size_t)(6 * si + r) * ld + 6 * sj], &base.A[(size_t)(6 * si + r) * ld + 6 * sj],
+                    6 * sizeof(double));
+    };
+    for (const auto& pr : g.pairs) {
+      blk(pr.first, pr.first);
+      blk(pr.first, pr.second);
+      blk(pr.second, pr.first);
+      blk(pr.second, pr.second);
+    }
+    for (int r = 0; r < D; ++r) S.A[(size_t)r * ld + D] = base.A[(size_t)r * ld + D];
+    std::memcpy(&S.A[(size_t)D * ld], &base.A[(size_t)D * ld], ld * sizeof(double));
+  }
   // started: the caller already issued lin_begin(x) (window_lm's first linearization,
   // launched before this Assembler was built)
   double run(const std::vector<Pose>& x, DenseSys& S, std::vector<double>& G, int& lins, bool started = false) const {
     const bool split = !g.pairs.empty() && g.lin_begin;
     if (split && !started) g.lin_begin(x);  // device work overlaps everything below up to lin_end
     if (S.D != base.D || S.keys != base.keys) S = base;
-    else std::memcpy(S.A.data(), base.A.data(), base.A.size() * sizeof(double));
+    else reset(S);
     G.assign(g.pairs.size() * kPairG, 0.0);
     if (!split && !g.pairs.empty()) {
       g.lin_pairs(x, G.data());
@@ -508,8 +529,7 @@ struct Assembler {
       double dGd = 0, dg = 0;
       for (int r = 0; r < n; ++r) {
         const double* Ir = I + (size_t)r * m;
-        double sr = 0;
-        for (int c = 0; c < n; ++c) sr += Ir[c] * dp[c];
+        const double sr = dot(Ir, dp, n);  // (I d)_r: vector partial sums on AVX-512 hosts
         const int cr = 6 * S.slot.at(L->keys[r / 6]) + r % 6;
         const double gr = Ir[n] - sr;
         S.at(cr, D) += gr;

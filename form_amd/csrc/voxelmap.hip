@@ -529,7 +529,17 @@ struct MatchArgs {
   // (its pinned slot of the profiler's work ring: the byte model of THIS launch)
   uint32_t* prof_acc;
   uint32_t* prof_work;
+  // Heaviest-first dispatch (VERDICT r4 "next round" 4; 8-lane build only): workgroup b
+  // processes query block order[b] (null: b).  Every query block stores its duration
+  // to cost[] (null: not kept) and the launch's last block rewrites order[] for the next
+  // match on the same map and query set: query blocks by duration class, longest first
+  // (stable within a class).  The results are the same in any order — only which
+  // workgroup takes which query block changes.
+  uint32_t* order;
+  uint32_t* cost;
+  int order_write;  // the last block writes order[] (nb <= kOrderMaxBlocks)
 };
+constexpr uint32_t kOrderMaxBlocks = 8 * 256;  // the last block's counting sort: <= 8 entries per thread
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
 // g, g+kGroup, ... (3-4 of the 27 voxels), then the group min-reduces
@@ -1551,6 +1561,32 @@ __device__ inline void match_tail(const MatchArgs& a, uint32_t* __restrict__ mcn
   if (tiled) pair_sort_tail(a, thist, so, host_counts, s_pb);
 }
 
+// The last block: the next launch's query-block order, longest first.  Four duration
+// classes (>= 16, 8, 4 us, shorter; 100 MHz ticks), a stable counting sort: thread t
+// takes query blocks [R t, R t + R), one four-way block scan gives each its slot.  Every
+// block's cost was stored (agent scope) before its ticket.
+__device__ inline void write_order(const MatchArgs& a, uint32_t nb) {
+  constexpr int R = kOrderMaxBlocks / kMatchThreads;
+  __shared__ uint32_t ws4[kMatchThreads / kWave][4];
+  uint32_t cls[R], cnt[4] = {0, 0, 0, 0};
+  const uint32_t b0 = threadIdx.x * R;
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const uint32_t b = b0 + u;
+    const uint32_t t = b < nb ? __hip_atomic_load(a.cost + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    cls[u] = t >= 1600u ? 0u : t >= 800u ? 1u : t >= 400u ? 2u : 3u;
+    if (b < nb) ++cnt[cls[u]];
+  }
+  uint32_t ex[4], tot[4];
+  block_excl_scan4(cnt, ex, tot, ws4);
+  const uint32_t base[4] = {0u, tot[0], tot[0] + tot[1], tot[0] + tot[1] + tot[2]};
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const uint32_t b = b0 + u;
+    if (b < nb) a.order[base[cls[u]] + ex[cls[u]]++] = b;
+  }
+}
+
 template <bool DENSE, bool FUSED = false>
 __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
@@ -1566,8 +1602,9 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
                                                          uint32_t* __restrict__ thist, SortOut so, FusedArgs fz) {
   extern __shared__ uint32_t s_hist[];  // [K]
   const double* Tj = a.Tj;
-  const bool planar = blockIdx.x < a.nb_pl;
-  const uint32_t bt = planar ? blockIdx.x : blockIdx.x - a.nb_pl;  // the block's index in its type
+  const uint32_t bq = a.order ? a.order[blockIdx.x] : blockIdx.x;  // this workgroup's query block
+  const bool planar = bq < a.nb_pl;
+  const uint32_t bt = planar ? bq : bq - a.nb_pl;  // the block's index in its type
   const uint32_t qi = bt * kQPB + threadIdx.x / kGroup;  // the block's first query + the group
   const int g = threadIdx.x % kGroup;
   const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
@@ -1734,7 +1771,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
       tc += s_work[1][i];
       mq = max(mq, s_work[2][i]);
     }
-    uint4* w4 = reinterpret_cast<uint4*>(work) + 2 * blockIdx.x;
+    uint4* w4 = reinterpret_cast<uint4*>(work) + 2 * bq;
     uint32_t d0 = 0, d1 = 0, d2 = 0;
 #ifdef FMX_DIAG_WALK
     for (int i = 0; i < kMatchThreads / kWave; ++i) {
@@ -1752,8 +1789,10 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     d1 = s_cert[1];
     d2 = s_cert[2];
 #endif
+    const uint32_t t_end = (uint32_t)wall_clock64();
     w4[0] = make_uint4(tp, tc, mq, d0);
-    w4[1] = make_uint4(t_begin, (uint32_t)wall_clock64(), d1, d2);
+    w4[1] = make_uint4(t_begin, t_end, d1, d2);
+    if (a.cost) __hip_atomic_store(a.cost + bq, t_end - t_begin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a.prof_work) {  // this launch's totals (byte model), drained with the ticket's vmcnt(0)
       __hip_atomic_fetch_add(a.prof_acc, tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(a.prof_acc + 1, tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1880,7 +1919,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   }
   __syncthreads();  // every emit's LDS counts are in
   if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
-    __hip_atomic_store(ins_blk + blockIdx.x, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ins_blk + bq, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if FMX_CERT_ANY
   if (threadIdx.x == 0 && a.cert_cnt) {  // the launch's certified / warm totals (a warm launch only)
     if (s_cert[0]) __hip_atomic_fetch_add(a.cert_cnt, s_cert[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1892,7 +1931,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     // per-(type, pair, tile) counts: agent-scope adds, scanned by the last block
     const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.ntl_pl;
     const uint32_t ntl = planar ? a.ntl_pl : a.ntl_pt;
-    const uint32_t tile = (planar ? blockIdx.x : blockIdx.x - a.nb_pl) / kTileBlocks;
+    const uint32_t tile = bt / kTileBlocks;
     for (int k = threadIdx.x; k < a.K; k += kMatchThreads)
       if (s_hist[k])
         __hip_atomic_fetch_add(thist + hbase + (size_t)k * ntl + tile, s_hist[k], __ATOMIC_RELAXED,
@@ -1902,7 +1941,6 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     // destination offset (k_pair_base / k_pair_scatter)
     const size_t hbase = planar ? (size_t)0 : (size_t)a.K * a.nb_pl;
     const uint32_t nbt = planar ? a.nb_pl : a.nb_pt;
-    const uint32_t bt = planar ? blockIdx.x : blockIdx.x - a.nb_pl;
     for (int k = threadIdx.x; k < a.K; k += kMatchThreads) hist[hbase + (size_t)k * nbt + bt] = s_hist[k];
   } else {
     // counts only: agent-scope adds into mcnt[type][pair]
@@ -1936,6 +1974,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     }
   }
   match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
+  if (a.order_write) write_order(a, gridDim.x);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2380,6 +2419,11 @@ void run_pair_scatter(fmx_ctx* c) {
   FMX_HIP(hipGetLastError());
 }
 
+// FMX_NO_LPT: query blocks dispatched in index order (A/B switch; same results)
+static bool no_lpt() {
+  static const bool v = std::getenv("FMX_NO_LPT") != nullptr;
+  return v;
+}
 // FMX_NO_WARM: every match cold; FMX_NO_CELL_CACHE: warm matches probe their own cell
 // again (A/B switches; results are identical either way)
 static bool no_warm() {
@@ -2467,6 +2511,18 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   ensure_zeroed(c->mticket, 1, st);
   ensure_zeroed(c->mcert, 2, st);
   a.cert_cnt = c->mcert.p;
+  // heaviest-first dispatch: the order the last match on this map and query set wrote
+  {
+    const uint32_t nbq = (c->n_qpl + kQPB - 1) / kQPB + (c->n_qpt + kQPB - 1) / kQPB;
+    const bool on = kGroup > 1 && !no_lpt() && nbq > 0 && nbq <= kOrderMaxBlocks;
+    c->mcost.ensure(nbq + 1);
+    c->mord.ensure(nbq + 1);
+    a.order = on && c->ord_gen == c->warm_gen && c->ord_nb == nbq ? c->mord.p : nullptr;
+    a.cost = on ? c->mcost.p : nullptr;
+    a.order_write = on ? 1 : 0;
+    c->ord_gen = on ? c->warm_gen : 0;
+    c->ord_nb = nbq;
+  }
   c->ins_blk.ensure(nb + 1);
   c->ins_off.ensure(nb + 1);
   ensure_zeroed(c->thist, (size_t)K * (a.ntl_pl + a.ntl_pt) + 1, st);
@@ -2582,6 +2638,9 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   a.cert_b2 = nullptr;
 #endif
   a.cert_cnt = nullptr;
+  a.order = nullptr;
+  a.cost = nullptr;
+  a.order_write = 0;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;

@@ -139,4 +139,65 @@ class FmxBatch {
   uint64_t launches_ = 0;
 };
 
+// The same seam from pair moments (fmx_moments / fmx_moments_contract): the device
+// reduces every pair's rows ONCE, at reference poses, into 16 x 16 moments; every later
+// linearization — one per LM iteration of GTSAM's optimizer, at whatever Values it
+// proposes — is a host contraction with no device round trip (full 13 x 13 only).
+// Reload (set_pairs) after every fmx_match / fmx_corr_set: the moments belong to the
+// correspondences they were taken from (checked against fmx_corr_generation).
+class FmxMomentBatch {
+ public:
+  FmxMomentBatch(fmx_ctx* ctx, double sigma) : ctx_(ctx), sigma_(sigma) {}
+
+  // pair k = (X(key_i[k]), X(key_j[k])); the moments are taken at pose_of's poses now
+  template <class PoseOf>
+  void set_pairs(const std::vector<uint64_t>& key_i, const std::vector<uint64_t>& key_j, PoseOf&& pose_of) {
+    if (key_i.size() != key_j.size()) throw std::invalid_argument("FmxMomentBatch: key lists differ in length");
+    ki_ = key_i;
+    kj_ = key_j;
+    const size_t K = ki_.size();
+    ri_.resize(12 * K);
+    rj_.resize(12 * K);
+    for (size_t k = 0; k < K; ++k) {
+      pose_of(ki_[k], &ri_[12 * k]);
+      pose_of(kj_[k], &rj_[12 * k]);
+    }
+    mom_.assign((K ? K : 1) * 272, 0.0);
+    const fmx_status st = fmx_moments(ctx_, ri_.data(), rj_.data(), mom_.data());
+    if (st != FMX_OK) throw std::runtime_error(std::string("fmx_moments: ") + fmx_last_error(ctx_));
+    if (fmx_corr_generation(ctx_, &gen_) != FMX_OK) throw std::runtime_error("fmx_corr_generation failed");
+  }
+  size_t pairs() const { return ki_.size(); }
+
+  // packed 13 x 13 G of every pair (K x 91) at pose_of's poses: host only
+  template <class PoseOf>
+  const double* linearize_all(PoseOf&& pose_of) {
+    uint64_t gen = 0;
+    if (fmx_corr_generation(ctx_, &gen) != FMX_OK || gen != gen_)
+      throw std::logic_error("FmxMomentBatch: the correspondences changed since set_pairs");
+    const size_t K = ki_.size();
+    pi_.resize(12 * K);
+    pj_.resize(12 * K);
+    for (size_t k = 0; k < K; ++k) {
+      pose_of(ki_[k], &pi_[12 * k]);
+      pose_of(kj_[k], &pj_[12 * k]);
+    }
+    G_.assign((K ? K : 1) * 91, 0.0);
+    err_.assign(K ? K : 1, 0.0);
+    const fmx_status st = fmx_moments_contract((uint32_t)K, mom_.data(), ri_.data(), rj_.data(), pi_.data(), pj_.data(),
+                                               sigma_, G_.data(), err_.data());
+    if (st != FMX_OK) throw std::runtime_error("fmx_moments_contract failed");
+    return G_.data();
+  }
+  Hessian2 hessian2(size_t k) const { return unpack13(G_.data() + 91 * k); }
+  double error(size_t k) const { return err_.at(k); }
+
+ private:
+  fmx_ctx* ctx_;
+  double sigma_;
+  std::vector<uint64_t> ki_, kj_;
+  std::vector<double> ri_, rj_, pi_, pj_, mom_, G_, err_;
+  uint64_t gen_ = 0;
+};
+
 }  // namespace fmx_seam

@@ -191,6 +191,44 @@ int main() {
     check(batch.error(0) != before, "new poses change the error", 0, batch.error(0), before);
     pose[100][3] -= 0.01;
   }
+  // the moment form of the seam: moments once at the current poses, then host-only
+  // linearizations at moved poses, against the oracle (1e-10)
+  {
+    fmx_seam::FmxMomentBatch mb(ctx, sigma);
+    mb.set_pairs(key_i, key_j, pose_of);
+    for (int step = 0; step < 3; ++step) {
+      for (auto& kv : pose) kv.second[3] += 0.004 * (step + 1), kv.second[7] -= 0.002;
+      mb.linearize_all(pose_of);
+      std::vector<double> Pi(12 * K), Pj(12 * K), Go((size_t)K * 91), eo(K);
+      for (uint32_t k = 0; k < K; ++k) {
+        pose_of(key_i[k], &Pi[12 * k]);
+        pose_of(key_j[k], &Pj[12 * k]);
+      }
+      orc_linearize(K, np.data(), ppi.data(), pni.data(), ppj.data(), nt.data(), tpi.data(), tpj.data(), Pi.data(),
+                    Pj.data(), sigma, 0, Go.data(), eo.data());
+      for (uint32_t k = 0; k < K; ++k) {
+        double scale = 0.0;
+        for (int q = 0; q < 91; ++q) scale = std::max(scale, std::fabs(Go[91 * k + q]));
+        const fmx_seam::Hessian2 h = mb.hessian2(k);
+        for (int u = 0; u < 6; ++u)
+          for (int v = 0; v < 6; ++v)
+            check(std::fabs(h.G11[6 * u + v] - fmx_seam::packed_at(&Go[91 * k], 13, u, v)) <= 1e-10 * scale,
+                  "moments G11 vs oracle", k, h.G11[6 * u + v], fmx_seam::packed_at(&Go[91 * k], 13, u, v));
+        check(std::fabs(mb.error(k) - eo[k]) <= 1e-10 * std::max(eo[k], 1e-300), "moments error vs oracle", k,
+              mb.error(k), eo[k]);
+      }
+    }
+    // a re-set of the correspondences invalidates the moments
+    if (fmx_corr_set(ctx, K, np.data(), ppi.data(), pni.data(), ppj.data(), nt.data(), tpi.data(), tpj.data()) != FMX_OK)
+      return 1;
+    bool threw = false;
+    try {
+      mb.linearize_all(pose_of);
+    } catch (const std::logic_error&) {
+      threw = true;
+    }
+    check(threw, "stale moments rejected", 0, threw ? 1.0 : 0.0, 1.0);
+  }
   fmx_destroy(ctx);
   if (g_fail) {
     std::fprintf(stderr, "%d checks failed\n", g_fail);

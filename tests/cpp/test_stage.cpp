@@ -19,7 +19,31 @@ static int g_fail = 0;
     }                                                            \
   } while (0)
 
+// the helpers' CPUs are within the process's load-time CPUs (taskset /
+// FMX_STAGE_CPUS), never the creator's own, and a one-CPU process keeps its mask.
+static int check_helper_cpus() {
+  int bad = 0;
+  for (int cpu = 0; cpu < CPU_SETSIZE; ++cpu) {
+    if (!CPU_ISSET(cpu, &fmx::g_load_cpus)) continue;
+    cpu_set_t m;
+    const bool set = fmx::helper_cpus(cpu, m);
+    if (!set) {
+      bad += CPU_COUNT(&fmx::g_load_cpus) > 1;  // only a single-CPU process may keep the inherited mask
+      continue;
+    }
+    if (CPU_ISSET(cpu, &m)) ++bad;
+    cpu_set_t x;
+    CPU_AND(&x, &m, &fmx::g_load_cpus);
+    if (!CPU_EQUAL(&x, &m)) ++bad;
+  }
+  return bad;
+}
+
 int main() {
+  if (check_helper_cpus()) {
+    std::printf("helper CPUs outside the load-time mask\n");
+    return 1;
+  }
   std::mt19937 g(7);
   fmx::Stager st;
   fmx::StageReq r[3];

@@ -18,3 +18,15 @@ def test_stage_helpers(name):
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([path], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "stage ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+def test_stage_helpers_respect_a_restricted_mask():
+    """The same run restricted to two CPUs (taskset-like affinity before the library
+    loads, and FMX_STAGE_CPUS narrowing it to one): the helper-CPU check holds."""
+    path = os.path.join(ROOT, "tests", "cpp", "test_stage")
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    for env_extra in ({}, {"FMX_STAGE_CPUS": str(cpus[0])}):
+        env = dict(os.environ, **env_extra)
+        r = subprocess.run([path], capture_output=True, text=True, timeout=300, env=env,
+                           preexec_fn=lambda: os.sched_setaffinity(0, set(cpus)))
+        assert r.returncode == 0 and "stage ok" in r.stdout, r.stdout + r.stderr[-3000:]
