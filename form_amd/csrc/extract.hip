@@ -36,6 +36,7 @@ constexpr int kRowThreads = 1024;  // 16 waves: the row phases are LDS-latency b
 
 struct ExArgs {
   int R, C, k, S, P, Ppt;
+  int row0;            // k_extract_rows: first row of this launch (piecewise launches over a staged scan)
   int cap_pl, cap_pt;  // per-row slot capacities
   double thr, min2, max2, radius2;
   int min_points;
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(kRowThreads) void k_extract_rows(const float4* __re
                                                               uint32_t* __restrict__ pt_slots,
                                                               uint32_t* __restrict__ row_counts) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int C = a.C, r = blockIdx.x, tid = threadIdx.x, k = KC > 0 ? KC : a.k;
+  const int C = a.C, r = a.row0 + blockIdx.x, tid = threadIdx.x, k = KC > 0 ? KC : a.k;
   float4* pts = reinterpret_cast<float4*>(smem);
   uint64_t* keys = reinterpret_cast<uint64_t*>(pts + C);  // accepted planar keys (curv bits, column)
   int* list = reinterpret_cast<int*>(keys);                // point phase: compacted columns (aliases keys)
@@ -1412,8 +1413,9 @@ void unpack_xyz(fmx_ctx* c, const float* d_packed, float4* d_out, size_t n, hipS
   FMX_HIP(hipGetLastError());
 }
 
-ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
-                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq) {
+// The arguments and scratch of one extraction (every buffer ensured before any launch:
+// a regrowth's hipFree synchronizes the device).
+static ExArgs extract_setup(fmx_ctx* c, int R, int C) {
   const auto& E = c->P.extraction;
   ExArgs a;
   a.R = R;
@@ -1422,6 +1424,7 @@ ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStrea
   a.S = (int)E.num_sectors;
   a.P = (int)E.planar_feats_per_sector;
   a.Ppt = (int)E.point_feats_per_sector;
+  a.row0 = 0;
   a.cap_pl = a.S * (a.P + 1);
   a.cap_pt = a.k > 0 ? C / a.k + 1 : C;
   a.thr = E.planar_threshold;
@@ -1440,7 +1443,6 @@ ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStrea
   c->nrm_slots.ensure((size_t)R * a.cap_pl);
   c->rows = R;
   c->cols = C;
-  const size_t lds = (size_t)C * (16 + 4 + 4 + 4 + 4);
   if (!c->lds_attr_set) {
     const int lmax = 4096 * (16 + 4 + 4 + 4 + 4);
     const void* kern[4] = {reinterpret_cast<const void*>(k_extract_rows<5, false>),
@@ -1450,6 +1452,15 @@ ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStrea
     for (const void* kf : kern) FMX_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, lmax));
     c->lds_attr_set = true;
   }
+  return a;
+}
+
+// k_extract_rows over rows [r0, r1) (one 1024-thread block per line).
+static void launch_rows(fmx_ctx* c, const float4* d_scan, ExArgs a, int r0, int r1, hipStream_t st) {
+  if (r1 <= r0) return;
+  const int R = a.R, C = a.C;
+  const size_t N = (size_t)R * C;
+  const size_t lds = (size_t)C * (16 + 4 + 4 + 4 + 4);
   // sector-parallel selection when every sector sorts in one wave's registers (<= 512
   // columns), there is a wave per sector, sectors are longer than the suppression
   // reach, and the kept lists fit the dead point area of LDS
@@ -1457,25 +1468,39 @@ ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStrea
   const size_t nwd = (size_t)(C + 63) / 64 + 1;
   const bool par = pps <= 512 && a.S <= 16 && pps >= 2 * a.k &&
                    8 * (size_t)C + 8 * nwd + 2 * 4 * (size_t)a.S * (a.P + 1) <= 16 * (size_t)C;
-  {
-    ProfScope ps(c->prof, PROF_EXTRACT_ROWS, 16.0 * N + N, st);
-    if (par) {
-      if (a.k == 5)
-        hipLaunchKernelGGL((k_extract_rows<5, true>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
-                           c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
-      else
-        hipLaunchKernelGGL((k_extract_rows<0, true>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
-                           c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
-    } else {
-      if (a.k == 5)
-        hipLaunchKernelGGL((k_extract_rows<5, false>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a,
-                           c->planar_mask.p, c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
-      else
-        hipLaunchKernelGGL((k_extract_rows<0, false>), dim3(R), dim3(kRowThreads), lds, st, d_scan, a,
-                           c->planar_mask.p, c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
-    }
+  a.row0 = r0;
+  const dim3 grid(r1 - r0);
+  ProfScope ps(c->prof, PROF_EXTRACT_ROWS, (16.0 * N + N) * (r1 - r0) / R, st);
+  if (par) {
+    if (a.k == 5)
+      hipLaunchKernelGGL((k_extract_rows<5, true>), grid, dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+    else
+      hipLaunchKernelGGL((k_extract_rows<0, true>), grid, dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+  } else {
+    if (a.k == 5)
+      hipLaunchKernelGGL((k_extract_rows<5, false>), grid, dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
+    else
+      hipLaunchKernelGGL((k_extract_rows<0, false>), grid, dim3(kRowThreads), lds, st, d_scan, a, c->planar_mask.p,
+                         c->sel_slots.p, c->pt_slots.p, c->row_counts.p);
   }
   FMX_HIP(hipGetLastError());
+}
+
+void extract_rows(fmx_ctx* c, const float4* d_scan, int R, int C, int r0, int r1, hipStream_t st) {
+  launch_rows(c, d_scan, extract_setup(c, R, C), r0, r1, st);
+}
+
+// rows_done: rows [0, rows_done) were already extracted by earlier extract_rows launches
+// on the same stream (a staged host scan: each line as soon as its bytes have landed)
+ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
+                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq, int rows_done) {
+  ExArgs a = extract_setup(c, R, C);
+  launch_rows(c, d_scan, a, rows_done, R, st);
+  a.row0 = 0;
+  const size_t N = (size_t)R * C;
   const int nslots = R * a.cap_pl;
   const int nblk = (C + 63) / 64;
   // k_normals: one workgroup per line, rows r-1..r+1 in LDS (160 KB per CU, minus
@@ -1565,10 +1590,11 @@ void extract_collect(fmx_ctx* c, const ExLaunch& L, fmx_feature_counts* out) {
 }
 
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
-                 const std::function<void()>& while_waiting) {
+                 const std::function<void()>& while_waiting, int rows_done) {
   c->h_u32.ensure(8);
   const uint32_t seq = next_flag(c);
-  const ExLaunch L = extract_launch(c, d_scan, R, C, c->stream, c->h_u32.p, c->h_u32.d, c->h_flag.p, c->h_flag.d, seq);
+  const ExLaunch L =
+      extract_launch(c, d_scan, R, C, c->stream, c->h_u32.p, c->h_u32.d, c->h_flag.p, c->h_flag.d, seq, rows_done);
   if (while_waiting) while_waiting();
   extract_collect(c, L, out);
 }

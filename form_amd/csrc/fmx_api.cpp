@@ -453,11 +453,19 @@ bool host_pinned(const void* p, size_t bytes) {
   }
   return true;
 }
+// FMX_STAGE_ROWS=0 (A/B diagnostic): extract a staged host scan only once all of it has landed
+bool stage_rows() {
+  static const bool v = env_int("FMX_STAGE_ROWS", 1) != 0;
+  return v;
+}
 // A host scan for the sequential path, into c->scan on the context stream: a pinned one
 // is DMA'd directly; a pageable one is staged by the helpers and this thread, each
-// completed quarter DMA'd right away.
-const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n) {
+// completed quarter DMA'd right away, unpacked, and its complete lines (R x C scan) handed
+// to k_extract_rows while the next quarter is still being staged.  *rows_done = the lines
+// whose extraction is already queued.
+const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n, int R, int C, int* rows_done) {
   const size_t bytes = n * sizeof(float4);
+  *rows_done = 0;
   c->scan.ensure(n);
   if (host_pageable() || host_pinned(xyzw, bytes)) {
     FMX_HIP(hipMemcpyAsync(c->scan.p, xyzw, bytes, hipMemcpyHostToDevice, c->stream));
@@ -469,25 +477,37 @@ const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n) {
   StageReq& r = c->st_seq;
   stage_submit(c, r, xyzw, c->pin_seq, bytes);
   // packed: the DMA lands in scan3 and k_unpack_xyz writes c->scan; offsets scale by 3/4
-  if (r.pack3) c->scan3.ensure(3 * n);
-  uint8_t* dev = r.pack3 ? reinterpret_cast<uint8_t*>(c->scan3.p) : reinterpret_cast<uint8_t*>(c->scan.p);
-  auto dsz = [&](size_t x) { return r.pack3 ? x / 16 * 12 : x; };
+  const bool packed = r.pack3;
+  if (packed) c->scan3.ensure(3 * n);
+  const bool rows = stage_rows();
+  if (rows) extract_rows(c, c->scan.p, R, C, 0, 0, c->stream);  // every scratch buffer before the first DMA
+  uint8_t* dev = packed ? reinterpret_cast<uint8_t*>(c->scan3.p) : reinterpret_cast<uint8_t*>(c->scan.p);
+  auto dsz = [&](size_t x) { return packed ? x / 16 * 12 : x; };
   const uint32_t step = std::max<uint32_t>(1, (r.nchunks + stage_dmas() - 1) / stage_dmas());
   uint32_t issued = 0;
+  size_t pts = 0;  // points on the device (unpacked)
   while (issued < r.nchunks) {
     uint32_t ready = issued;
     while (ready < r.nchunks && r.chunk_done(ready)) ++ready;
     if (ready - issued >= step || ready == r.nchunks) {
-      const size_t a = dsz((size_t)issued * r.chunk), b = dsz(std::min(bytes, (size_t)ready * r.chunk));
+      const size_t s0 = (size_t)issued * r.chunk, s1 = std::min(bytes, (size_t)ready * r.chunk);
+      const size_t a = dsz(s0), b = dsz(s1);
       FMX_HIP(hipMemcpyAsync(dev + a, c->pin_seq + a, b - a, hipMemcpyHostToDevice, c->stream));
       issued = ready;
+      if (rows) {
+        const size_t p1 = s1 / sizeof(float4);
+        if (packed) unpack_xyz(c, c->scan3.p + 3 * pts, c->scan.p + pts, p1 - pts, c->stream);
+        pts = p1;
+        const int done = (int)(pts / (size_t)C);
+        extract_rows(c, c->scan.p, R, C, *rows_done, done, c->stream);
+        *rows_done = done;
+      }
       continue;
     }
     if (!r.work_one()) std::this_thread::yield();  // help; then wait for the helpers' chunks
   }
-  const bool packed = r.pack3;
   c->stager.retire(&r);
-  if (packed) unpack_xyz(c, c->scan3.p, c->scan.p, n, c->stream);
+  if (packed && !rows) unpack_xyz(c, c->scan3.p, c->scan.p, n, c->stream);
   return c->scan.p;
 }
 
@@ -504,12 +524,13 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
     throw StatusError(FMX_E_INVAL, "unsupported scan geometry (columns must be <= 4096)");
   pf_drop(c);  // a queued extraction shares the scratch buffers
   const float4* d;
+  int rows_done = 0;
   if (on_dev) {
     d = reinterpret_cast<const float4*>(xyzw);
   } else {
-    d = stage_host_scan(c, xyzw, n);
+    d = stage_host_scan(c, xyzw, n, (int)R, (int)C, &rows_done);
   }
-  run_extract(c, d, (int)R, (int)C, out, while_waiting);
+  run_extract(c, d, (int)R, (int)C, out, while_waiting, rows_done);
   c->q_scan = scan;
   c->have_queries = true;
   ++c->warm_gen;  // a new query set: no warm start from an earlier match
@@ -574,7 +595,7 @@ void pf_launch(fmx_ctx* c, bool force = true) {
   try {
     const uint32_t seq = ++c->pf_seq;
     c->pf_L = extract_launch(c, d, (int)E.num_rows, (int)E.num_columns, c->side2, c->h_pf.p, c->h_pf.d, c->h_pf.p + 4,
-                             c->h_pf.d + 4, seq);
+                             c->h_pf.d + 4, seq, 0);
   } catch (...) {
     swap_query_set(c);
     throw;

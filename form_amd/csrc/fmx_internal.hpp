@@ -762,10 +762,13 @@ namespace gl { FMX_VM_DECLS }
 int prof_ring_slot(fmx_ctx* c);
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
-                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq);
+                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq, int rows_done = 0);
+// k_extract_rows over lines [r0, r1) of an R x C scan (r0 == r1: only ensures the scratch
+// buffers); extract_launch(..., rows_done = r1) then queues the rest of the extraction
+void extract_rows(fmx_ctx* c, const float4* d_scan, int R, int C, int r0, int r1, hipStream_t st);
 void extract_collect(fmx_ctx* c, const ExLaunch& L, fmx_feature_counts* out);
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
-                 const std::function<void()>& while_waiting = nullptr);
+                 const std::function<void()>& while_waiting = nullptr, int rows_done = 0);
 // packed x, y, z (a staged host scan) -> float4 points with pad 0, on stream st
 void unpack_xyz(fmx_ctx* c, const float* d_packed, float4* d_out, size_t n, hipStream_t st);
 // st: stream to build on (default the context stream; register_scan uses the side
