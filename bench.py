@@ -430,6 +430,26 @@ def c5_setup(a, rank, world, local):
     return ctx, pos4, nrm4, n_map, w
 
 
+def c5_build_line(a, ctx, n_map, w, reps=3):
+    """The C5 map build (a9, map.tpp:128-146: the reference's serial to_voxel_map) of the
+    50M-record terrain map, `reps` rebuilds with HIP events (profiled: the four build
+    kernels as one class), with its roofline against §8(d)'s B_build."""
+    I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
+    ctx.profile(True)
+    ctx.profile_reset()
+    for _ in range(reps):
+        ctx.map_build([0], I34[None], w)
+    ctx.sync()
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    d = prof.get("map_build")
+    if not d or not d["launches"]:
+        return None
+    return {"records": n_map, "builds": int(d["launches"]), "ms_per_build": round(d["ms"] / d["launches"], 4),
+            "records_per_s": round(n_map * d["launches"] / (d["ms"] * 1e-3), 1),
+            "roofline": roofline(a, "map_build", d, "c5_build")}
+
+
 C5_DISTS = {
     # a 240 m scan of the terrain (drawn with replacement, grid order): the round-1/2 line
     "local": "2M samples (with replacement) of the terrain within 240 m of the sensor, grid order",
@@ -547,6 +567,8 @@ def run_c5(a, rank, world, local, steps, warmup, profile=True, dists=("local", "
     work per step is fixed.  Returns {dist: line} on rank 0."""
     ctx, pos4, nrm4, n_map, w = c5_setup(a, rank, world, local)
     out = {}
+    if profile and rank == 0:
+        out["map_build"] = c5_build_line(a, ctx, n_map, w)
     for dn in dists:
         q4, n4, Ttrue = c5_queries(a, dn, pos4, nrm4, rank, world)
         ctx.set_queries_device(q4, n4)
@@ -640,10 +662,13 @@ def sub_stream_line(a, wl, rank, world, local, single, pipe):
 # did, from the kernel's own probe / candidate counters.
 ALG_BYTES_MODEL = {
     "match": "per query 16 B read + 45 B result (+32 B planar normal) + warm state 20 B written, 52 B read; "
-             "64 B per brick probe, 32 B per candidate record tested; a query the warm certificate settles "
-             "probes and tests nothing (round 4: 87-92 % of warm queries)",
-    "match_linearize": "per query 16 B read (+32 B planar normal of the winner); 64 B per brick probe, 32 B per "
-                       "candidate record; 256 B of block partials per block",
+             "64 B per brick probe, 32 B per candidate record tested (64 B when the map interleaves normals); "
+             "a query the warm certificate settles probes and tests nothing (round 4: 87-92 % of warm queries)",
+    "match_linearize": "per query 16 B read (+32 B planar normal of the winner unless the map interleaves it "
+                       "with the position); 64 B per brick probe; per candidate record its line: 32 B, or 64 B "
+                       "interleaved (>= FMX_INTERLEAVE_MIN records: C5); 256 B of block partials per block",
+    "map_build": "SURVEY.md §8(d) B_build = 2 (32 M_pl + 16 M_pt) + 16 S: the local records read and the "
+                 "world-sorted records written at the local size, 16 B per hash slot, S = 2 M (load 0.5)",
     "window": "72 B per plane row (p_i, n_i, p_j as fp64) + 48 B per point pair + 92 doubles of G per pair",
     "moments": "72 B per plane row (p_i, n_i, p_j as fp64) + 48 B per point pair + 2 x 136 doubles of moments "
                "per pair",
@@ -724,6 +749,8 @@ def main():
             out = res[dists[0]]
             if len(dists) > 1:
                 out["wholemap"] = res["wholemap"]
+            if res.get("map_build"):
+                out["map_build"] = res["map_build"]
             if a.rehearse_ranks:
                 out = {"rehearsal": True, "value": None, "ranks": world, "sharded_c5": {"pose": out["pose"]}}
             print(json.dumps(out), flush=True)
@@ -825,8 +852,10 @@ def main():
     del scans
     for wl in [w_.strip() for w_ in a.sub_workloads.split(",") if w_.strip() and w_.strip() != a.workload]:
         subs[wl] = sub_stream_line(a, wl, rank, world, local, single, pipe)
+    c5_build = None
     if rank == 0 and c5 is not None:
         c5_whole = c5["wholemap"]
+        c5_build = c5.get("map_build")
         c5 = c5["local"]
     if rank != 0:
         if world > 1:
@@ -921,6 +950,8 @@ def main():
     if c5 is not None:
         out["sharded_c5"] = c5
         out["sharded_c5_wholemap"] = c5_whole
+        if c5_build:
+            out["c5_map_build"] = c5_build
     cp = os.path.join(ROOT, "profiles", f"critical_path_{a.workload}.json")
     if os.path.exists(cp):  # a committed rocprofv3-trace figure, not measured by this run
         with open(cp) as f:

@@ -109,8 +109,9 @@ static void sync_all(fmx_ctx* c) {
   if (c->side2) FMX_HIP(hipStreamSynchronize(c->side2));
 }
 // A match launch's algorithmic bytes: the per-launch part known at
-// launch time + 64 B per hash probe and 32 B per candidate record, the counts the launch
-// itself published to its ring slot.
+// launch time + 64 B per hash probe and per candidate record its line (32 B: position +
+// tag; 64 B when the map interleaves the normal with it, which the winner's normal then
+// costs nothing more), the counts the launch itself published to its ring slot.
 static void prof_collect(fmx_ctx* c) {
   Prof& pr = c->prof;
   if (pr.pending.empty()) return;
@@ -122,7 +123,7 @@ static void prof_collect(fmx_ctx* c) {
     if (e.ring >= 0) {
       const uint32_t* w = pr.wring.p + 4 * (size_t)e.ring;
       const double probes = w[0], cands = w[1];
-      bytes += 64.0 * probes + 32.0 * cands;
+      bytes += 64.0 * probes + (c->map.rsh == 6 ? 64.0 : 32.0) * cands;
       double* m = pr.mwork[e.warm ? 1 : 0];
       m[0] += 1;
       m[1] += e.queries;
@@ -1707,7 +1708,7 @@ void fmx_destroy(fmx_ctx* c) {
   }
   {
     auto& M = c->map;
-    M.table.release(); M.bcnt.release(); M.state.release(); M.rinfo.release(); M.claim.release(); M.dense.release();
+    M.table.release(); M.ccnt.release(); M.state.release(); M.rinfo.release(); M.claim.release(); M.dense.release();
     M.pos.release(); M.nrm.release();
   }
   c->h_mapposes.release(); c->map_blob.release(); c->h_mapinfo.release();

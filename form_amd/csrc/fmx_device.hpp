@@ -291,10 +291,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {  // splitmix64 finalizer
 // [beg[c], beg[c + 1]); bit c of `dense` marks a cell stored with a sub-cell header
 // (voxelmap.hip, dense cells).
 struct alignas(64) Brick {
-  unsigned long long key;  // epoch | pack_key of the brick coordinates
+  unsigned long long key;  // epoch | pack_key of the brick coordinates (bit 63: claim in progress)
   uint32_t beg[9];
   uint32_t dense;
-  uint32_t pad[4];
+  uint32_t slot;  // build only: the brick's slot in the build's claim list (cell counts, then begins)
+  uint32_t pad[3];
 };
 static_assert(sizeof(Brick) == 64, "brick = 64 B");
 __device__ __forceinline__ uint64_t brick_key(int x, int y, int z, uint32_t epoch) {

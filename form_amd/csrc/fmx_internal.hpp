@@ -188,7 +188,7 @@ struct Pool {
 // headers of dense cells), grouped by cell; normals for planar records only.
 struct VoxMap {
   DBuf<uint4> table;            // fmx::Brick (epoch-tagged keys: no clear between builds)
-  DBuf<uint32_t> bcnt;          // per brick cell: record count (zero between builds)
+  DBuf<uint32_t> ccnt;          // per claim slot: 8 cell counts, then the cells' first record slots
   DBuf<uint4> state;            // two alternating BuildState (voxelmap.hip)
   uint32_t epoch = 0;           // build epoch of the current map (1..63)
   uint64_t cap[2] = {0, 0};     // powers of two

@@ -92,21 +92,28 @@ __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
 // own table section (point bricks at off1) and segment list.
 //
 // The build (map.tpp:128-146 + push_back :41-52), four launches, no table clear:
-//   k_map_insert  one lane per record: world transform, voxel key, claim or find the
-//                 brick (epoch-tagged CAS, linear probing; a claim appends the brick to
-//                 the claim list), count the record into its cell (the returned count
+//   k_map_insert  one lane per record: world transform, voxel key; the first lane of the
+//                 wave's records of one brick finds or claims the brick (epoch-tagged CAS,
+//                 linear probing) and reads its claim slot; then one count atomic per
+//                 (wave, cell) group on the claim slot's cell counts (the returned count
 //                 is the record's rank in the cell)
-//   k_map_alloc   one lane per claimed brick: the cells' record ranges (wave scan +
-//                 one atomic per wave and type), dense cells get a sub-cell header;
-//                 the counts are reset for the next build
-//   k_map_scatter one lane per record: the record at its cell's first slot + rank
+//   k_map_alloc   one lane per claim slot: the cells' record ranges (block scan + one
+//                 atomic per block and type) into the brick and, with the header slots of
+//                 a dense cell added, over the slot's counts (the scatter's bases)
+//   k_map_scatter one lane per record: the record at its cell's base + rank
 //   k_map_dense   one block per dense cell (> kDenseMin records): counting sort of
 //                 its records into 4 x 4 x 4 sub-cells, header = the sub-cell ends
+// Claim slots are reserved per wave for every probing lane (one atomic per wave) and
+// listed in insertion order: consecutive records are mostly neighbours, so the counts,
+// the ranges and the scatter's bases are read and written near one another instead of
+// at the table's hashed positions — the table is touched once per probe and once per
+// claimed brick (20.6 GB per 50M-record build with per-bucket counts, the
+// counts' random lines and the scatter's brick reads were ~60 % of it).
 // The order of records inside a cell (and of the cells' ranges) follows the atomics,
 // so it varies from build to build; nothing observable depends on it: k_match's
 // argmin is over the total order (d^2, reference shift rank, build order).
 struct BuildState {  // per build, two alternating copies (the other is cleared)
-  uint32_t nclaim;   // claimed bricks
+  uint32_t nclaim;   // claim slots reserved (probing lanes)
   uint32_t cur[2];   // record slot cursors (planar from 0, point from BuildArgs::pt_base)
   uint32_t err;      // range error: a record outside the packable key range
   uint32_t ndense;   // dense cells
@@ -121,6 +128,8 @@ constexpr int kDenseRecs = 8;             // records per thread: dense cells up 
 constexpr uint32_t kUnsorted = 0xFFFFFFFFu;  // header[0] of a dense cell too large to sort
 constexpr uint32_t kDenseGrid = 1024;     // k_map_dense blocks (each loops over the dense list)
 constexpr int kAllocThreads = 1024;       // k_map_alloc: one cursor atomic per block and type
+constexpr unsigned long long kClaimLock = 1ull << 63;  // a bucket's key while its claimer fills slot / counts
+constexpr uint32_t kNoBrick = 0xFFFFFFFFu;  // a claim slot whose lane found its brick already claimed
 
 struct BuildArgs {
   const float4* pool_pos[2];
@@ -132,12 +141,12 @@ struct BuildArgs {
   uint32_t pt_base;  // first point slot: planar records + the most header slots they can need
   double w;
   Brick* bricks;
-  uint32_t* bcnt;   // [brick][8] record counts, zero between builds
+  uint32_t* ccnt;   // [claim slot][8]: cell record counts (insert), then cell bases (alloc)
   uint64_t mask[2];
   uint64_t off1;  // first point brick
   uint32_t epoch;
-  uint2* rinfo;     // per record: cell (brick * 8 + c) or ~0, rank in the cell
-  uint32_t* claim;  // claimed bricks
+  uint2* rinfo;     // per record: claim slot * 8 + cell or ~0, rank in the cell
+  uint32_t* claim;  // per claim slot: the claimed brick, or kNoBrick
   uint32_t* dense;  // dense cells
   BuildState* st;
   BuildState* st_next;
@@ -232,68 +241,83 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   int bl;
   uint32_t brank, bsize;
   wave_group(valid, key, bl, brank, bsize);
+  const bool prober = valid && brank == 0;
+  // a claim slot per probing lane, reserved before the probe (one atomic per wave): a
+  // claimer fills its brick's slot field before it releases the bucket, so that no lane
+  // ever waits on a claimer that is itself waiting (lanes that find their brick claimed
+  // leave their slot empty)
+  const uint64_t pm = __ballot(prober);
+  uint32_t ps = 0;
+  {
+    const int leader = __ffsll((unsigned long long)pm) - 1;
+    if (lane_id() == leader) ps = atomicAdd(&a.st->nclaim, (uint32_t)__popcll(pm));
+    ps = (uint32_t)__shfl((int)ps, leader < 0 ? 0 : leader, 64) + (uint32_t)__popcll(pm & lanemask_lt());
+  }
   const unsigned long long bkey = brick_key(cx, cy, cz, a.epoch);
   const uint64_t boff = t == 0 ? 0 : a.off1;
   Brick* bricks = a.bricks + boff;
   const uint64_t mask = a.mask[t];
   uint64_t h = mix64(bkey) & mask;
-  bool claimed = false;
-  const bool prober = valid && brank == 0;
+  uint32_t slot = 0;
   if (prober) {
     for (;;) {  // more buckets than records: a bucket of another epoch always exists
-      const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur == bkey) break;
-      if (key_epoch(cur) != a.epoch) {  // empty for this build: claim it
-        const unsigned long long prev = atomicCAS(&bricks[h].key, cur, bkey);
-        if (prev == cur) {
-          claimed = true;
+      const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long ck = cur & ~kClaimLock;
+      if (ck == bkey) {
+        if (cur & kClaimLock) {  // another wave's claimer is filling it in (a few stores)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        slot = __hip_atomic_load(&bricks[h].slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.claim[ps] = kNoBrick;
+        break;
+      }
+      if (key_epoch(ck) != a.epoch) {  // empty for this build: claim it
+        const unsigned long long prev = atomicCAS(&bricks[h].key, cur, bkey | kClaimLock);
+        if (prev == cur) {  // claimed: the slot and its zero counts, then the key (release)
+          slot = ps;
+          bricks[h].slot = ps;
+          uint4* cc = reinterpret_cast<uint4*>(a.ccnt + (size_t)ps * 8);
+          cc[0] = make_uint4(0, 0, 0, 0);
+          cc[1] = make_uint4(0, 0, 0, 0);
+          a.claim[ps] = (uint32_t)(boff + h);
+          __hip_atomic_store(&bricks[h].key, bkey, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
-        if (prev == bkey) break;
-        if (key_epoch(prev) != a.epoch) continue;  // (not reached: only this epoch's keys are written)
+        continue;  // lost the race: look at the bucket again
       }
       h = (h + 1) & mask;
     }
   }
-  h = (uint64_t)__shfl((unsigned long long)h, bl < 0 ? 0 : bl, 64);  // the group's bucket
-  // claimed bricks onto the claim list: one atomic per wave (a single counter takes
-  // every claim of the build: ~1.2e7 at C5)
-  const uint64_t cm = __ballot(claimed);
-  if (cm) {
-    const int leader = __ffsll((unsigned long long)cm) - 1;
-    uint32_t cb = 0;
-    if (lane_id() == leader) cb = atomicAdd(&a.st->nclaim, (uint32_t)__popcll(cm));
-    cb = __shfl(cb, leader, 64);
-    if (claimed) a.claim[cb + (uint32_t)__popcll(cm & lanemask_lt())] = (uint32_t)(boff + h);
-  }
+  slot = (uint32_t)__shfl((int)slot, bl < 0 ? 0 : bl, 64);  // the group's claim slot
   // rank in the cell: one count atomic per (wave, cell) group
-  const uint32_t cell = (uint32_t)((boff + h) * 8 + brick_cell(cx, cy, cz));
+  const uint32_t cell = slot * 8 + brick_cell(cx, cy, cz);
   int cl;
   uint32_t crank, csize;
   wave_group(valid, cell, cl, crank, csize);
   uint32_t cbase = 0;
-  if (valid && crank == 0) cbase = atomicAdd(a.bcnt + cell, csize);
+  if (valid && crank == 0) cbase = atomicAdd(a.ccnt + cell, csize);
   cbase = (uint32_t)__shfl((int)cbase, cl < 0 ? 0 : cl, 64);
   if (valid) a.rinfo[rec] = make_uint2(cell, cbase + crank);
 }
 
-// One lane per claimed brick: record ranges of its 8 cells, allocated per type from the
-// state's cursors (one atomic per wave); dense cells reserve kHdr header slots and are
-// listed for k_map_dense.  The grid is sized for the worst case (every record claiming a
-// brick); lanes past nclaim only take part in the wave scans.
+// One lane per claim slot: record ranges of its brick's 8 cells, allocated per type from
+// the state's cursors (one atomic per block and type), into the brick (k_match) and, as
+// the scatter's per-cell bases (past a dense cell's header), over the slot's counts;
+// dense cells reserve kHdr header slots and are listed for k_map_dense.  The grid is
+// sized for the worst case (every record probing); lanes past nclaim and empty slots
+// only take part in the scans.
 __global__ __launch_bounds__(kAllocThreads) void k_map_alloc(BuildArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ncl = __hip_atomic_load(&a.st->nclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x * blockDim.x >= ncl) return;  // whole block past the list
-  const bool valid = i < ncl;
-  const uint32_t gb = valid ? a.claim[i] : 0u;
+  const uint32_t gb = i < ncl ? a.claim[i] : kNoBrick;
+  const bool valid = gb != kNoBrick;
   const int t = gb >= a.off1 ? 1 : 0;
   uint32_t sz[8], tot = 0, dmask = 0;
+  uint4* cp = reinterpret_cast<uint4*>(a.ccnt + (size_t)i * 8);
   if (valid) {
-    uint4* cp = reinterpret_cast<uint4*>(a.bcnt + (size_t)gb * 8);
     const uint4 c0 = cp[0], c1 = cp[1];
-    cp[0] = make_uint4(0, 0, 0, 0);  // zero between builds
-    cp[1] = make_uint4(0, 0, 0, 0);
     const uint32_t c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -330,14 +354,17 @@ __global__ __launch_bounds__(kAllocThreads) void k_map_alloc(BuildArgs a) {
   }
   if (!valid) return;
   Brick& B = a.bricks[gb];
-  uint32_t run = base;
+  uint32_t run = base, first[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     B.beg[k] = run;
+    first[k] = run + (((dmask >> k) & 1) ? kHdr : 0);
     run += sz[k];
   }
   B.beg[8] = run;
   B.dense = dmask;
+  cp[0] = make_uint4(first[0], first[1], first[2], first[3]);
+  cp[1] = make_uint4(first[4], first[5], first[6], first[7]);
   if (dmask) {
     const uint32_t o = atomicAdd(&a.st->ndense, (uint32_t)__popc(dmask));
     uint32_t j = 0;
@@ -361,9 +388,7 @@ __global__ __launch_bounds__(256) void k_map_scatter(BuildArgs a) {
   if (rec >= a.n) return;
   const uint2 ri = a.rinfo[rec];
   if (ri.x == 0xFFFFFFFFu) return;
-  const Brick& B = a.bricks[ri.x >> 3];
-  const uint32_t c = ri.x & 7;
-  const uint32_t o = B.beg[c] + (((B.dense >> c) & 1) ? kHdr : 0) + ri.y;
+  const uint32_t o = a.ccnt[ri.x] + ri.y;  // the cell's first record slot (alloc) + rank
   const RecW R = rec_world(a, rec, true);
   rec_at(a.pos, o, a.rsh) = make_double4(R.p[0], R.p[1], R.p[2], rec_tag(rec, R.seg));
   if (R.t == 0) rec_at(a.nrm, o, a.rsh) = make_double4(R.n[0], R.n[1], R.n[2], 0.0);
@@ -2309,13 +2334,12 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     M.cap[t] = next_pow2(std::max<uint64_t>((uint64_t)nrec[t] + 1, 256));
   }
   const uint64_t slots = M.cap[0] + M.cap[1];  // buckets
-  const bool grown = 4 * slots > M.table.cap || 8 * slots > M.bcnt.cap || M.state.cap < 4;
+  const bool grown = 4 * slots > M.table.cap || M.state.cap < 4;
   M.table.ensure(4 * slots);
-  M.bcnt.ensure(8 * slots);
+  M.ccnt.ensure(8 * ((size_t)n + 1));  // claim slots <= probing lanes <= records
   M.state.ensure(4);  // two BuildState of 32 B
   if (grown || M.epoch >= kEpochMax) {  // fresh storage or epoch wrap: clear everything once
     FMX_HIP(hipMemsetAsync(M.table.p, 0, M.table.cap * sizeof(uint4), st));
-    FMX_HIP(hipMemsetAsync(M.bcnt.p, 0, M.bcnt.cap * sizeof(uint32_t), st));
     FMX_HIP(hipMemsetAsync(M.state.p, 0, M.state.cap * sizeof(uint4), st));
     M.epoch = 0;
   }
@@ -2340,11 +2364,13 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
     M.nrm.ensure((size_t)pt_base + 1);
     M.nrm_p = M.nrm.p;
   }
-  // algorithmic bytes: read local records (16 B pos + 16 B planar normal, twice: insert
-  // and scatter recompute the transform) + write world records (32 B + 32 B planar) + the
-  // 64-B brick of each record's cell (claim + count, then its range) + rank word
-  const double bytes = 2.0 * (32.0 * nrec[0] + 16.0 * nrec[1]) + 2.0 * 32.0 * nrec[0] + 32.0 * nrec[1] +
-                       2.0 * 64.0 * n / 8.0 + 16.0 * n;
+  // algorithmic bytes, SURVEY.md §8(d) B_build = 2 (32 M_pl + 16 M_pt) + 16 S: read the
+  // local records and write the world-sorted ones (32 B per planar record: position +
+  // normal as read, 16 B per point record; the same again written), + 16 B per hash slot
+  // with S = 2 M slots (load 0.5).  The build as written moves more: insert and scatter
+  // both read the local records, the world records are fp64 (64 / 32 B), the table is
+  // touched per probe and per claim — DESIGN.md §Map build compares it with the PMC bytes.
+  const double bytes = 2.0 * (32.0 * nrec[0] + 16.0 * nrec[1]) + 16.0 * 2.0 * n;
   ProfScope ps(c->prof, PROF_MAP_BUILD, bytes, st);
   HostScope* hs_l = new HostScope(7);
   BuildArgs ba;
@@ -2360,7 +2386,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   ba.pt_base = pt_base;
   ba.w = c->cell_w;
   ba.bricks = reinterpret_cast<Brick*>(M.table.p);
-  ba.bcnt = M.bcnt.p;
+  ba.ccnt = M.ccnt.p;
   ba.mask[0] = M.cap[0] - 1;
   ba.mask[1] = M.cap[1] - 1;
   ba.off1 = M.cap[0];
@@ -2538,8 +2564,9 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   // result write (pair 4 + d2 8 + p_i 32 [+ n_i 32] + flag 1) + the warm state: NN
   // record index and own-cell entry written (4 + 16 B), and on a warm launch also read,
   // with the warm record itself (4 + 16 + 32 B); + one 64-B line per hash probe (a brick;
-  // a dense cell's 256-B header counts as 4 probes) + 32 B per candidate record tested
-  // (double4: position + build order/segment) — those two from the counts THIS launch
+  // a dense cell's 256-B header counts as 4 probes) + per candidate record tested its
+  // line (32 B double4: position + build order/segment; 64 B when interleaved with the
+  // normal) — those two from the counts THIS launch
   // publishes to its profiler slot (prof_collect adds them)
   const double bytes = 16.0 * nq + 45.0 * nq + 32.0 * c->n_qpl + (a.rec ? 20.0 * nq : 0.0) + (a.warm ? 52.0 * nq : 0.0);
   const int pslot = nb > 0 ? prof_ring_slot(c) : -1;
@@ -2675,11 +2702,12 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   const FusedArgs fz{c->map_poses_p, 1.0 / sigma, c->bpart.p, c->bpart.p + (size_t)nb * kFzLd, c->fz_tickets.p,
                      c->ticket.p, dst, flag, seq};
   const SortOut so{};
-  // bytes: query read (16 B) + the accepted match's normal (32 B, planar) + 32 * 8 B
-  // block partials + 64 B per probe and 32 B per candidate (this launch's own counts,
-  // added by prof_collect from its profiler slot)
+  // bytes: query read (16 B) + the accepted match's normal (32 B, planar; in the winner's
+  // own line when records are interleaved) + 32 * 8 B block partials + 64 B per probe and
+  // per candidate the bytes of its record line (prof_collect: this launch's own counts
+  // from its profiler slot)
   const double nq = (double)c->n_qpl + c->n_qpt;
-  const double bytes = 16.0 * nq + 32.0 * c->n_qpl + 256.0 * nb;
+  const double bytes = 16.0 * nq + (c->map.rsh == 6 ? 0.0 : 32.0 * c->n_qpl) + 256.0 * nb;
   const int pslot = prof_ring_slot(c);
   ensure_zeroed(c->mprof, 2, st);
   a.prof_acc = c->mprof.p;

@@ -2,7 +2,7 @@
 # C5, per query distribution (local = the 240 m scan, wholemap = 2M distinct features
 # over the whole map): rocprofv3 kernel stats, then PMC HBM traffic per kernel (one
 # counter group per run, as MI355X_MICROARCH.md §rocprofv3 prescribes).
-# Outputs: gpurun_out/pmc_c5_<dist>/traffic.json, gpurun_out/c5_<dist>_kernel_stats_fmx.csv
+# Outputs: gpurun_out/pmc_c5_<dist>/traffic.json (+ pmc_c5_local/traffic_build.json), gpurun_out/c5_<dist>_kernel_stats_fmx.csv
 set -o pipefail
 export TMPDIR=/tmp
 RX='k_match|k_linearize|k_map_|k_pair_scatter'
@@ -20,6 +20,8 @@ for dist in local wholemap; do
   done
   W=c5; [ $dist = wholemap ] && W=c5_wholemap  # the workload key bench.py looks up
   python tools/pmc_traffic.py $W $D/traffic.json $D/p1 $D/p2 $D/p3 > /dev/null
+  # the map build's own summary (bench.py's c5_map_build roofline: workload key c5_build)
+  [ $dist = local ] && python tools/pmc_traffic.py c5_build $D/traffic_build.json $D/p1 $D/p2 $D/p3 > /dev/null
   find $D -name "*counter_collection.csv" -delete
   cat gpurun_out/c5_${dist}_kernel_stats_fmx.csv | head -6
   python -c "
