@@ -516,7 +516,7 @@ def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmu
     torch.cuda.synchronize()
     barrier(world)
     t_local = time.perf_counter() - t0
-    prof, work = {}, {"queries": 1.0}
+    prof, work = {}, {}
     nprof = max(steps // 2, 1)
     if profile:
         ctx.profile(True)
@@ -525,7 +525,7 @@ def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmu
             reg(ctx, w)
         ctx.sync()
         prof = ctx.profile_read()
-        work = ctx.match_work()
+        work = ctx.profile_match_work()  # every profiled launch's own counters
         ctx.profile(False)
     t_max = max_over_ranks(t_local, world, local)
     if rank != 0:
@@ -555,8 +555,10 @@ def c5_line(a, ctx, dist_name, Ttrue, n_map, w, rank, world, local, steps, warmu
         name, d = max(prof.items(), key=lambda kv: kv[1]["ms"])
         out["roofline"] = roofline(a, name, d, "c5" if dist_name == "local" else "c5_wholemap")
         out["kernels_ms_per_step"] = {k: round(v["ms"] / nprof, 4) for k, v in prof.items() if v["ms"] > 0}
-        out["match_work_per_query"] = {k: round(v / max(work["queries"], 1), 3) for k, v in work.items()
-                                       if k != "queries"}
+        q = sum(v["queries"] for v in work.values())
+        out["match_work_per_query"] = {k: round(sum(v[k] for v in work.values()) / max(q, 1.0), 3)
+                                       for k in ("probes", "candidates")}
+        out["match_work_split"] = match_work_split({k: v for k, v in work.items() if v["launches"]})
     return out
 
 

@@ -54,7 +54,12 @@
 #ifndef FMX_MATCH_DEPTH_PLAIN
 #define FMX_MATCH_DEPTH_PLAIN 2  // record loads in flight per lane without the dense-cell walk
 #endif
-#define FMX_MATCH_ATTR __attribute__((amdgpu_waves_per_eu(DENSE ? FMX_MATCH_WAVES : FMX_MATCH_WAVES_PLAIN, 8)))
+#ifndef FMX_MATCH_WAVES_FUSED
+#define FMX_MATCH_WAVES_FUSED FMX_MATCH_WAVES_PLAIN  // ... the fused match + linearization (C5)
+#endif
+#define FMX_MATCH_ATTR                                                                                        \
+  __attribute__((amdgpu_waves_per_eu(DENSE ? FMX_MATCH_WAVES : (FUSED ? FMX_MATCH_WAVES_FUSED : FMX_MATCH_WAVES_PLAIN), \
+                                     8)))
 #ifndef FMX_MATCH_DEPTH
 #define FMX_MATCH_DEPTH 4
 #endif
@@ -562,7 +567,8 @@ struct MatchArgs {
   // workgroup takes which query block changes.
   uint32_t* order;
   uint32_t* cost;
-  int order_write;  // the last block writes order[] (nb <= kOrderMaxBlocks)
+  uint32_t* order_out;  // where the last block writes the next order (null: none; nb <= kOrderMaxBlocks) —
+                        // the same buffer as order when that is set: every block has read its entry by then
 };
 constexpr uint32_t kOrderMaxBlocks = 8 * 256;  // the last block's counting sort: <= 8 entries per thread
 
@@ -1608,7 +1614,7 @@ __device__ inline void write_order(const MatchArgs& a, uint32_t nb) {
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const uint32_t b = b0 + u;
-    if (b < nb) a.order[base[cls[u]] + ex[cls[u]]++] = b;
+    if (b < nb) a.order_out[base[cls[u]] + ex[cls[u]]++] = b;
   }
 }
 
@@ -1999,7 +2005,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     }
   }
   match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
-  if (a.order_write) write_order(a, gridDim.x);
+  if (a.order_out) write_order(a, gridDim.x);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2545,7 +2551,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
     c->mord.ensure(nbq + 1);
     a.order = on && c->ord_gen == c->warm_gen && c->ord_nb == nbq ? c->mord.p : nullptr;
     a.cost = on ? c->mcost.p : nullptr;
-    a.order_write = on ? 1 : 0;
+    a.order_out = on ? c->mord.p : nullptr;
     c->ord_gen = on ? c->warm_gen : 0;
     c->ord_nb = nbq;
   }
@@ -2667,7 +2673,7 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
   a.cert_cnt = nullptr;
   a.order = nullptr;
   a.cost = nullptr;
-  a.order_write = 0;
+  a.order_out = nullptr;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;
