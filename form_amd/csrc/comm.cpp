@@ -175,14 +175,14 @@ void comm_wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq, uint32
   const double limit = comm_timeout_s();
   std::string why;
   for (uint32_t spins = 1;; ++spins) {
-    if (*f == seq) {
+    if (flag_reached(*f, seq)) {
       __atomic_thread_fence(__ATOMIC_ACQUIRE);
       return;
     }
     if ((spins & 0x3FFF) != 0) continue;
     const hipError_t e = hipStreamQuery(c->stream);
     if (e == hipSuccess) {
-      if (*f == seq) continue;
+      if (flag_reached(*f, seq)) continue;
       why = "the collective's stream completed without publishing the all-reduced system";
       break;
     }

@@ -701,15 +701,21 @@ inline void stream_wait(fmx_ctx* c) {
 // seq).  Cheaper than a stream round trip: the host resumes as soon as the word
 // lands, before the kernel retires.  A stream that went idle without the word, or a
 // stream error, throws (no silent hang).
+// A completion word holds the sequence number of the LAST kernel that published to it.
+// Its publishers are in one stream in sequence order, so a word at or past seq means the
+// kernel of seq has completed (and its results are in): a result left pending while later
+// kernels published (a speculative window launch across an extraction, say) is waited
+// for with ">=", never "==" (which would spin until the stream drained, then fail).
+inline bool flag_reached(uint32_t f, uint32_t seq) { return (int32_t)(f - seq) >= 0; }
 inline void wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq, hipStream_t st = nullptr) {
   HostScope hs(1);
   ++c->host_waits;
   for (uint32_t spins = 1;; ++spins) {
-    if (*f == seq) break;
+    if (flag_reached(*f, seq)) break;
     if ((spins & 0x3FFF) == 0) {
       const hipError_t e = hipStreamQuery(st ? st : c->stream);
       if (e == hipSuccess) {
-        if (*f == seq) break;
+        if (flag_reached(*f, seq)) break;
         throw HipError("kernel completed without publishing its result flag");
       }
       if (e != hipErrorNotReady) throw HipError(std::string("hipStreamQuery: ") + hipGetErrorString(e));

@@ -243,7 +243,10 @@ fmx_status fmx_register_points(fmx_ctx* ctx, const double pose_init34[12], doubl
  * with RCCL on the context's HIP stream, device buffer to device buffer, before they
  * reach the host, so every rank returns the identical global system.  The reference
  * has no multi-device path; this is the north star's "RCCL all-reduce of the normal
- * equations over xGMI".  RCCL is loaded on first use (FMX_E_RCCL if absent). */
+ * equations over xGMI".  RCCL is loaded on first use (FMX_E_RCCL if absent).  A wait for
+ * an all-reduce is bounded: it polls the stream and ncclCommGetAsyncError and, after
+ * FMX_COMM_TIMEOUT_S seconds (environment, default 60), aborts the communicator and
+ * returns FMX_E_RCCL — the context must then be destroyed. */
 fmx_status fmx_comm_unique_id(uint8_t id[128]);
 fmx_status fmx_comm_init(fmx_ctx* ctx, const uint8_t id[128], int nranks, int rank);
 
