@@ -1192,6 +1192,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       ++spec_builds;
       std::vector<double> mpo(12 * map_scans.size());
       for (size_t k = 0; k < map_scans.size(); ++k) std::memcpy(&mpo[12 * k], x[slot.at(map_scans[k])].m, 12 * sizeof(double));
+      FMX_TRACE_("  spec map (drain %d)\n", (int)e.spec_map);
       if (e.spec_map) FMX_HIP(hipStreamSynchronize(c->side));  // pinned staging reuse (see register_scan)
       FMX_HIP(hipStreamWaitEvent(c->side, c->ev_fork.last(), 0));
       FMX_TRACE_("  spec map build\n");
@@ -1222,8 +1223,9 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     }
     g.lin_begin = nullptr;
     g.lin_end = nullptr;
-    g.lin_pairs = [&](const std::vector<Pose>& x, double* G) {
+    g.lin_pairs = [&, np](const std::vector<Pose>& x, double* G) {  // (np: this block's local, by value)
       HostScope hs(10);
+      FMX_TRACE_("  full lm lin (lin change %.3e)\n", g.trial_lin_change);
       maybe_spec_map(x);
       for (size_t p = 0; p < np; ++p) {
         mxi[p] = &x[g.pairs[p].first];

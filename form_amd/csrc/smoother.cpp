@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #ifdef FMX_LM_PROF  // diagnostic build: host LM phase times (printed at exit)
@@ -635,8 +636,10 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
   };
   double cur, newErr = err;
   bool conv;
+  static const bool lm_trace = std::getenv("FMX_LM_TRACE") != nullptr;  // diagnostic
   do {
     cur = newErr;
+    if (lm_trace) fprintf(stderr, "    lm iter %d err %.6e lambda %.1e lins %d\n", R.iters, err, lambda, R.lins);
     iterate();
     ++R.iters;
     newErr = err;
