@@ -96,29 +96,31 @@ __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
 // record rec < n0 is planar record rec, else point record rec - n0; each type has its
 // own table section (point bricks at off1) and segment list.
 //
-// The build (map.tpp:128-146 + push_back :41-52), four launches, no table clear:
+// The build (map.tpp:128-146 + push_back :41-52), five launches, no table clear:
 //   k_map_insert  one lane per record: world transform, voxel key; the first lane of the
 //                 wave's records of one brick finds or claims the brick (epoch-tagged CAS,
-//                 linear probing) and reads its claim slot; then one count atomic per
-//                 (wave, cell) group on the claim slot's cell counts (the returned count
-//                 is the record's rank in the cell)
+//                 linear probing); claimed bricks take claim slots (one atomic per wave),
+//                 written into the brick with the slot's cell counts zeroed; every record
+//                 notes its brick and cell
+//   k_map_count   one lane per record: the brick's claim slot, one count atomic per
+//                 (wave, cell) group on the slot's counts (the returned count is the
+//                 record's rank in the cell)
 //   k_map_alloc   one lane per claim slot: the cells' record ranges (block scan + one
 //                 atomic per block and type) into the brick and, with the header slots of
 //                 a dense cell added, over the slot's counts (the scatter's bases)
 //   k_map_scatter one lane per record: the record at its cell's base + rank
 //   k_map_dense   one block per dense cell (> kDenseMin records): counting sort of
 //                 its records into 4 x 4 x 4 sub-cells, header = the sub-cell ends
-// Claim slots are reserved per wave for every probing lane (one atomic per wave) and
-// listed in insertion order: consecutive records are mostly neighbours, so the counts,
+// Claim slots are listed in insertion order: consecutive records are mostly neighbours, so the counts,
 // the ranges and the scatter's bases are read and written near one another instead of
-// at the table's hashed positions — the table is touched once per probe and once per
-// claimed brick (20.6 GB per 50M-record build with per-bucket counts, the
-// counts' random lines and the scatter's brick reads were ~60 % of it).
+// at the table's hashed positions, and the scatter reads no brick (20.6 GB
+// per 50M-record build with per-bucket counts, their random lines and the scatter's
+// brick reads a large share of it).
 // The order of records inside a cell (and of the cells' ranges) follows the atomics,
 // so it varies from build to build; nothing observable depends on it: k_match's
 // argmin is over the total order (d^2, reference shift rank, build order).
 struct BuildState {  // per build, two alternating copies (the other is cleared)
-  uint32_t nclaim;   // claim slots reserved (probing lanes)
+  uint32_t nclaim;   // claimed bricks (= claim slots)
   uint32_t cur[2];   // record slot cursors (planar from 0, point from BuildArgs::pt_base)
   uint32_t err;      // range error: a record outside the packable key range
   uint32_t ndense;   // dense cells
@@ -133,8 +135,7 @@ constexpr int kDenseRecs = 8;             // records per thread: dense cells up 
 constexpr uint32_t kUnsorted = 0xFFFFFFFFu;  // header[0] of a dense cell too large to sort
 constexpr uint32_t kDenseGrid = 1024;     // k_map_dense blocks (each loops over the dense list)
 constexpr int kAllocThreads = 1024;       // k_map_alloc: one cursor atomic per block and type
-constexpr unsigned long long kClaimLock = 1ull << 63;  // a bucket's key while its claimer fills slot / counts
-constexpr uint32_t kNoBrick = 0xFFFFFFFFu;  // a claim slot whose lane found its brick already claimed
+constexpr uint32_t kNoBrick = 0xFFFFFFFFu;  // k_map_alloc: a lane past the claim list
 
 struct BuildArgs {
   const float4* pool_pos[2];
@@ -151,7 +152,7 @@ struct BuildArgs {
   uint64_t off1;  // first point brick
   uint32_t epoch;
   uint2* rinfo;     // per record: claim slot * 8 + cell or ~0, rank in the cell
-  uint32_t* claim;  // per claim slot: the claimed brick, or kNoBrick
+  uint32_t* claim;  // per claim slot: the claimed brick
   uint32_t* dense;  // dense cells
   BuildState* st;
   BuildState* st_next;
@@ -247,61 +248,70 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
   uint32_t brank, bsize;
   wave_group(valid, key, bl, brank, bsize);
   const bool prober = valid && brank == 0;
-  // a claim slot per probing lane, reserved before the probe (one atomic per wave): a
-  // claimer fills its brick's slot field before it releases the bucket, so that no lane
-  // ever waits on a claimer that is itself waiting (lanes that find their brick claimed
-  // leave their slot empty)
-  const uint64_t pm = __ballot(prober);
-  uint32_t ps = 0;
-  {
-    const int leader = __ffsll((unsigned long long)pm) - 1;
-    if (lane_id() == leader) ps = atomicAdd(&a.st->nclaim, (uint32_t)__popcll(pm));
-    ps = (uint32_t)__shfl((int)ps, leader < 0 ? 0 : leader, 64) + (uint32_t)__popcll(pm & lanemask_lt());
-  }
   const unsigned long long bkey = brick_key(cx, cy, cz, a.epoch);
   const uint64_t boff = t == 0 ? 0 : a.off1;
   Brick* bricks = a.bricks + boff;
   const uint64_t mask = a.mask[t];
   uint64_t h = mix64(bkey) & mask;
-  uint32_t slot = 0;
+  bool claimed = false;
   if (prober) {
     for (;;) {  // more buckets than records: a bucket of another epoch always exists
-      const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long ck = cur & ~kClaimLock;
-      if (ck == bkey) {
-        if (cur & kClaimLock) {  // another wave's claimer is filling it in (a few stores)
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        slot = __hip_atomic_load(&bricks[h].slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a.claim[ps] = kNoBrick;
-        break;
-      }
-      if (key_epoch(ck) != a.epoch) {  // empty for this build: claim it
-        const unsigned long long prev = atomicCAS(&bricks[h].key, cur, bkey | kClaimLock);
-        if (prev == cur) {  // claimed: the slot and its zero counts, then the key (release)
-          slot = ps;
-          bricks[h].slot = ps;
-          uint4* cc = reinterpret_cast<uint4*>(a.ccnt + (size_t)ps * 8);
-          cc[0] = make_uint4(0, 0, 0, 0);
-          cc[1] = make_uint4(0, 0, 0, 0);
-          a.claim[ps] = (uint32_t)(boff + h);
-          __hip_atomic_store(&bricks[h].key, bkey, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long cur = __hip_atomic_load(&bricks[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == bkey) break;
+      if (key_epoch(cur) != a.epoch) {  // empty for this build: claim it
+        const unsigned long long prev = atomicCAS(&bricks[h].key, cur, bkey);
+        if (prev == cur) {
+          claimed = true;
           break;
         }
-        continue;  // lost the race: look at the bucket again
+        if (prev == bkey) break;
+        continue;  // another brick took the bucket: look at it again
       }
       h = (h + 1) & mask;
     }
   }
-  slot = (uint32_t)__shfl((int)slot, bl < 0 ? 0 : bl, 64);  // the group's claim slot
-  // rank in the cell: one count atomic per (wave, cell) group
-  const uint32_t cell = slot * 8 + brick_cell(cx, cy, cz);
+  // claimed bricks take consecutive claim slots (one atomic per wave): the slot goes into
+  // the brick (k_map_count reads it) and its cell counts are zeroed
+  const uint64_t cm = __ballot(claimed);
+  if (cm) {
+    const int leader = __ffsll((unsigned long long)cm) - 1;
+    uint32_t cb = 0;
+    if (lane_id() == leader) cb = atomicAdd(&a.st->nclaim, (uint32_t)__popcll(cm));
+    cb = (uint32_t)__shfl((int)cb, leader, 64);
+    if (claimed) {
+      const uint32_t ps = cb + (uint32_t)__popcll(cm & lanemask_lt());
+      bricks[h].slot = ps;
+      uint4* cc = reinterpret_cast<uint4*>(a.ccnt + (size_t)ps * 8);
+      cc[0] = make_uint4(0, 0, 0, 0);
+      cc[1] = make_uint4(0, 0, 0, 0);
+      a.claim[ps] = (uint32_t)(boff + h);
+    }
+  }
+  h = (uint64_t)__shfl((unsigned long long)h, bl < 0 ? 0 : bl, 64);  // the group's bucket
+  if (valid) a.rinfo[rec] = make_uint2((uint32_t)((boff + h) * 8 + brick_cell(cx, cy, cz)), 0u);
+}
+
+// One lane per record, after k_map_insert (every claimer's slot is in its brick): the
+// record's cell in its brick's claim slot, counted with one atomic per (wave, cell) group
+// (the returned count is the record's rank in the cell).  Two launches instead of a
+// claim lock: a lock held while the claimer fills the slot serialized the waves of
+// C4's dense cells (insert 22 -> 113 us, round 5).
+__global__ __launch_bounds__(256) void k_map_count(BuildArgs a) {
+  const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x * blockDim.x >= a.n) return;
+  uint2 ri = make_uint2(0xFFFFFFFFu, 0u);
+  if (rec < a.n) ri = a.rinfo[rec];
+  const bool valid = ri.x != 0xFFFFFFFFu;
+  // the wave's records of one cell: its first lane reads the brick's slot and counts
   int cl;
   uint32_t crank, csize;
-  wave_group(valid, cell, cl, crank, csize);
-  uint32_t cbase = 0;
-  if (valid && crank == 0) cbase = atomicAdd(a.ccnt + cell, csize);
+  wave_group(valid, ri.x, cl, crank, csize);
+  uint32_t cell = 0, cbase = 0;
+  if (valid && crank == 0) {
+    cell = a.bricks[ri.x >> 3].slot * 8 + (ri.x & 7);
+    cbase = atomicAdd(a.ccnt + cell, csize);
+  }
+  cell = (uint32_t)__shfl((int)cell, cl < 0 ? 0 : cl, 64);
   cbase = (uint32_t)__shfl((int)cbase, cl < 0 ? 0 : cl, 64);
   if (valid) a.rinfo[rec] = make_uint2(cell, cbase + crank);
 }
@@ -2329,7 +2339,7 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   c->map_inv_p = c->map_blob.p + 12 * (size_t)Kc;
   const Seg* dseg = reinterpret_cast<const Seg*>(c->map_blob.p + 24 * (size_t)Kc);
   // fused build of both types: one brick table (planar bricks, then point bricks),
-  // one record numbering, four launches (k_map_insert / alloc / scatter / dense)
+  // one record numbering, five launches (k_map_insert / count / alloc / scatter / dense)
   VoxMap& M = c->map;
   const uint32_t n = nrec[0] + nrec[1];
   if (n >= (1u << 27)) throw StatusError(FMX_E_SIZE, "voxel map: more than 2^27 records (k_match tie key)");
@@ -2414,6 +2424,8 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   hipLaunchKernelGGL(k_map_insert, dim3(nb), dim3(256), 0, st, ba);
   FMX_HIP(hipGetLastError());
   if (n > 0) {
+    hipLaunchKernelGGL(k_map_count, dim3(nb), dim3(256), 0, st, ba);
+    FMX_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_map_alloc, dim3((n + kAllocThreads - 1) / kAllocThreads), dim3(kAllocThreads), 0, st, ba);
     FMX_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_map_scatter, dim3(nb), dim3(256), 0, st, ba);

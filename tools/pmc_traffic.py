@@ -44,6 +44,7 @@ KMAP = {
     "k_linearize<1>": "linearize_pairs",
     "k_linearize<0>": "linearize_full",
     "k_map_insert": "map_build_insert",
+    "k_map_count": "map_build_count",
     "k_map_alloc": "map_build_alloc",
     "k_map_scatter": "map_build_scatter",
     "k_map_dense": "map_build_dense",
@@ -96,7 +97,7 @@ def main():
     # the map build as one class (bench.py's "map_build": its four kernels, once each per
     # build): insert / alloc / scatter mix coalesced record streams with random table
     # lines, so the sum keeps both bounds and takes the upper one
-    parts = [kernels[k] for k in ("map_build_insert", "map_build_alloc", "map_build_scatter", "map_build_dense")
+    parts = [kernels[k] for k in ("map_build_insert", "map_build_count", "map_build_alloc", "map_build_scatter", "map_build_dense")
              if k in kernels and "hbm_bytes_lo" in kernels[k]]
     if parts:
         lo = sum(p["hbm_bytes_lo"] for p in parts)
