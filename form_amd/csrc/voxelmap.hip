@@ -2463,9 +2463,13 @@ void run_pair_scatter(fmx_ctx* c) {
   FMX_HIP(hipGetLastError());
 }
 
-// FMX_NO_LPT: query blocks dispatched in index order (A/B switch; same results)
+// FMX_LPT=1: heaviest-first query-block dispatch (opt-in; same results).  Measured
+// round 5 (profiles/r5_ab_envs.txt): the warm launches it applies to were already short
+// (certificate), the cold one has no order, and the order read + the last block's
+// counting sort cost more than the shorter tail gained — match 0.296 -> 0.311 ms per C4
+// scan with it, so index order is the default.
 static bool no_lpt() {
-  static const bool v = std::getenv("FMX_NO_LPT") != nullptr;
+  static const bool v = std::getenv("FMX_LPT") == nullptr || std::getenv("FMX_NO_LPT") != nullptr;
   return v;
 }
 // FMX_NO_WARM: every match cold; FMX_NO_CELL_CACHE: warm matches probe their own cell
