@@ -52,7 +52,14 @@
 #endif
 #endif
 #ifndef FMX_MATCH_DEPTH_PLAIN
+#if defined(FMX_MATCH_GROUP) && FMX_MATCH_GROUP == 1
+#define FMX_MATCH_DEPTH_PLAIN 1  // ... one lane per query (C5): two in flight spilled a record per
+                                 // candidate to scratch at 7 waves (48 B of scratch traffic per query,
+                                 // ~95 MB per whole-map launch); one: whole-map launch 0.754 -> 0.698 ms
+                                 // per registration, local 0.805 -> 0.774 (profiles/r5_c5_ab.txt)
+#else
 #define FMX_MATCH_DEPTH_PLAIN 2  // record loads in flight per lane without the dense-cell walk
+#endif
 #endif
 #ifndef FMX_MATCH_WAVES_FUSED
 #define FMX_MATCH_WAVES_FUSED FMX_MATCH_WAVES_PLAIN  // ... the fused match + linearization (C5)
