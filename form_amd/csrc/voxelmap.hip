@@ -106,13 +106,13 @@ __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
 // The build (map.tpp:128-146 + push_back :41-52), five launches, no table clear:
 //   k_map_insert  one lane per record: world transform, voxel key; the first lane of the
 //                 wave's records of one brick finds or claims the brick (epoch-tagged CAS,
-//                 linear probing); claimed bricks take claim slots (one atomic per wave),
-//                 written into the brick with the slot's cell counts zeroed; every record
-//                 notes its brick and cell
+//                 linear probing); a claimed brick's claim slot is its claimer's record
+//                 index, written into the brick with the slot's cell counts zeroed; every
+//                 record notes its brick and cell
 //   k_map_count   one lane per record: the brick's claim slot, one count atomic per
 //                 (wave, cell) group on the slot's counts (the returned count is the
 //                 record's rank in the cell)
-//   k_map_alloc   one lane per claim slot: the cells' record ranges (block scan + one
+//   k_map_alloc   four claim slots per lane: the cells' record ranges (block scan + one
 //                 atomic per block and type) into the brick and, with the header slots of
 //                 a dense cell added, over the slot's counts (the scatter's bases)
 //   k_map_scatter one lane per record: the record at its cell's base + rank
@@ -127,7 +127,7 @@ __device__ __forceinline__ int find_seg(const Seg* segs, int K, uint32_t rec) {
 // so it varies from build to build; nothing observable depends on it: k_match's
 // argmin is over the total order (d^2, reference shift rank, build order).
 struct BuildState {  // per build, two alternating copies (the other is cleared)
-  uint32_t nclaim;   // claimed bricks (= claim slots)
+  uint32_t nclaim;   // (unused: claim slots are record indices)
   uint32_t cur[2];   // record slot cursors (planar from 0, point from BuildArgs::pt_base)
   uint32_t err;      // range error: a record outside the packable key range
   uint32_t ndense;   // dense cells
@@ -142,7 +142,7 @@ constexpr int kDenseRecs = 8;             // records per thread: dense cells up 
 constexpr uint32_t kUnsorted = 0xFFFFFFFFu;  // header[0] of a dense cell too large to sort
 constexpr uint32_t kDenseGrid = 1024;     // k_map_dense blocks (each loops over the dense list)
 constexpr int kAllocThreads = 1024;       // k_map_alloc: one cursor atomic per block and type
-constexpr uint32_t kNoBrick = 0xFFFFFFFFu;  // k_map_alloc: a lane past the claim list
+constexpr uint32_t kNoBrick = 0xFFFFFFFFu;  // a claim slot whose record claimed no brick
 
 struct BuildArgs {
   const float4* pool_pos[2];
@@ -159,7 +159,7 @@ struct BuildArgs {
   uint64_t off1;  // first point brick
   uint32_t epoch;
   uint2* rinfo;     // per record: claim slot * 8 + cell or ~0, rank in the cell
-  uint32_t* claim;  // per claim slot: the claimed brick
+  uint32_t* claim;  // per claim slot (= record index): the brick its record claimed, or kNoBrick
   uint32_t* dense;  // dense cells
   BuildState* st;
   BuildState* st_next;
@@ -277,23 +277,17 @@ __global__ __launch_bounds__(256) void k_map_insert(BuildArgs a) {
       h = (h + 1) & mask;
     }
   }
-  // claimed bricks take consecutive claim slots (one atomic per wave): the slot goes into
-  // the brick (k_map_count reads it) and its cell counts are zeroed
-  const uint64_t cm = __ballot(claimed);
-  if (cm) {
-    const int leader = __ffsll((unsigned long long)cm) - 1;
-    uint32_t cb = 0;
-    if (lane_id() == leader) cb = atomicAdd(&a.st->nclaim, (uint32_t)__popcll(cm));
-    cb = (uint32_t)__shfl((int)cb, leader, 64);
-    if (claimed) {
-      const uint32_t ps = cb + (uint32_t)__popcll(cm & lanemask_lt());
-      bricks[h].slot = ps;
-      uint4* cc = reinterpret_cast<uint4*>(a.ccnt + (size_t)ps * 8);
-      cc[0] = make_uint4(0, 0, 0, 0);
-      cc[1] = make_uint4(0, 0, 0, 0);
-      a.claim[ps] = (uint32_t)(boff + h);
-    }
+  // a claimed brick's claim slot is its claimer's record index: no counter (one atomic per
+  // wave on a single word serialized the build — C5 insert 9.1 ms for 50M records, C4
+  // ~20 us; round 5).  The slot goes into the brick (k_map_count reads it), its cell counts
+  // are zeroed, and every record's slot entry says whether it claimed
+  if (claimed) {
+    bricks[h].slot = rec;
+    uint4* cc = reinterpret_cast<uint4*>(a.ccnt + (size_t)rec * 8);
+    cc[0] = make_uint4(0, 0, 0, 0);
+    cc[1] = make_uint4(0, 0, 0, 0);
   }
+  if (rec < a.n) a.claim[rec] = claimed ? (uint32_t)(boff + h) : kNoBrick;
   h = (uint64_t)__shfl((unsigned long long)h, bl < 0 ? 0 : bl, 64);  // the group's bucket
   if (valid) a.rinfo[rec] = make_uint2((uint32_t)((boff + h) * 8 + brick_cell(cx, cy, cz)), 0u);
 }
@@ -323,76 +317,85 @@ __global__ __launch_bounds__(256) void k_map_count(BuildArgs a) {
   if (valid) a.rinfo[rec] = make_uint2(cell, cbase + crank);
 }
 
-// One lane per claim slot: record ranges of its brick's 8 cells, allocated per type from
-// the state's cursors (one atomic per block and type), into the brick (k_match) and, as
-// the scatter's per-cell bases (past a dense cell's header), over the slot's counts;
-// dense cells reserve kHdr header slots and are listed for k_map_dense.  The grid is
-// sized for the worst case (every record probing); lanes past nclaim and empty slots
-// only take part in the scans.
+// kAllocPer consecutive claim slots (= record indices) per lane: record ranges of each
+// claimed brick's 8 cells, allocated per type from the state's cursors (one atomic per
+// block and type), into the brick (k_match) and, as the scatter's per-cell bases (past a
+// dense cell's header), over the slot's counts; dense cells reserve kHdr header slots
+// and are listed for k_map_dense.  Slots whose record claimed nothing are skipped.
+constexpr int kAllocPer = 4;
 __global__ __launch_bounds__(kAllocThreads) void k_map_alloc(BuildArgs a) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t ncl = __hip_atomic_load(&a.st->nclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (blockIdx.x * blockDim.x >= ncl) return;  // whole block past the list
-  const uint32_t gb = i < ncl ? a.claim[i] : kNoBrick;
-  const bool valid = gb != kNoBrick;
-  const int t = gb >= a.off1 ? 1 : 0;
-  uint32_t sz[8], tot = 0, dmask = 0;
-  uint4* cp = reinterpret_cast<uint4*>(a.ccnt + (size_t)i * 8);
-  if (valid) {
-    const uint4 c0 = cp[0], c1 = cp[1];
-    const uint32_t c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * kAllocPer;
+  uint32_t gb[kAllocPer], tot[kAllocPer], dm[kAllocPer], sz[kAllocPer][8];
+  uint32_t vt[2] = {0u, 0u};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const bool d = c[k] > (uint32_t)kDenseMin;
-      dmask |= (d ? 1u : 0u) << k;
-      sz[k] = c[k] + (d ? kHdr : 0);
-      tot += sz[k];
+  for (int u = 0; u < kAllocPer; ++u) {
+    const uint32_t i = i0 + u;
+    gb[u] = i < a.n ? a.claim[i] : kNoBrick;
+    tot[u] = 0;
+    dm[u] = 0;
+    if (gb[u] != kNoBrick) {
+      const uint4* cp = reinterpret_cast<const uint4*>(a.ccnt + (size_t)i * 8);
+      const uint4 c0 = cp[0], c1 = cp[1];
+      const uint32_t c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool d = c[k] > (uint32_t)kDenseMin;
+        dm[u] |= (d ? 1u : 0u) << k;
+        sz[u][k] = c[k] + (d ? kHdr : 0);
+        tot[u] += sz[u][k];
+      }
+      vt[gb[u] >= a.off1 ? 1 : 0] += tot[u];
     }
   }
-  // per type: block-wide exclusive scan of the range sizes, one atomic per block
+  // per type: block-wide exclusive scan of the lanes' range totals, one atomic per block
   __shared__ uint32_t s_w[2][kAllocThreads / kWave];
   __shared__ uint32_t s_b[2];
   const int w = threadIdx.x / kWave;
-  uint32_t incl[2], v[2];
+  uint32_t incl[2];
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    v[tt] = valid && t == tt ? tot : 0u;
-    incl[tt] = wave_incl_scan(v[tt]);
+    incl[tt] = wave_incl_scan(vt[tt]);
     if (lane_id() == 63) s_w[tt][w] = incl[tt];
   }
   __syncthreads();
   if (threadIdx.x < 2) {
     uint32_t bt = 0;
-    for (int i = 0; i < kAllocThreads / kWave; ++i) bt += s_w[threadIdx.x][i];
+    for (int q = 0; q < kAllocThreads / kWave; ++q) bt += s_w[threadIdx.x][q];
     s_b[threadIdx.x] = bt ? atomicAdd(&a.st->cur[threadIdx.x], bt) : 0u;
   }
   __syncthreads();
-  uint32_t base = 0;
+  uint32_t run[2];
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     uint32_t wo = s_b[tt];
-    for (int i = 0; i < w; ++i) wo += s_w[tt][i];
-    if (t == tt) base = wo + incl[tt] - v[tt] + (tt == 1 ? a.pt_base : 0u);
+    for (int q = 0; q < w; ++q) wo += s_w[tt][q];
+    run[tt] = wo + incl[tt] - vt[tt] + (tt == 1 ? a.pt_base : 0u);
   }
-  if (!valid) return;
-  Brick& B = a.bricks[gb];
-  uint32_t run = base, first[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    B.beg[k] = run;
-    first[k] = run + (((dmask >> k) & 1) ? kHdr : 0);
-    run += sz[k];
-  }
-  B.beg[8] = run;
-  B.dense = dmask;
-  cp[0] = make_uint4(first[0], first[1], first[2], first[3]);
-  cp[1] = make_uint4(first[4], first[5], first[6], first[7]);
-  if (dmask) {
-    const uint32_t o = atomicAdd(&a.st->ndense, (uint32_t)__popc(dmask));
-    uint32_t j = 0;
+  for (int u = 0; u < kAllocPer; ++u) {
+    if (gb[u] == kNoBrick) continue;
+    const int t = gb[u] >= a.off1 ? 1 : 0;
+    Brick& B = a.bricks[gb[u]];
+    uint32_t r = run[t], first[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if ((dmask >> k) & 1) a.dense[o + j++] = gb * 8 + k;
+    for (int k = 0; k < 8; ++k) {
+      B.beg[k] = r;
+      first[k] = r + (((dm[u] >> k) & 1) ? kHdr : 0);
+      r += sz[u][k];
+    }
+    B.beg[8] = r;
+    B.dense = dm[u];
+    run[t] = r;
+    uint4* cp = reinterpret_cast<uint4*>(a.ccnt + (size_t)(i0 + u) * 8);
+    cp[0] = make_uint4(first[0], first[1], first[2], first[3]);
+    cp[1] = make_uint4(first[4], first[5], first[6], first[7]);
+    if (dm[u]) {
+      const uint32_t o = atomicAdd(&a.st->ndense, (uint32_t)__popc(dm[u]));
+      uint32_t j = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if ((dm[u] >> k) & 1) a.dense[o + j++] = gb[u] * 8 + k;
+    }
   }
 }
 
@@ -2433,7 +2436,8 @@ void run_map_build(fmx_ctx* c, const std::vector<uint64_t>& scans, const double*
   if (n > 0) {
     hipLaunchKernelGGL(k_map_count, dim3(nb), dim3(256), 0, st, ba);
     FMX_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_map_alloc, dim3((n + kAllocThreads - 1) / kAllocThreads), dim3(kAllocThreads), 0, st, ba);
+    hipLaunchKernelGGL(k_map_alloc, dim3((n + kAllocThreads * kAllocPer - 1) / (kAllocThreads * kAllocPer)),
+                       dim3(kAllocThreads), 0, st, ba);
     FMX_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_map_scatter, dim3(nb), dim3(256), 0, st, ba);
     FMX_HIP(hipGetLastError());
