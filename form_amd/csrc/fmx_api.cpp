@@ -1119,7 +1119,8 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     }
     HostScope* hs_lm = new HostScope(8);
     FMX_TRACE_("scan %llu it %u: lm\n", (unsigned long long)j, it);
-    const WinLMResult R = window_lm(g, window_poses(e), &icp_base);
+    static const bool no_base_cache = std::getenv("FMX_NO_BASE_CACHE") != nullptr;  // A/B switch
+    const WinLMResult R = window_lm(g, window_poses(e), no_base_cache ? nullptr : &icp_base);
     FMX_TRACE_("scan %llu it %u: lm done\n", (unsigned long long)j, it);
     delete hs_lm;
     lm_it += R.iters;
