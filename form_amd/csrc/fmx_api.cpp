@@ -982,7 +982,6 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
   std::vector<const double*> mp;             // contraction arguments (moments.hpp)
   std::vector<const Pose*> mri, mrj, mxi, mxj;
   MomBatch mbatch;
-  WinLMBase icp_base;  // the ICP loop's LMs share keys, priors and linear factors: one base system
   for (uint32_t it = 0; it < P.max_num_rematches; ++it) {
     ++icp;
     const Pose before = e.values.at(j);
@@ -1119,8 +1118,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     }
     HostScope* hs_lm = new HostScope(8);
     FMX_TRACE_("scan %llu it %u: lm\n", (unsigned long long)j, it);
-    static const bool no_base_cache = std::getenv("FMX_NO_BASE_CACHE") != nullptr;  // A/B switch
-    const WinLMResult R = window_lm(g, window_poses(e), no_base_cache ? nullptr : &icp_base);
+    const WinLMResult R = window_lm(g, window_poses(e));
     FMX_TRACE_("scan %llu it %u: lm done\n", (unsigned long long)j, it);
     delete hs_lm;
     lm_it += R.iters;

@@ -444,32 +444,26 @@ namespace {
 // factor order, so every element sees the same sequence of additions as a fresh sum.
 struct Assembler {
   const WinGraph& g;
-  DenseSys own;
-  const DenseSys& base;
-  // cache (may be null): a base built by an earlier LM over the same keys, priors and
-  // linear factors (WinLMBase), or the place to keep this one's
-  Assembler(const WinGraph& gr, WinLMBase* cache) : g(gr), base(cache ? cache->base : own) {
-    if (cache && cache->valid) return;
-    DenseSys& b = cache ? cache->base : own;
-    b.init(g.keys);
-    const int D = b.D;
+  DenseSys base;
+  explicit Assembler(const WinGraph& gr) : g(gr) {
+    base.init(g.keys);
+    const int D = base.D;
     for (const PriorF* P : g.priors) {
       const double inv = 1.0 / P->sigma;
-      const int s = b.slot.at(P->key);
-      for (int k = 0; k < 6; ++k) b.at(6 * s + k, 6 * s + k) += inv * inv;
+      const int s = base.slot.at(P->key);
+      for (int k = 0; k < 6; ++k) base.at(6 * s + k, 6 * s + k) += inv * inv;
     }
     for (const LinF* L : g.lins) {
       const int n = 6 * (int)L->keys.size(), m = n + 1;
       std::vector<int> col(n);
       for (size_t k = 0; k < L->keys.size(); ++k)
-        for (int e = 0; e < 6; ++e) col[6 * k + e] = 6 * b.slot.at(L->keys[k]) + e;
+        for (int e = 0; e < 6; ++e) col[6 * k + e] = 6 * base.slot.at(L->keys[k]) + e;
       const double* I = L->info.data();
       for (int r = 0; r < n; ++r) {
-        double* row = &b.A[(size_t)col[r] * (D + 1)];
+        double* row = &base.A[(size_t)col[r] * (D + 1)];
         for (int c = 0; c < n; ++c) row[col[c]] += I[(size_t)r * m + c];
       }
     }
-    if (cache) cache->valid = true;
   }
   // S back to the base system.  A linearization changes only the entries the pairs'
   // 6 x 6 blocks ((i,i), (i,j), (j,i), (j,j)) and the rhs row / column cover (the prior
@@ -568,12 +562,12 @@ struct Assembler {
 // defaultOptimize + iterate/tryLambda).  Each trial is evaluated by a full
 // linearization: it yields the error the accept test needs and, when accepted, the
 // next iteration's system (one device launch per trial).
-WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0, WinLMBase* cache) {
+WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
   WinLMResult R;
   R.x = x0;
   const bool split = !g.pairs.empty() && g.lin_begin;
   if (split) g.lin_begin(R.x);  // the first linearization runs while the base system is built
-  const Assembler asmb(g, cache);
+  const Assembler asmb(g);
   DenseSys S, Sn;
   std::vector<double> Gn;
   double err = asmb.run(R.x, S, R.G, R.lins, split);

@@ -59,6 +59,8 @@ struct WinLMResult {
   int lins = 0;           // lin_pairs calls
 };
 
+WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0);
+
 // Dense augmented system over `keys` (any order), columns 6*slot + d, rhs last.
 struct DenseSys {
   std::vector<uint64_t> keys;
@@ -71,17 +73,6 @@ struct DenseSys {
   double add_prior(const PriorF& P, const Pose& x);                       // returns error
   double add_linf(const LinF& L, const std::vector<Pose>& xk);            // x per L.keys
 };
-
-// A window_lm's x-independent base system (the priors' and linear factors' information,
-// summed in factor order).  The LMs of one ICP loop share keys, priors and linear factors
-// (only the pairs' correspondences change), so register_scan builds it with the first
-// and reuses it: the same sums, once per scan instead of once per ICP iteration.
-struct WinLMBase {
-  DenseSys base;
-  bool valid = false;
-};
-
-WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0, WinLMBase* cache = nullptr);
 
 // Solve A x = g for SPD A (n x n row-major, overwritten by the factor); false if A is
 // not positive definite.
