@@ -16,7 +16,7 @@ B="--steps 10 --warmup 5 --no-cpu-baseline --no-c5 --no-ablation --sub-workloads
 RX='k_match|k_extract_rows|k_normals|k_closest|k_fit|k_linearize|k_map_|k_insert|k_win_|k_pair_scatter|k_unpack'
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA"
 if [ "${PART:-scan}" = scan ]; then
-  for w in ${WORKLOADS:-c4 c2 c3}; do
+  [ "${PMC:-1}" = 1 ] && for w in ${WORKLOADS:-c4 c2 c3}; do
     i=0
     for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
       i=$((i+1))
@@ -29,10 +29,12 @@ if [ "${PART:-scan}" = scan ]; then
 import json; d=json.load(open('$D/traffic_$w.json'))
 for k,v in d['kernels'].items(): print('$w', k, v.get('hbm_bytes_per_launch'), round(v.get('l2_hit_rate') or 0, 3), v['launches'])"
   done
-  rm -rf $D/sq_c4
-  timeout -s KILL 300 rocprofv3 --pmc $SQ --kernel-include-regex "k_match" -d $D/sq_c4 -o run --output-format csv -- python bench.py --workload c4 $B > $D/sq_c4.out 2> $D/sq_c4.err || { tail -20 $D/sq_c4.err; exit 1; }
-  python tools/pmc_traffic.py c4 $D/sq_wavestate_c4.json $D/sq_c4 > /dev/null || exit 1
-  find $D/sq_c4 -name "*counter_collection.csv" -delete
+  if [ "${PMC:-1}" = 1 ]; then
+    rm -rf $D/sq_c4
+    timeout -s KILL 300 rocprofv3 --pmc $SQ --kernel-include-regex "k_match" -d $D/sq_c4 -o run --output-format csv -- python bench.py --workload c4 $B > $D/sq_c4.out 2> $D/sq_c4.err || { tail -20 $D/sq_c4.err; exit 1; }
+    python tools/pmc_traffic.py c4 $D/sq_wavestate_c4.json $D/sq_c4 > /dev/null || exit 1
+    find $D/sq_c4 -name "*counter_collection.csv" -delete
+  fi
   for w in ${CPATH:-c4 c2}; do
     rm -rf $D/prof_$w
     # default --steps 40 (+ a 40-scan profile pass after them: skip 40)
