@@ -85,17 +85,22 @@ inline cpu_set_t llc_siblings(int cpu) {
   return m;
 }
 
-// Where the helpers of a creator running on `creator_cpu` may run: the load-time CPUs
-// (g_load_cpus) that share its last-level cache, minus its own CPU; failing that, every
-// load-time CPU but its own; if that leaves nothing, the inherited mask (nullopt-like:
-// returns false).
+// Where the helpers of a creator running on `creator_cpu` may run: every load-time CPU
+// (g_load_cpus) but the creator's; if that leaves nothing, the inherited mask (returns
+// false).  FMX_STAGE_LLC=1 (A/B) prefers the load-time CPUs sharing the creator's last-level
+// cache: measured round 5 on a shared GPU box it starved the helpers (the creator's CCX is
+// shared with other jobs' threads): pageable pipelined host input 0.98 -> 0.83 of the
+// device-resident rate (profiles/r5_ab_stage_cpus.txt).
 inline bool helper_cpus(int creator_cpu, cpu_set_t& out) {
-  cpu_set_t near = llc_siblings(creator_cpu), pref;
-  CPU_AND(&pref, &near, &g_load_cpus);
-  if (creator_cpu >= 0) CPU_CLR(creator_cpu, &pref);
-  if (CPU_COUNT(&pref) > 0) {
-    out = pref;
-    return true;
+  static const bool llc = std::getenv("FMX_STAGE_LLC") != nullptr;
+  if (llc) {
+    cpu_set_t near = llc_siblings(creator_cpu), pref;
+    CPU_AND(&pref, &near, &g_load_cpus);
+    if (creator_cpu >= 0) CPU_CLR(creator_cpu, &pref);
+    if (CPU_COUNT(&pref) > 0) {
+      out = pref;
+      return true;
+    }
   }
   out = g_load_cpus;
   if (creator_cpu >= 0) CPU_CLR(creator_cpu, &out);
