@@ -9,6 +9,7 @@
 // prefix right away (sequential registration), or it runs entirely in the background
 // while the previous scan registers (an announced next scan, fmx_next_scan).
 #pragma once
+#include <dirent.h>
 #include <immintrin.h>
 #include <sched.h>
 
@@ -27,14 +28,27 @@
 
 namespace fmx {
 
-// The CPUs the process may use, captured when the library is loaded — before a caller
-// pins its registering thread (bench.py does, after importing) — and narrowed by
-// FMX_STAGE_CPUS ("0-3,8,10-11") when set.  The staging helpers run only on these.
+// The CPUs the process may use — the union of its threads' affinity masks when the
+// library is loaded (a caller that pinned its registering thread before loading it,
+// as bench.py does, still has threads on the launch mask: taskset / numactl / a rank
+// binding) — narrowed by FMX_STAGE_CPUS ("0-3,8,10-11") when set.  The staging helpers
+// run only on these.  (Round 5: the loading thread's own mask alone was the pinned CPU,
+// so every helper ran on the registering thread's CPU: pageable host input 0.98 -> 0.83
+// of the device-resident rate.)
 inline cpu_set_t capture_load_cpus() {
   cpu_set_t m;
   CPU_ZERO(&m);
   if (sched_getaffinity(0, sizeof(m), &m) != 0) {
     for (int i = 0; i < CPU_SETSIZE; ++i) CPU_SET(i, &m);
+  }
+  if (DIR* d = opendir("/proc/self/task")) {
+    while (const dirent* e = readdir(d)) {
+      const int tid = std::atoi(e->d_name);
+      cpu_set_t t;
+      CPU_ZERO(&t);
+      if (tid > 0 && sched_getaffinity(tid, sizeof(t), &t) == 0) CPU_OR(&m, &m, &t);
+    }
+    closedir(d);
   }
   if (const char* e = std::getenv("FMX_STAGE_CPUS")) {
     cpu_set_t o;

@@ -3,8 +3,11 @@
 // (float4 -> x, y, z), several requests in flight, reuse after retire, helpers stopped
 // and restarted.  Built twice by tests/cpp/Makefile: plain and with
 // -fsanitize=thread (data races between the helpers, the caller and retire/reset).
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <random>
 #include <vector>
 
@@ -39,9 +42,39 @@ static int check_helper_cpus() {
   return bad;
 }
 
+// Round 5: a process whose loading thread is pinned to one CPU (bench.py pins its
+// registering thread before the library loads) still has its other threads on the
+// launch mask; the helpers' mask is their union, not the pinned CPU alone.
+static int check_pinned_loader() {
+  cpu_set_t all;
+  CPU_ZERO(&all);
+  if (sched_getaffinity(0, sizeof(all), &all) != 0 || CPU_COUNT(&all) < 2) return 0;  // nothing to check
+  std::atomic<bool> go{false};
+  std::thread other([&] {  // keeps the launch mask
+    while (!go.load()) std::this_thread::yield();
+  });
+  int first = 0;
+  while (!CPU_ISSET(first, &all)) ++first;
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(first, &one);
+  sched_setaffinity(0, sizeof(one), &one);
+  const cpu_set_t got = fmx::capture_load_cpus();
+  sched_setaffinity(0, sizeof(all), &all);
+  go = true;
+  other.join();
+  cpu_set_t x;
+  CPU_AND(&x, &got, &all);
+  return CPU_EQUAL(&x, &all) ? 0 : 1;
+}
+
 int main() {
   if (check_helper_cpus()) {
     std::printf("helper CPUs outside the load-time mask\n");
+    return 1;
+  }
+  if (!std::getenv("FMX_STAGE_CPUS") && check_pinned_loader()) {
+    std::printf("a pinned loading thread narrowed the helpers' mask to its CPU\n");
     return 1;
   }
   std::mt19937 g(7);
