@@ -101,10 +101,8 @@ inline cpu_set_t llc_siblings(int cpu) {
 
 // Where the helpers of a creator running on `creator_cpu` may run: every load-time CPU
 // (g_load_cpus) but the creator's; if that leaves nothing, the inherited mask (returns
-// false).  FMX_STAGE_LLC=1 (A/B) prefers the load-time CPUs sharing the creator's last-level
-// cache: measured round 5 on a shared GPU box it starved the helpers (the creator's CCX is
-// shared with other jobs' threads): pageable pipelined host input 0.98 -> 0.83 of the
-// device-resident rate (profiles/r5_ab_stage_cpus.txt).
+// false).  FMX_STAGE_LLC=1 (A/B) prefers the load-time CPUs sharing the creator's
+// last-level cache (on a shared GPU box the creator's CCX also runs other jobs' threads).
 inline bool helper_cpus(int creator_cpu, cpu_set_t& out) {
   static const bool llc = std::getenv("FMX_STAGE_LLC") != nullptr;
   if (llc) {
