@@ -454,9 +454,12 @@ bool host_pinned(const void* p, size_t bytes) {
   }
   return true;
 }
-// FMX_STAGE_ROWS=0 (A/B diagnostic): extract a staged host scan only once all of it has landed
+// FMX_STAGE_ROWS=1 (A/B): extract a staged host scan's lines as each DMA piece lands
+// instead of once all of it has.  Measured round 5 (profiles/r5_ab_host_input.txt):
+// pageable sequential 0.82-0.84 -> 0.74-0.80 of device-sequential with it — the small
+// per-piece launches and unpacks cost the staging thread more than the overlap gains.
 bool stage_rows() {
-  static const bool v = env_int("FMX_STAGE_ROWS", 1) != 0;
+  static const bool v = env_int("FMX_STAGE_ROWS", 0) != 0;
   return v;
 }
 // A host scan for the sequential path, into c->scan on the context stream: a pinned one
