@@ -1726,7 +1726,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
-  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release(); c->mcert.release(); c->mprof.release(); c->mord.release(); c->mcost.release();
+  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release(); c->mprof.release(); c->mord.release(); c->mcost.release();
   c->cert_b2.release();
   {
     auto& S = c->spec;

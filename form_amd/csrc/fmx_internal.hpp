@@ -473,7 +473,6 @@ struct fmx_ctx {
   fmx::DBuf<uint32_t> ins_blk, ins_off;           // per match block insert counts / offsets
   uint32_t ins_tot[2] = {0, 0};                   // insert totals of the last match
   uint32_t cert_tot[2] = {0, 0};                  // ... its certified / warm query counts
-  fmx::DBuf<uint32_t> mcert;                      // the match launches' certified / warm sums (self-resetting)
   fmx::DBuf<uint32_t> mprof;                      // profiled match launches' probe / candidate sums (self-resetting)
   fmx::DBuf<uint32_t> mord, mcost;                // heaviest-first query-block order + per-block durations (k_match)
   uint64_t ord_gen = 0;                           // warm_gen when mord was written (0: none)

@@ -571,9 +571,6 @@ struct MatchArgs {
   int cert_ok;  // cert_b2 holds the bounds of the match that wrote the warm records
                 // (an 8-lane match on this map and query set; the one-lane build keeps none)
 #endif
-  // per launch: [0] certified queries, [1] warm queries (agent-scope sums of the
-  // blocks' counts, published by the last block to host_counts[2K + 2 ..] and zeroed)
-  uint32_t* cert_cnt;
   // profiled launches only (else null): the launch's total probes / candidates, summed
   // in prof_acc (agent scope, self-resetting) and stored by the last block to prof_work
   // (its pinned slot of the profiler's work ring: the byte model of THIS launch)
@@ -1535,9 +1532,33 @@ __device__ __forceinline__ bool match_result(const MatchArgs& a, const MapView& 
 // The last block's bookkeeping of a match (every block's counts are in): the pair
 // counts (counts mode, zeroing mcnt), the per-block insert counts scanned into k_insert
 // offsets + totals, the tiled pair sort's tail.
-__device__ inline void match_tail(const MatchArgs& a, uint32_t* __restrict__ mcnt, uint32_t* __restrict__ host_counts,
-                                  uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off,
-                                  uint32_t* __restrict__ thist, const SortOut& so) {
+// Per-block words ins_blk[b]: the block's insert count (bits 0-9), certified queries
+// (10-19) and warm queries (20-29) — the counts fit 10 bits (<= 256 queries per block).
+// Returns the launch's certified / warm totals (valid in thread 0).
+constexpr uint32_t kInsMask = 0x3FFu;
+__device__ __forceinline__ uint32_t blk_word(uint32_t ins, uint32_t cert, uint32_t warm) {
+  return ins | cert << 10 | warm << 20;
+}
+__device__ __forceinline__ uint2 block_sum2(uint32_t x, uint32_t y) {
+  __shared__ uint32_t s2[2][kMatchThreads / kWave];
+  x = wave_sum(x);
+  y = wave_sum(y);
+  if (lane_id() == 0) {
+    s2[0][threadIdx.x / kWave] = x;
+    s2[1][threadIdx.x / kWave] = y;
+  }
+  __syncthreads();
+  uint2 t = make_uint2(0u, 0u);
+  if (threadIdx.x == 0)
+    for (int i = 0; i < kMatchThreads / kWave; ++i) {
+      t.x += s2[0][i];
+      t.y += s2[1][i];
+    }
+  return t;
+}
+__device__ inline uint2 match_tail(const MatchArgs& a, uint32_t* __restrict__ mcnt, uint32_t* __restrict__ host_counts,
+                                   uint32_t* __restrict__ ins_blk, uint32_t* __restrict__ ins_off,
+                                   uint32_t* __restrict__ thist, const SortOut& so) {
   if (!a.sorted)
     for (int i = threadIdx.x; i < 2 * a.K; i += kMatchThreads)
       host_store(host_counts + i, __hip_atomic_exchange(mcnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1560,6 +1581,15 @@ __device__ inline void match_tail(const MatchArgs& a, uint32_t* __restrict__ mcn
       v[2][u] = i < nth0 ? __hip_atomic_exchange(thist + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
       v[3][u] = i < nth1 ? __hip_atomic_exchange(thist + nth0 + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     }
+    uint32_t cs = 0, wsum = 0;  // the blocks' certified / warm counts (upper fields of ins_blk)
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        cs += (v[q][u] >> 10) & kInsMask;
+        wsum += v[q][u] >> 20;
+        v[q][u] &= kInsMask;
+      }
     uint32_t sum[4], ex[4], tot[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1600,16 +1630,28 @@ __device__ inline void match_tail(const MatchArgs& a, uint32_t* __restrict__ mcn
       }
       pair_sort_finish(a, so, host_counts, s_pb);
     }
-    return;
+    return block_sum2(cs, wsum);
   }
+  uint32_t cs = 0, wsum = 0;
+  for (uint32_t i = threadIdx.x; i < a.nb_pl + a.nb_pt; i += kMatchThreads) {
+    const uint32_t x = __hip_atomic_load(ins_blk + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cs += (x >> 10) & kInsMask;
+    wsum += x >> 20;
+  }
+  const uint2 cw = block_sum2(cs, wsum);
+  __syncthreads();
   for (int tt = 0; tt < 2; ++tt) {  // planar blocks [0, nb_pl), point blocks [nb_pl, nb)
     const uint32_t b0 = tt == 0 ? 0u : a.nb_pl, n = tt == 0 ? a.nb_pl : a.nb_pt;
     const uint32_t tot = block_scan_runs<8>(
-        n, 0u, [&](uint32_t i) { return __hip_atomic_load(ins_blk + b0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); },
+        n, 0u,
+        [&](uint32_t i) {
+          return __hip_atomic_load(ins_blk + b0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kInsMask;
+        },
         [&](uint32_t i, uint32_t o) { ins_off[b0 + i] = o; }, ws);
     if (threadIdx.x == 0) host_store(host_counts + 2 * a.K + tt, tot);
   }
   if (tiled) pair_sort_tail(a, thist, so, host_counts, s_pb);
+  return cw;
 }
 
 // The last block: the next launch's query-block order, longest first.  Four duration
@@ -1969,13 +2011,14 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     return;
   }
   __syncthreads();  // every emit's LDS counts are in
-  if (threadIdx.x == 0)  // this block's insert count (k_insert offsets), agent-visible
-    __hip_atomic_store(ins_blk + bq, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // this block's insert count (k_insert offsets) and certified / warm queries, one
+  // agent-visible word summed by the last block (per-block adds into one launch-wide
+  // counter measured +9 us per C4 launch: every block's atomic on the same address)
 #if FMX_CERT_ANY
-  if (threadIdx.x == 0 && a.cert_cnt) {  // the launch's certified / warm totals (a warm launch only)
-    if (s_cert[0]) __hip_atomic_fetch_add(a.cert_cnt, s_cert[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (s_cert[2]) __hip_atomic_fetch_add(a.cert_cnt + 1, s_cert[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(ins_blk + bq, blk_word(s_ins, s_cert[0], s_cert[2]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  if (threadIdx.x == 0) __hip_atomic_store(ins_blk + bq, s_ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
   const int t = planar ? 0 : 1;
   if (a.sorted && a.tiles) {
@@ -2009,22 +2052,17 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     s_last = __hip_atomic_fetch_add(mticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  if (threadIdx.x == 0) {  // certified / warm queries of this launch -> host, counters zeroed
-    uint32_t nc = 0, nw = 0;
-    if (a.cert_cnt) {
-      nc = __hip_atomic_exchange(a.cert_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      nw = __hip_atomic_exchange(a.cert_cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    host_store(host_counts + 2 * a.K + 2, nc);
-    host_store(host_counts + 2 * a.K + 3, nw);
+  const uint2 cw = match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
+  if (threadIdx.x == 0) {  // certified / warm queries of this launch -> host
+    host_store(host_counts + 2 * a.K + 2, cw.x);
+    host_store(host_counts + 2 * a.K + 3, cw.y);
     if (a.prof_work) {  // the launch's probes / candidates / certified / warm -> its profiler slot
       host_store(a.prof_work, __hip_atomic_exchange(a.prof_acc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       host_store(a.prof_work + 1, __hip_atomic_exchange(a.prof_acc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      host_store(a.prof_work + 2, nc);
-      host_store(a.prof_work + 3, nw);
+      host_store(a.prof_work + 2, cw.x);
+      host_store(a.prof_work + 3, cw.y);
     }
   }
-  match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
   if (a.order_out) write_order(a, gridDim.x);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2568,8 +2606,6 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->work_blocks = nb;
   ensure_zeroed(c->mcnt, 2 * (size_t)K, st);
   ensure_zeroed(c->mticket, 1, st);
-  ensure_zeroed(c->mcert, 2, st);
-  a.cert_cnt = c->mcert.p;
   // heaviest-first dispatch: the order the last match on this map and query set wrote
   {
     const uint32_t nbq = (c->n_qpl + kQPB - 1) / kQPB + (c->n_qpt + kQPB - 1) / kQPB;
@@ -2697,7 +2733,6 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
 #if FMX_CERT_ANY
   a.cert_b2 = nullptr;
 #endif
-  a.cert_cnt = nullptr;
   a.order = nullptr;
   a.cost = nullptr;
   a.order_out = nullptr;
