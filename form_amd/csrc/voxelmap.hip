@@ -1886,7 +1886,9 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     w4[0] = make_uint4(tp, tc, mq, d0);
     w4[1] = make_uint4(t_begin, t_end, d1, d2);
     if (a.cost) __hip_atomic_store(a.cost + bq, t_end - t_begin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.prof_work) {  // this launch's totals (byte model), drained with the ticket's vmcnt(0)
+    // (a profiled launch's probe / candidate totals: the last block sums these words; the
+    // fused launch, whose blocks have no tail, adds them up as it goes)
+    if (FUSED && a.prof_work) {
       __hip_atomic_fetch_add(a.prof_acc, tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(a.prof_acc + 1, tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2053,12 +2055,21 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
   __syncthreads();
   if (!s_last) return;
   const uint2 cw = match_tail(a, mcnt, host_counts, ins_blk, ins_off, thist, so);
+  uint2 pc = make_uint2(0u, 0u);
+  if (a.prof_work) {  // profiled: the blocks' probe / candidate words, summed
+    uint32_t tp = 0, tc = 0;
+    for (uint32_t b = threadIdx.x; b < gridDim.x; b += kMatchThreads) {
+      tp += __hip_atomic_load(work + kWorkWords * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tc += __hip_atomic_load(work + kWorkWords * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    pc = block_sum2(tp, tc);
+  }
   if (threadIdx.x == 0) {  // certified / warm queries of this launch -> host
     host_store(host_counts + 2 * a.K + 2, cw.x);
     host_store(host_counts + 2 * a.K + 3, cw.y);
     if (a.prof_work) {  // the launch's probes / candidates / certified / warm -> its profiler slot
-      host_store(a.prof_work, __hip_atomic_exchange(a.prof_acc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      host_store(a.prof_work + 1, __hip_atomic_exchange(a.prof_acc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      host_store(a.prof_work, pc.x);
+      host_store(a.prof_work + 1, pc.y);
       host_store(a.prof_work + 2, cw.x);
       host_store(a.prof_work + 3, cw.y);
     }
