@@ -35,5 +35,7 @@ else
   python tools/stats_fmx.py $(find $D/prof -name "*kernel_stats.csv" | head -1) > $D/kernel_stats_fmx.csv
   head -12 $D/kernel_stats_fmx.csv
   CPATH="c4 c2" PMC=0 PART=scan bash tools/gpu_r5_evidence.sh || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || { tail -20 $D/smoke.log; exit 1; }
+  tail -3 $D/smoke.log
 fi
 echo END-DONE
