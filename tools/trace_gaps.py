@@ -16,8 +16,10 @@ print("kernels:", len(ev))
 # steps start at the extraction kernel
 starts = [i for i, e in enumerate(ev) if "k_extract_rows" in e[2]]
 print("steps seen:", len(starts))
-if len(starts) >= 3:
-    a, b = starts[-3], starts[-2]
+# argv[2]: which step to print, counted from the end (default 3: the third-to-last start)
+back = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+if len(starts) >= back:
+    a, b = starts[-back], starts[-back + 1]
     seg = ev[a:b]
     t0 = seg[0][0]
     span = ev[b][0] - t0
