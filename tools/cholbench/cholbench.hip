@@ -137,6 +137,134 @@ __global__ __launch_bounds__(kThreads) void k_chol(const double* __restrict__ A,
   }
 }
 
+
+// Version 2 of the factor: the diagonal block's column step as ONE wave-synchronous
+// pass (the rank-1 update from the unscaled column, scaled by 1 / L_jj, then the column
+// scaled: every lane's loads precede its stores), the 16 x 16 inverse of the diagonal
+// factor by 16 lanes (one column each), and the panel rows as MFMA tiles L21 = A21 X^T.
+__global__ __launch_bounds__(kThreads) void k_chol2(const double* __restrict__ A, const double* __restrict__ g,
+                                                    double* __restrict__ x, int D, unsigned long long* stamps) {
+  extern __shared__ double L[];  // [kMax][kLd]
+  __shared__ double s_rd[kMax];
+  __shared__ double s_x[16][17];  // X = L11^-1 (lower)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int Dp = (D + 15) & ~15;
+  for (int e = tid; e < Dp * Dp; e += kThreads) {
+    const int i = e / Dp, j = e % Dp;
+    L[i * kLd + j] = (i < D && j < D) ? A[(size_t)i * D + j] : (i == j ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int k0 = 0; k0 < Dp; k0 += 16) {
+    if (w == 0) {
+      for (int j = 0; j < 16; ++j) {
+        const int c = k0 + j;
+        const double piv = L[c * kLd + c];
+        const double rp = 1.0 / piv;
+        double upd[4], lij = 0.0;
+        int ii[4], mm[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = lane + 64 * q, i = e >> 4, m = e & 15;
+          ii[q] = i;
+          mm[q] = m;
+          upd[q] = (m > j && i >= m) ? L[(k0 + i) * kLd + c] * L[(k0 + m) * kLd + c] : 0.0;
+        }
+        if (lane < 16 && lane > j) lij = L[(k0 + lane) * kLd + c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (mm[q] > j && ii[q] >= mm[q]) L[(k0 + ii[q]) * kLd + k0 + mm[q]] -= upd[q] * rp;
+        const double d = sqrt(piv), rd = 1.0 / d;
+        if (lane < 16 && lane > j) L[(k0 + lane) * kLd + c] = lij * rd;
+        if (lane == j) {
+          L[c * kLd + c] = d;
+          s_rd[c] = rd;
+        }
+        wave_lds_sync();
+      }
+      if (lane < 16) {  // column `lane` of X = L11^-1: forward substitution
+        double xv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          double s = i == lane ? 1.0 : 0.0;
+#pragma unroll
+          for (int k = 0; k < i; ++k) s -= L[(k0 + i) * kLd + k0 + k] * xv[k];
+          xv[i] = s * s_rd[k0 + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s_x[i][lane] = xv[i];
+      }
+    }
+    __syncthreads();
+    const int T = (Dp - k0 - 16) / 16;
+    for (int t = w; t < T; t += kThreads / 64) {  // panel tile t: L21 rows r0.. = A21 X^T
+      const int r0 = k0 + 16 + 16 * t;
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      double a[4], b[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {  // A[i][k] = A21[r0 + i][k0 + k], B[k][j] = X[j][k]
+        const int k = 4 * kk + (lane >> 4);
+        a[kk] = L[(r0 + (lane & 15)) * kLd + k0 + k];
+        b[kk] = s_x[lane & 15][k];
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk], b[kk], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L[(r0 + (lane >> 4) + 4 * r) * kLd + k0 + (lane & 15)] = acc[r];
+    }
+    __syncthreads();
+    const int ntiles = T * (T + 1) / 2;
+    for (int t = w; t < ntiles; t += kThreads / 64) {
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= t) ++I;
+      const int J = t - I * (I + 1) / 2;
+      const int r0 = k0 + 16 + 16 * I, c0 = k0 + 16 + 16 * J;
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      double a[4], b[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = k0 + 4 * kk + (lane >> 4);
+        a[kk] = L[(r0 + (lane & 15)) * kLd + k];
+        b[kk] = L[(c0 + (lane & 15)) * kLd + k];
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk], b[kk], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L[(r0 + (lane >> 4) + 4 * r) * kLd + c0 + (lane & 15)] -= acc[r];
+    }
+    __syncthreads();
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (w == 0) {
+    double b0 = lane < D ? g[lane] : 0.0, b1 = lane + 64 < D ? g[lane + 64] : 0.0;
+    for (int j = 0; j < Dp; ++j) {
+      const double yj = __shfl(j < 64 ? b0 : b1, j & 63) * s_rd[j];
+      if (lane == (j & 63)) {
+        if (j < 64) b0 = yj;
+        else b1 = yj;
+      }
+      if (lane > j) b0 -= L[lane * kLd + j] * yj;
+      if (lane + 64 > j && lane + 64 < Dp) b1 -= L[(lane + 64) * kLd + j] * yj;
+    }
+    for (int j = Dp - 1; j >= 0; --j) {
+      const double xj = __shfl(j < 64 ? b0 : b1, j & 63) * s_rd[j];
+      if (lane == (j & 63)) {
+        if (j < 64) b0 = xj;
+        else b1 = xj;
+      }
+      if (lane < j) b0 -= L[j * kLd + lane] * xj;
+      if (lane + 64 < j) b1 -= L[j * kLd + lane + 64] * xj;
+    }
+    if (lane < D) x[lane] = b0;
+    if (lane + 64 < D) x[lane + 64] = b1;
+  }
+  const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) {
+    stamps[0] = t1 - t0;
+    stamps[1] = t2 - t1;
+  }
+}
+
 static void host_solve(const std::vector<double>& A, const std::vector<double>& g, std::vector<double>& x, int D) {
   std::vector<double> L(A);
   for (int j = 0; j < D; ++j) {
@@ -166,10 +294,13 @@ static void host_solve(const std::vector<double>& A, const std::vector<double>& 
 int main() {
   const size_t smem = (size_t)kMax * kLd * sizeof(double);
   CK(hipFuncSetAttribute((const void*)k_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  CK(hipFuncSetAttribute((const void*)k_chol2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
   std::mt19937_64 rng(7);
   std::normal_distribution<double> nd;
-  printf("D,factor_us,solves_us,launch_to_done_us,max_rel_err\n");
+  printf("version,D,factor_us,solves_us,launch_to_done_us,max_rel_err\n");
+  for (int ver = 1; ver <= 2; ++ver)
   for (int D : {72, 108, 126}) {
+    auto kern = ver == 1 ? k_chol : k_chol2;
     std::vector<double> M((size_t)D * D), A((size_t)D * D, 0.0), g(D), xr, xg(D);
     for (auto& v : M) v = nd(rng);
     for (int i = 0; i < D; ++i)
@@ -188,7 +319,7 @@ int main() {
     CK(hipMalloc(&ds, 16));
     CK(hipMemcpy(dA, A.data(), A.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dg, g.data(), D * 8, hipMemcpyHostToDevice));
-    for (int it = 0; it < 20; ++it) hipLaunchKernelGGL(k_chol, dim3(1), dim3(kThreads), smem, 0, dA, dg, dx, D, ds);
+    for (int it = 0; it < 20; ++it) hipLaunchKernelGGL(kern, dim3(1), dim3(kThreads), smem, 0, dA, dg, dx, D, ds);
     CK(hipDeviceSynchronize());
     // launch-to-completion, one at a time (what an LM step would pay per trial)
     hipEvent_t e0, e1;
@@ -198,7 +329,7 @@ int main() {
     double tot = 0;
     for (int it = 0; it < N; ++it) {
       CK(hipEventRecord(e0, 0));
-      hipLaunchKernelGGL(k_chol, dim3(1), dim3(kThreads), smem, 0, dA, dg, dx, D, ds);
+      hipLaunchKernelGGL(kern, dim3(1), dim3(kThreads), smem, 0, dA, dg, dx, D, ds);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms = 0;
@@ -210,7 +341,7 @@ int main() {
     CK(hipMemcpy(xg.data(), dx, D * 8, hipMemcpyDeviceToHost));
     double err = 0;
     for (int i = 0; i < D; ++i) err = std::fmax(err, std::fabs(xg[i] - xr[i]) / (std::fabs(xr[i]) + 1e-300));
-    printf("%d,%.2f,%.2f,%.2f,%.2e\n", D, st[0] * 0.01, st[1] * 0.01, tot / N * 1e3, err);
+    printf("v%d,%d,%.2f,%.2f,%.2f,%.2e\n", ver, D, st[0] * 0.01, st[1] * 0.01, tot / N * 1e3, err);
     fflush(stdout);
     CK(hipFree(dA));
     CK(hipFree(dg));
