@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kThreads) void k_chol(const double* __restrict__ A,
     L[i * kLd + j] = (i < D && j < D) ? A[(size_t)i * D + j] : (i == j ? 1.0 : 0.0);
   }
   __syncthreads();
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
   for (int k0 = 0; k0 < Dp; k0 += 16) {
     if (w == 0) {  // the 16 x 16 diagonal block, column by column (lower part only)
       for (int j = 0; j < 16; ++j) {
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kThreads) void k_chol(const double* __restrict__ A,
     }
     __syncthreads();
   }
-  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
   if (w == 0) {  // L y = g, then L^T x = y; lane l holds entries l and l + 64
     double b0 = lane < D ? g[lane] : 0.0, b1 = lane + 64 < D ? g[lane + 64] : 0.0;
     for (int j = 0; j < Dp; ++j) {
@@ -134,6 +134,7 @@ __global__ __launch_bounds__(kThreads) void k_chol(const double* __restrict__ A,
   if (tid == 0) {
     stamps[0] = t1 - t0;
     stamps[1] = t2 - t1;
+    stamps[2] = c1 - c0;
   }
 }
 
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(kThreads) void k_chol2(const double* __restrict__ A
     L[i * kLd + j] = (i < D && j < D) ? A[(size_t)i * D + j] : (i == j ? 1.0 : 0.0);
   }
   __syncthreads();
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
   for (int k0 = 0; k0 < Dp; k0 += 16) {
     if (w == 0) {
       for (int j = 0; j < 16; ++j) {
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(kThreads) void k_chol2(const double* __restrict__ A
     }
     __syncthreads();
   }
-  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
   if (w == 0) {
     double b0 = lane < D ? g[lane] : 0.0, b1 = lane + 64 < D ? g[lane + 64] : 0.0;
     for (int j = 0; j < Dp; ++j) {
@@ -262,6 +263,7 @@ __global__ __launch_bounds__(kThreads) void k_chol2(const double* __restrict__ A
   if (tid == 0) {
     stamps[0] = t1 - t0;
     stamps[1] = t2 - t1;
+    stamps[2] = c1 - c0;
   }
 }
 
@@ -297,7 +299,7 @@ int main() {
   CK(hipFuncSetAttribute((const void*)k_chol2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
   std::mt19937_64 rng(7);
   std::normal_distribution<double> nd;
-  printf("version,D,factor_us,solves_us,launch_to_done_us,max_rel_err\n");
+  printf("version,D,factor_us,solves_us,launch_to_done_us,max_rel_err,factor_core_clocks,core_MHz\n");
   for (int ver = 1; ver <= 2; ++ver)
   for (int D : {72, 108, 126}) {
     auto kern = ver == 1 ? k_chol : k_chol2;
@@ -316,7 +318,7 @@ int main() {
     CK(hipMalloc(&dA, A.size() * 8));
     CK(hipMalloc(&dg, D * 8));
     CK(hipMalloc(&dx, D * 8));
-    CK(hipMalloc(&ds, 16));
+    CK(hipMalloc(&ds, 24));
     CK(hipMemcpy(dA, A.data(), A.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dg, g.data(), D * 8, hipMemcpyHostToDevice));
     for (int it = 0; it < 20; ++it) hipLaunchKernelGGL(kern, dim3(1), dim3(kThreads), smem, 0, dA, dg, dx, D, ds);
@@ -336,12 +338,13 @@ int main() {
       CK(hipEventElapsedTime(&ms, e0, e1));
       tot += ms;
     }
-    unsigned long long st[2];
-    CK(hipMemcpy(st, ds, 16, hipMemcpyDeviceToHost));
+    unsigned long long st[3];
+    CK(hipMemcpy(st, ds, 24, hipMemcpyDeviceToHost));
     CK(hipMemcpy(xg.data(), dx, D * 8, hipMemcpyDeviceToHost));
     double err = 0;
     for (int i = 0; i < D; ++i) err = std::fmax(err, std::fabs(xg[i] - xr[i]) / (std::fabs(xr[i]) + 1e-300));
-    printf("v%d,%d,%.2f,%.2f,%.2f,%.2e\n", ver, D, st[0] * 0.01, st[1] * 0.01, tot / N * 1e3, err);
+    printf("v%d,%d,%.2f,%.2f,%.2f,%.2e,%llu,%.0f\n", ver, D, st[0] * 0.01, st[1] * 0.01, tot / N * 1e3, err, st[2],
+           st[2] / (st[0] * 0.01));
     fflush(stdout);
     CK(hipFree(dA));
     CK(hipFree(dg));
