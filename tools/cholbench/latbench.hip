@@ -11,7 +11,8 @@
 
 constexpr int N = 4096;
 
-__global__ __launch_bounds__(256) void k_lat(int which, double* out, unsigned long long* dt) {
+__global__ __launch_bounds__(256) void k_lat(int which, double* out, unsigned long long* dt, int* gidx,
+                                             unsigned* host_word) {
   __shared__ int s_idx[256];
   __shared__ double s_v[256];
   const int tid = threadIdx.x;
@@ -41,6 +42,21 @@ __global__ __launch_bounds__(256) void k_lat(int which, double* out, unsigned lo
     for (int i = 0; i < N; ++i) x = __shfl(x, (threadIdx.x + 1) & 63) + 1.0;
   } else if (which == 6) {  // fp64 FMA chain
     for (int i = 0; i < N; ++i) x = fma(x, 0.999, 1e-3);
+  } else if (which == 7) {  // dependent global loads (small table: cache-resident)
+    for (int i = 0; i < N; ++i) idx = gidx[idx];
+    x += idx;
+  } else if (which == 8) {  // dependent agent-scope atomic loads (as the last-block tails read)
+    for (int i = 0; i < N; ++i) idx = __hip_atomic_load(gidx + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x += idx;
+  } else if (which == 9) {  // dependent agent-scope fetch-adds (tickets)
+    for (int i = 0; i < N; ++i)
+      idx = __hip_atomic_fetch_add(gidx + 256 + (idx & 255), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 255;
+    x += idx;
+  } else if (which == 10) {  // system-scope store to host memory, waited for (a completion word)
+    for (int i = 0; i < N / 16; ++i) {
+      __hip_atomic_store(host_word + tid, (unsigned)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   out[tid] = x;
@@ -49,19 +65,28 @@ __global__ __launch_bounds__(256) void k_lat(int which, double* out, unsigned lo
 
 int main() {
   const char* names[] = {"lds_load_chain", "barrier", "lds_store_barrier_load_barrier", "f64_sqrt_chain",
-                         "f64_recip_chain", "shfl_chain", "f64_fma_chain"};
+                         "f64_recip_chain", "shfl_chain", "f64_fma_chain", "global_load_chain",
+                         "agent_atomic_load_chain", "agent_fetch_add_chain", "host_store_acked"};
   double* dout;
   unsigned long long* ddt;
+  int* gidx;
+  unsigned* hw;
   if (hipMalloc(&dout, 256 * 8) != hipSuccess || hipMalloc(&ddt, 8) != hipSuccess) return 1;
+  if (hipMalloc(&gidx, 512 * 4) != hipSuccess || hipHostMalloc(&hw, 256 * 4, hipHostMallocDefault) != hipSuccess) return 1;
+  {
+    int h[512];
+    for (int i = 0; i < 512; ++i) h[i] = i < 256 ? (i + 1) & 255 : 0;
+    if (hipMemcpy(gidx, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) return 1;
+  }
   printf("step,ns_per_step\n");
-  for (int w = 0; w < 7; ++w) {
+  for (int w = 0; w < 11; ++w) {
     unsigned long long dt = 0;
     for (int rep = 0; rep < 3; ++rep) {  // the last of three back-to-back launches
-      hipLaunchKernelGGL(k_lat, dim3(1), dim3(256), 0, 0, w, dout, ddt);
+      hipLaunchKernelGGL(k_lat, dim3(1), dim3(256), 0, 0, w, dout, ddt, gidx, hw);
       if (hipDeviceSynchronize() != hipSuccess) return 1;
     }
     if (hipMemcpy(&dt, ddt, 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    printf("%s,%.2f\n", names[w], dt * 10.0 / N);
+    printf("%s,%.2f\n", names[w], dt * 10.0 / (w == 10 ? N / 16 : N));
   }
   return 0;
 }
