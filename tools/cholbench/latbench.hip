@@ -63,6 +63,41 @@ __global__ __launch_bounds__(256) void k_lat(int which, double* out, unsigned lo
   if (tid == 0) *dt = t1 - t0;
 }
 
+
+// The last-block pattern of k_match / k_win_linearize: every block stores one word per
+// thread (agent scope, as the kernels' per-block counts), waits for it, takes a ticket;
+// the last block then reads one word of every block with agent-scope loads (one round) —
+// words written by blocks on the other XCDs, whose L2s are not this one's.  Reported:
+// the last block's read round (us) and the ticket-to-end span of the last block.
+__global__ __launch_bounds__(256) void k_tail(unsigned* words, unsigned* ticket, unsigned long long* dt, int rounds) {
+  const int tid = threadIdx.x;
+  __hip_atomic_store(words + (size_t)blockIdx.x * 256 + tid, blockIdx.x + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int s_last;
+  if (tid == 0) s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned acc = 0;
+  const unsigned R = (gridDim.x + 255) / 256;  // blocks per thread, as the match tail's R-runs
+  for (int r = 0; r < rounds; ++r) {  // dependent rounds: thread t reads word 0 of blocks [R t, R t + R)
+    unsigned part = 0;
+    for (unsigned u = 0; u < R; ++u) {
+      const unsigned b = tid * R + u;
+      if (b < gridDim.x)
+        part += __hip_atomic_load(words + (size_t)b * 256 + (acc & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    acc += part & 1;
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) {
+    dt[0] = t1 - t0;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (acc == 0xFFFFFFFFu) words[0] = acc;
+}
+
 int main() {
   const char* names[] = {"lds_load_chain", "barrier", "lds_store_barrier_load_barrier", "f64_sqrt_chain",
                          "f64_recip_chain", "shfl_chain", "f64_fma_chain", "global_load_chain",
@@ -87,6 +122,25 @@ int main() {
     }
     if (hipMemcpy(&dt, ddt, 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
     printf("%s,%.2f\n", names[w], dt * 10.0 / (w == 10 ? N / 16 : N));
+  }
+  // last-block read rounds over words written by 1200 blocks (C4 match: ~1215 blocks)
+  {
+    unsigned *words, *ticket;
+    unsigned long long* dt2;
+    const int nb = 1200;
+    if (hipMalloc(&words, (size_t)nb * 256 * 4) != hipSuccess || hipMalloc(&ticket, 4) != hipSuccess ||
+        hipMalloc(&dt2, 8) != hipSuccess)
+      return 1;
+    if (hipMemset(ticket, 0, 4) != hipSuccess) return 1;
+    for (int rounds : {1, 4}) {
+      unsigned long long v = 0;
+      for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL(k_tail, dim3(nb), dim3(256), 0, 0, words, ticket, dt2, rounds);
+        if (hipDeviceSynchronize() != hipSuccess) return 1;
+      }
+      if (hipMemcpy(&v, dt2, 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+      printf("last_block_%d_rounds_over_%d_blocks_us,%.2f\n", rounds, nb, v * 0.01);
+    }
   }
   return 0;
 }
