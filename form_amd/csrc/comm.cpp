@@ -95,6 +95,7 @@ void comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank) {
   ncclComm_t comm = nullptr;
   check(rccl().comm_init_rank(&comm, nranks, u, rank), "ncclCommInitRank");
   c->comm = comm;
+  c->comm_failed = false;
   c->comm_size = nranks;
   c->comm_rank = rank;
 }
@@ -166,8 +167,9 @@ bool withhold_flag() {  // test switch: see k_publish_sums
 // the collective, so wait_flag's stream check never fires): here the wait polls
 // ncclCommGetAsyncError and is bounded by FMX_COMM_TIMEOUT_S.  On either, the
 // communicator is aborted (ncclCommAbort makes the RCCL kernels exit), the stream is
-// drained, and the call fails with FMX_E_RCCL; the context stays usable without a
-// communicator.
+// drained, and the call fails with FMX_E_RCCL.  The context then refuses every sharded
+// call (comm_check) until fmx_comm_init attaches a new communicator: its queries are a
+// shard, so a rank-local system would silently stand in for the global one.
 void comm_wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq, uint32_t* hold) {
   HostScope hs(1);
   ++c->host_waits;
@@ -206,6 +208,7 @@ void comm_wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq, uint32
   c->comm = nullptr;
   c->comm_size = 1;
   c->comm_rank = 0;
+  c->comm_failed = true;
   if (rccl().comm_abort) (void)rccl().comm_abort(comm);
   else (void)rccl().comm_destroy(comm);
   (void)hipStreamSynchronize(c->stream);
@@ -213,6 +216,12 @@ void comm_wait_flag(fmx_ctx* c, const volatile uint32_t* f, uint32_t seq, uint32
 }
 
 }  // namespace
+
+void comm_check(const fmx_ctx* c) {
+  if (c->comm_failed)
+    throw StatusError(FMX_E_RCCL, "the communicator was aborted by an earlier failure; sharded calls fail until "
+                                  "fmx_comm_init attaches a new one");
+}
 
 void comm_allreduce_publish(fmx_ctx* c, double* dev, size_t n, HBuf<double>& host) {
   if (n > 0xFFFFFFFFu) throw StatusError(FMX_E_INVAL, "all-reduce too large");

@@ -1489,16 +1489,10 @@ static void launch_rows(fmx_ctx* c, const float4* d_scan, ExArgs a, int r0, int 
   FMX_HIP(hipGetLastError());
 }
 
-void extract_rows(fmx_ctx* c, const float4* d_scan, int R, int C, int r0, int r1, hipStream_t st) {
-  launch_rows(c, d_scan, extract_setup(c, R, C), r0, r1, st);
-}
-
-// rows_done: rows [0, rows_done) were already extracted by earlier extract_rows launches
-// on the same stream (a staged host scan: each line as soon as its bytes have landed)
 ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
-                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq, int rows_done) {
+                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq) {
   ExArgs a = extract_setup(c, R, C);
-  launch_rows(c, d_scan, a, rows_done, R, st);
+  launch_rows(c, d_scan, a, 0, R, st);
   a.row0 = 0;
   const size_t N = (size_t)R * C;
   const int nslots = R * a.cap_pl;
@@ -1590,11 +1584,10 @@ void extract_collect(fmx_ctx* c, const ExLaunch& L, fmx_feature_counts* out) {
 }
 
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
-                 const std::function<void()>& while_waiting, int rows_done) {
+                 const std::function<void()>& while_waiting) {
   c->h_u32.ensure(8);
   const uint32_t seq = next_flag(c);
-  const ExLaunch L =
-      extract_launch(c, d_scan, R, C, c->stream, c->h_u32.p, c->h_u32.d, c->h_flag.p, c->h_flag.d, seq, rows_done);
+  const ExLaunch L = extract_launch(c, d_scan, R, C, c->stream, c->h_u32.p, c->h_u32.d, c->h_flag.p, c->h_flag.d, seq);
   if (while_waiting) while_waiting();
   extract_collect(c, L, out);
 }

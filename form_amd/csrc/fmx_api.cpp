@@ -8,9 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
-#include <execinfo.h>
 #include <functional>
-#include <csignal>
 #include <unistd.h>
 #include <map>
 #include <new>
@@ -196,12 +194,6 @@ struct KeyScanner {
     return marg;
   }
 };
-
-// FMX_NO_FUSED (A/B diagnostic): never defer fmx_match, so nothing runs fused
-bool no_fused() {
-  static const bool v = std::getenv("FMX_NO_FUSED") != nullptr;
-  return v;
-}
 
 // A deferred fmx_match (ctx->lazy): launched now, before anything reads or changes
 // the state it depends on.
@@ -396,17 +388,6 @@ uint32_t stage_dmas() {
   static const uint32_t v = (uint32_t)std::max(1, env_int("FMX_STAGE_DMAS", 4));
   return v;
 }
-// FMX_HOST_PAGEABLE (A/B diagnostic): the pre-round-4 path, one pageable hipMemcpyAsync
-bool host_pageable() {
-  static const bool v = std::getenv("FMX_HOST_PAGEABLE") != nullptr;
-  return v;
-}
-// Staged host scans cross PCIe as packed x, y, z (12 of 16 bytes; k_unpack_xyz restores
-// the layout on the device); FMX_STAGE_PACK=0 sends the float4 points as they are.
-bool stage_pack() {
-  static const bool v = env_int("FMX_STAGE_PACK", 1) != 0;
-  return v;
-}
 // Pinned staging buffers of `bytes` each (grown only; growing drains every stream and
 // staging request first, since DMAs may still read the old ones).
 void pinned_ensure(fmx_ctx* c, size_t bytes) {
@@ -429,7 +410,7 @@ void pinned_ensure(fmx_ctx* c, size_t bytes) {
 void stage_submit(fmx_ctx* c, StageReq& r, const void* src, void* dst, size_t bytes) {
   c->stager.retire(&r);
   c->stager.start(stage_threads());
-  r.reset(src, dst, bytes, stage_chunk(), stage_pack());
+  r.reset(src, dst, bytes, stage_chunk(), /*pack=*/true);  // x, y, z only (stage_host_scan)
   if (c->stager.threads() > 0) c->stager.submit(&r);
 }
 // Every chunk of r copied (this thread helps) and r released by the helpers.
@@ -454,24 +435,14 @@ bool host_pinned(const void* p, size_t bytes) {
   }
   return true;
 }
-// FMX_STAGE_ROWS=1 (A/B): extract a staged host scan's lines as each DMA piece lands
-// instead of once all of it has.  Measured round 5 (profiles/r5_ab_host_input.txt):
-// pageable sequential 0.82-0.84 -> 0.74-0.80 of device-sequential with it — the small
-// per-piece launches and unpacks cost the staging thread more than the overlap gains.
-bool stage_rows() {
-  static const bool v = env_int("FMX_STAGE_ROWS", 0) != 0;
-  return v;
-}
 // A host scan for the sequential path, into c->scan on the context stream: a pinned one
-// is DMA'd directly; a pageable one is staged by the helpers and this thread, each
-// completed quarter DMA'd right away, unpacked, and its complete lines (R x C scan) handed
-// to k_extract_rows while the next quarter is still being staged.  *rows_done = the lines
-// whose extraction is already queued.
-const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n, int R, int C, int* rows_done) {
+// is DMA'd directly; a pageable one is staged by the helpers and this thread as packed
+// x, y, z (12 of every 16 bytes: a PointXYZf's pad is always 0, utils.hpp:38-46), each
+// completed quarter DMA'd right away, then unpacked on the device (k_unpack_xyz).
+const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n) {
   const size_t bytes = n * sizeof(float4);
-  *rows_done = 0;
   c->scan.ensure(n);
-  if (host_pageable() || host_pinned(xyzw, bytes)) {
+  if (host_pinned(xyzw, bytes)) {
     FMX_HIP(hipMemcpyAsync(c->scan.p, xyzw, bytes, hipMemcpyHostToDevice, c->stream));
     return c->scan.p;
   }
@@ -480,38 +451,23 @@ const float4* stage_host_scan(fmx_ctx* c, const float* xyzw, size_t n, int R, in
   // the host waited for: it has completed
   StageReq& r = c->st_seq;
   stage_submit(c, r, xyzw, c->pin_seq, bytes);
-  // packed: the DMA lands in scan3 and k_unpack_xyz writes c->scan; offsets scale by 3/4
-  const bool packed = r.pack3;
-  if (packed) c->scan3.ensure(3 * n);
-  const bool rows = stage_rows();
-  if (rows) extract_rows(c, c->scan.p, R, C, 0, 0, c->stream);  // every scratch buffer before the first DMA
-  uint8_t* dev = packed ? reinterpret_cast<uint8_t*>(c->scan3.p) : reinterpret_cast<uint8_t*>(c->scan.p);
-  auto dsz = [&](size_t x) { return packed ? x / 16 * 12 : x; };
+  c->scan3.ensure(3 * n);
+  uint8_t* dev = reinterpret_cast<uint8_t*>(c->scan3.p);
   const uint32_t step = std::max<uint32_t>(1, (r.nchunks + stage_dmas() - 1) / stage_dmas());
   uint32_t issued = 0;
-  size_t pts = 0;  // points on the device (unpacked)
   while (issued < r.nchunks) {
     uint32_t ready = issued;
     while (ready < r.nchunks && r.chunk_done(ready)) ++ready;
     if (ready - issued >= step || ready == r.nchunks) {
-      const size_t s0 = (size_t)issued * r.chunk, s1 = std::min(bytes, (size_t)ready * r.chunk);
-      const size_t a = dsz(s0), b = dsz(s1);
+      const size_t a = (size_t)issued * r.chunk / 16 * 12, b = std::min(bytes, (size_t)ready * r.chunk) / 16 * 12;
       FMX_HIP(hipMemcpyAsync(dev + a, c->pin_seq + a, b - a, hipMemcpyHostToDevice, c->stream));
       issued = ready;
-      if (rows) {
-        const size_t p1 = s1 / sizeof(float4);
-        if (packed) unpack_xyz(c, c->scan3.p + 3 * pts, c->scan.p + pts, p1 - pts, c->stream);
-        pts = p1;
-        const int done = (int)(pts / (size_t)C);
-        extract_rows(c, c->scan.p, R, C, *rows_done, done, c->stream);
-        *rows_done = done;
-      }
       continue;
     }
     if (!r.work_one()) std::this_thread::yield();  // help; then wait for the helpers' chunks
   }
   c->stager.retire(&r);
-  if (packed && !rows) unpack_xyz(c, c->scan3.p, c->scan.p, n, c->stream);
+  unpack_xyz(c, c->scan3.p, c->scan.p, n, c->stream);
   return c->scan.p;
 }
 
@@ -527,14 +483,8 @@ void do_extract(fmx_ctx* c, const float* xyzw, size_t n, uint64_t scan, int on_d
   if (C > 4096 || C < 2 * E.neighbor_points + 2 || E.num_sectors == 0 || E.num_sectors > C)
     throw StatusError(FMX_E_INVAL, "unsupported scan geometry (columns must be <= 4096)");
   pf_drop(c);  // a queued extraction shares the scratch buffers
-  const float4* d;
-  int rows_done = 0;
-  if (on_dev) {
-    d = reinterpret_cast<const float4*>(xyzw);
-  } else {
-    d = stage_host_scan(c, xyzw, n, (int)R, (int)C, &rows_done);
-  }
-  run_extract(c, d, (int)R, (int)C, out, while_waiting, rows_done);
+  const float4* d = on_dev ? reinterpret_cast<const float4*>(xyzw) : stage_host_scan(c, xyzw, n);
+  run_extract(c, d, (int)R, (int)C, out, while_waiting);
   c->q_scan = scan;
   c->have_queries = true;
   ++c->warm_gen;  // a new query set: no warm start from an earlier match
@@ -585,13 +535,10 @@ void pf_launch(fmx_ctx* c, bool force = true) {
     c->pf_scan.ensure(c->ann_n);
     if (c->ann_pinned) {
       FMX_HIP(hipMemcpyAsync(c->pf_scan.p, c->ann_ptr, c->ann_n * sizeof(float4), hipMemcpyHostToDevice, c->side2));
-    } else if (c->st_pf[c->ann_slot].pack3) {
+    } else {  // staged as packed x, y, z
       c->pf_scan3.ensure(3 * c->ann_n);
       FMX_HIP(hipMemcpyAsync(c->pf_scan3.p, c->pin_pf[c->ann_slot], c->ann_n * 12, hipMemcpyHostToDevice, c->side2));
       unpack_xyz(c, c->pf_scan3.p, c->pf_scan.p, c->ann_n, c->side2);
-    } else {
-      FMX_HIP(hipMemcpyAsync(c->pf_scan.p, c->pin_pf[c->ann_slot], c->ann_n * sizeof(float4), hipMemcpyHostToDevice,
-                             c->side2));
     }
     d = c->pf_scan.p;
   }
@@ -599,7 +546,7 @@ void pf_launch(fmx_ctx* c, bool force = true) {
   try {
     const uint32_t seq = ++c->pf_seq;
     c->pf_L = extract_launch(c, d, (int)E.num_rows, (int)E.num_columns, c->side2, c->h_pf.p, c->h_pf.d, c->h_pf.p + 4,
-                             c->h_pf.d + 4, seq, 0);
+                             c->h_pf.d + 4, seq);
   } catch (...) {
     swap_query_set(c);
     throw;
@@ -938,25 +885,13 @@ bool trace_on() {
     }                                     \
   } while (0)
 
-// The smoother's LMs linearize either every trial on the device from the rows
-// (k_win_linearize over the sorted match / the window store) or from the pair moments
-// (k_win_moments once per ICP iteration, host contractions, moments.cpp).
-// FMX_LIN_ROWS=1 / FMX_MOMENTS=1 choose (A/B); the default is kLinRowsDefault.
-constexpr bool kLinRowsDefault = true;
+// The smoother's LMs linearize every trial on the device from the rows (k_win_linearize
+// over the sorted match / the window store) — or, with FMX_MOMENTS=1 (opt-in; measured
+// neutral on C4 and slower on C2, DESIGN.md "pair moments"), from the pair moments
+// (k_win_moments once per ICP iteration, host contractions, moments.cpp) in the ICP loop
+// and from the stored pairs' moments in the final LM.
 bool lin_rows() {
-  static const bool v = std::getenv("FMX_MOMENTS") ? false : std::getenv("FMX_LIN_ROWS") ? true : kLinRowsDefault;
-  return v;
-}
-// FMX_NO_SPEC_MOMENTS=1 (A/B): a speculative match's pair moments are launched by the ICP
-// iteration that takes it instead of right behind the match
-bool spec_moments() {
-  static const bool v = std::getenv("FMX_NO_SPEC_MOMENTS") == nullptr;
-  return v;
-}
-// FMX_FULL_ROWS=1 (A/B): the final LM (every stored pair) linearizes on the device from
-// the window store's rows even when the ICP loop uses moments
-bool full_rows() {
-  static const bool v = std::getenv("FMX_FULL_ROWS") != nullptr;
+  static const bool v = std::getenv("FMX_MOMENTS") == nullptr;
   return v;
 }
 
@@ -979,7 +914,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
   if (!fast.keys.empty()) g.lins.push_back(&fast);
   std::vector<double> table;
   const bool mom = !lin_rows();
-  const bool mom_full = mom && !full_rows();  // the final LM from the stored pairs' moments too
+  const bool mom_full = mom;  // the final LM from the stored pairs' moments too
   std::vector<double> momv;                  // the current scan's pair moments (K x kMomPairD)
   std::vector<Pose> mref;                    // ... their reference poses: [k] pair k's X(i), [K] X(j)
   std::vector<const double*> mp;             // contraction arguments (moments.hpp)
@@ -1015,11 +950,9 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
         for (double v : xi) dn += v * v;
         last_likely = std::sqrt(dn) >= P.new_pose_threshold;
       }
-      static const bool spec_log = std::getenv("FMX_SPEC_LOG") != nullptr;  // diagnostic
-      if (spec_log && lc >= 0.0) fprintf(stderr, "spec it %u lin_change %.3e err %.3e rel %.3e\n", it, lc, ce, lc / ce);
       if (last_likely && it + 1 < P.max_num_rematches && std::memcmp(xj.m, before.m, sizeof(xj.m)) != 0) {
         FMX_TRACE_("  spec match\n");
-        if (mom && spec_moments()) {
+        if (mom) {
           // the next iteration's reference: its LM starts from the window values with
           // X(j) = this trial's (fast mode keeps only X(j), constraints.cpp:257-266)
           std::vector<double> ref(12 * ((size_t)K + 1));
@@ -1031,7 +964,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
         }
       }
     };
-    bool launched = false, ready = false, already = false;  // (moments: captured by the LM's callbacks below)
+    bool launched = false, ready = false;  // (moments: captured by the LM's callbacks below)
     if (mom) {
       // The pairs' moments at the LM's starting values: launched by the LM's first
       // linearization (split form: the host builds the base system and the non-pair
@@ -1053,12 +986,10 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
           mref[K] = x[slot.at(j)];
           for (int k = 0; k <= K; ++k) std::memcpy(&table[12 * k], mref[k].m, 12 * sizeof(double));
           momv.resize((size_t)std::max(K, 1) * kMomPairD);
-          static const bool eager = std::getenv("FMX_MOM_EAGER") != nullptr;  // diagnostic
           FMX_TRACE_("scan %llu it %u: moments launch K %d chunks %u\n", (unsigned long long)j, it, K, c->max_chunks);
-          win_moments_current(c, table.data(), eager ? momv.data() : nullptr);  // launch only; win_finish in lin_end
+          win_moments_current(c, table.data(), nullptr);  // launch only; win_finish in lin_end
           FMX_TRACE_("  launched\n");
           launched = true;
-          if (eager) already = true;
         }
         maybe_spec(x);
         mxi.resize(K);
@@ -1072,7 +1003,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
         HostScope hs(10);
         if (!ready) {
           FMX_TRACE_("  wait\n");
-          if (!already) win_finish(c, momv.data());
+          win_finish(c, momv.data());
           FMX_TRACE_("  moments in\n");
           match_counts_fetch(c, false);  // the match finished before the moments
           for (int k = 0; k < K; ++k)  // pairs without rows are never written by the kernel
@@ -1095,11 +1026,6 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
         FMX_TRACE_("  eval\n");
       };
       set_lin(g, lin_begin, lin_end);
-      static const bool nosplit = std::getenv("FMX_MOM_NOSPLIT") != nullptr;  // diagnostic
-      if (nosplit) {
-        g.lin_begin = nullptr;
-        g.lin_end = nullptr;
-      }
     } else {
       // split form: launch, the host assembles the non-pair terms, then wait (smoother.hpp)
       auto lin_begin = [&](const std::vector<Pose>& x) {
@@ -1131,15 +1057,11 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
     logmap(compose(inverse(before), after), xi);
     double dn = 0;
     for (double v : xi) dn += v * v;
-    {
-      static const bool spec_log = std::getenv("FMX_SPEC_LOG") != nullptr;  // diagnostic
-      if (spec_log) fprintf(stderr, "icp it %u lm_iters %d final %s\n", it, R.iters, std::sqrt(dn) < P.new_pose_threshold ? "converged" : "next");
-    }
     if (std::sqrt(dn) < P.new_pose_threshold) break;
     e.values[j] = after;  // update_current_pose
   }
-  // the last match is the scan's constraint set: into the window store (its pair
-  // moments, or its rows for FMX_LIN_ROWS)
+  // the last match is the scan's constraint set: into the window store (its rows, or
+  // its pair moments in FMX_MOMENTS mode)
   record_cons(c, e, j);
   if (mom_full) {
     for (uint32_t k = 0; k < c->K; ++k)
@@ -1496,7 +1418,7 @@ void register_scan(fmx_ctx* c, const float* xyzw, size_t n, int on_dev, fmx_feat
       map_inputs();
       FMX_HIP(hipStreamWaitEvent(c->stream, c->ev_join.last(), 0));
       if (!P.disable_smoothing) {
-        if (!lin_rows() && spec_moments()) {  // + the first ICP iteration's moments (its x0: the window values)
+        if (!lin_rows()) {  // + the first ICP iteration's moments (its x0: the window values)
           std::vector<double> ref(12 * ((size_t)c->K + 1));
           for (uint32_t k = 0; k < c->K; ++k) std::memcpy(&ref[12 * k], e.values.at(c->map_scans[k]).m, 12 * sizeof(double));
           std::memcpy(&ref[12 * (size_t)c->K], e.values.at(j).m, 12 * sizeof(double));
@@ -1623,23 +1545,9 @@ void fmx_default_params(fmx_params* p) {
   p->voxel_subdivision = 1;
 }
 
-// FMX_SEGV_TRACE (diagnostic): a native backtrace on SIGSEGV / SIGABRT, then the default action
-static void segv_trace(int sig) {
-  void* fr[64];
-  const int n = backtrace(fr, 64);
-  const char msg[] = "fmx: native backtrace\n";
-  (void)!write(2, msg, sizeof(msg) - 1);
-  backtrace_symbols_fd(fr, n, 2);
-  signal(sig, SIG_DFL);
-  raise(sig);
-}
 
 fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
   if (!p || !out) return FMX_E_INVAL;
-  if (std::getenv("FMX_SEGV_TRACE")) {
-    signal(SIGSEGV, segv_trace);
-    signal(SIGABRT, segv_trace);
-  }
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return FMX_E_HIP;
@@ -1726,7 +1634,7 @@ void fmx_destroy(fmx_ctx* c) {
   c->bpart.release(); c->ticket.release(); c->h_poses.release(); c->h_G.release(); c->h_i32.release();
   c->h_corr.release(); c->h_meta.release(); c->h_counts.release(); c->h_flag.release();
   c->mcnt.release(); c->mticket.release(); c->ins_blk.release(); c->ins_off.release();
-  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release(); c->mprof.release(); c->mord.release(); c->mcost.release();
+  c->fz_work.release(); c->fz_h_work.release(); c->fz_tickets.release(); c->mprof.release();
   c->cert_b2.release();
   {
     auto& S = c->spec;
@@ -1856,8 +1764,7 @@ fmx_status fmx_match(fmx_ctx* c, const double pose_j[12], double max_dist, uint3
     check_match_reach(c, max_dist, c->P.min_dist_map);
     // no count outputs on a large query set (the one-lane-per-query build): deferred,
     // so that fmx_linearize_matched at this pose can run fused with it
-    const bool defer = !cpl && !cpt && match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) == 1 &&
-                       !no_fused();
+    const bool defer = !cpl && !cpt && match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) == 1;
     if (defer) {
       c->lazy.pending = true;
       std::memcpy(c->lazy.pose, pose_j, sizeof(c->lazy.pose));
@@ -2007,7 +1914,7 @@ fmx_status fmx_register_points(fmx_ctx* c, const double pose_init[12], double ma
     if (!c->have_queries) throw StatusError(FMX_E_STATE, "no queries (fmx_extract or fmx_set_queries)");
     if (!pose_init || !pose_out) throw StatusError(FMX_E_INVAL, "null pose");
     if (!(max_dist > 0) || !(sigma > 0) || !(threshold >= 0)) throw StatusError(FMX_E_INVAL, "bad max_dist / sigma");
-    const bool fused = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) == 1 && !no_fused();
+    const bool fused = match_group_for((uint64_t)c->n_qpl + c->n_qpt, c->K) == 1;
     Pose T;
     std::memcpy(T.m, pose_init, sizeof(T.m));
     uint32_t it = 0;

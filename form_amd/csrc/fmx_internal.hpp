@@ -200,14 +200,9 @@ struct VoxMap {
   double4* nrm_p = nullptr;     // normals: nrm.p, or pos.p + 1 when interleaved
 };
 // Maps of at least this many records interleave positions and normals (voxelmap.hip,
-// rec_at); FMX_INTERLEAVE_MIN overrides (A/B), 0 = always.
-inline uint32_t interleave_min() {
-  static const uint32_t v = [] {
-    const char* e = std::getenv("FMX_INTERLEAVE_MIN");
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)(4u << 20);
-  }();
-  return v;
-}
+// rec_at).
+constexpr uint32_t kInterleaveMin = 4u << 20;
+inline uint32_t interleave_min() { return kInterleaveMin; }
 
 struct Seg {
   uint32_t off;       // first build-order record
@@ -474,9 +469,6 @@ struct fmx_ctx {
   uint32_t ins_tot[2] = {0, 0};                   // insert totals of the last match
   uint32_t cert_tot[2] = {0, 0};                  // ... its certified / warm query counts
   fmx::DBuf<uint32_t> mprof;                      // profiled match launches' probe / candidate sums (self-resetting)
-  fmx::DBuf<uint32_t> mord, mcost;                // heaviest-first query-block order + per-block durations (k_match)
-  uint64_t ord_gen = 0;                           // warm_gen when mord was written (0: none)
-  uint32_t ord_nb = 0;                            // ... for this many query blocks
   uint32_t match_nb_pl = 0, match_nb = 0;         // blocks of the last match
   uint32_t n_qo = 0;                              // queries of the last query-order match
   fmx::HBuf<uint32_t> h_flag;                     // mapped completion word (wait_flag)
@@ -513,6 +505,7 @@ struct fmx_ctx {
   // ---- multi-GPU exchange (comm.cpp): RCCL communicator, or null
   void* comm = nullptr;
   int comm_size = 1, comm_rank = 0;
+  bool comm_failed = false;  // an all-reduce failed and aborted the communicator (comm_check)
   fmx::DBuf<double> d_sum;  // device-side linearization sums all-reduced in place
   fmx::HBuf<uint32_t> h_hold;  // FMX_TEST_WITHHOLD_FLAG: the word that releases a withheld publish
 
@@ -767,13 +760,10 @@ namespace gl { FMX_VM_DECLS }
 int prof_ring_slot(fmx_ctx* c);
 // launchers (extract.hip / voxelmap.hip / linearize.hip)
 ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStream_t st, uint32_t* tot_h,
-                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq, int rows_done = 0);
-// k_extract_rows over lines [r0, r1) of an R x C scan (r0 == r1: only ensures the scratch
-// buffers); extract_launch(..., rows_done = r1) then queues the rest of the extraction
-void extract_rows(fmx_ctx* c, const float4* d_scan, int R, int C, int r0, int r1, hipStream_t st);
+                        uint32_t* tot_d, uint32_t* flag_h, uint32_t* flag_d, uint32_t seq);
 void extract_collect(fmx_ctx* c, const ExLaunch& L, fmx_feature_counts* out);
 void run_extract(fmx_ctx* c, const float4* d_scan, int R, int C, fmx_feature_counts* out,
-                 const std::function<void()>& while_waiting = nullptr, int rows_done = 0);
+                 const std::function<void()>& while_waiting = nullptr);
 // packed x, y, z (a staged host scan) -> float4 points with pad 0, on stream st
 void unpack_xyz(fmx_ctx* c, const float* d_packed, float4* d_out, size_t n, hipStream_t st);
 // st: stream to build on (default the context stream; register_scan uses the side
@@ -820,6 +810,8 @@ uint32_t map_snapshot(fmx_ctx* c, int t, const std::vector<uint64_t>& scans, con
 void comm_unique_id(uint8_t id[128]);
 void comm_init(fmx_ctx* c, const uint8_t id[128], int nranks, int rank);
 void comm_destroy(fmx_ctx* c);
+// FMX_E_RCCL after an aborted communicator, until fmx_comm_init (every sharded entry)
+void comm_check(const fmx_ctx* c);
 void run_match_linearize_total(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* out);
 void comm_allreduce_sum(fmx_ctx* c, double* dev, size_t n);  // no-op without a communicator
 // all-reduce n device doubles, copy them to host.p (write-through + completion word), wait

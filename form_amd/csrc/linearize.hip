@@ -261,6 +261,7 @@ static QoRows qo_rows(fmx_ctx* c) {
 void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, double* out) {
   if (!c->have_map) throw StatusError(FMX_E_STATE, "no map");
   if (!c->have_qo) throw StatusError(FMX_E_STATE, "no query-order match");
+  comm_check(c);
   hipStream_t st = c->stream;
   for (int i = 0; i < 29; ++i) out[i] = 0.0;
   if ((c->K == 0 || c->n_qo == 0) && !c->comm) return;  // sharded: every rank joins the collective
@@ -299,6 +300,7 @@ void run_linearize_total(fmx_ctx* c, const double* pose_j34, double sigma, doubl
 // completion-word / all-reduce handling as run_linearize_total.
 void run_match_linearize_total(fmx_ctx* c, const double* pose_j34, double max_dist, double sigma, double* out) {
   if (!c->have_map) throw StatusError(FMX_E_STATE, "no map");
+  comm_check(c);
   c->h_G.ensure(32);
   const bool comm = c->comm != nullptr;
   if (comm) c->d_sum.ensure(32);

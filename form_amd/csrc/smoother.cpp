@@ -636,10 +636,8 @@ WinLMResult window_lm(const WinGraph& g, const std::vector<Pose>& x0) {
   };
   double cur, newErr = err;
   bool conv;
-  static const bool lm_trace = std::getenv("FMX_LM_TRACE") != nullptr;  // diagnostic
   do {
     cur = newErr;
-    if (lm_trace) fprintf(stderr, "    lm iter %d err %.6e lambda %.1e lins %d\n", R.iters, err, lambda, R.lins);
     iterate();
     ++R.iters;
     newErr = err;

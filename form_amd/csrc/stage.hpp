@@ -71,49 +71,10 @@ inline cpu_set_t capture_load_cpus() {
 }
 inline const cpu_set_t g_load_cpus = capture_load_cpus();  // dynamic init at library load
 
-// CPUs sharing the last-level cache with `cpu` (sysfs; empty set if unknown).
-inline cpu_set_t llc_siblings(int cpu) {
-  cpu_set_t m;
-  CPU_ZERO(&m);
-  if (cpu < 0) return m;
-  char path[128];
-  std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
-  FILE* f = std::fopen(path, "r");
-  if (!f) return m;
-  char buf[256] = {0};
-  if (std::fgets(buf, sizeof(buf), f)) {
-    const std::string s(buf);
-    size_t p = 0;
-    while (p < s.size()) {
-      const size_t q = s.find(',', p);
-      const std::string part = s.substr(p, q == std::string::npos ? std::string::npos : q - p);
-      const size_t dash = part.find('-');
-      const int lo = std::atoi(part.c_str()), hi = dash == std::string::npos ? lo : std::atoi(part.c_str() + dash + 1);
-      for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c)
-        if (c >= 0) CPU_SET(c, &m);
-      if (q == std::string::npos) break;
-      p = q + 1;
-    }
-  }
-  std::fclose(f);
-  return m;
-}
-
 // Where the helpers of a creator running on `creator_cpu` may run: every load-time CPU
 // (g_load_cpus) but the creator's; if that leaves nothing, the inherited mask (returns
-// false).  FMX_STAGE_LLC=1 (A/B) prefers the load-time CPUs sharing the creator's
-// last-level cache (on a shared GPU box the creator's CCX also runs other jobs' threads).
+// false).
 inline bool helper_cpus(int creator_cpu, cpu_set_t& out) {
-  static const bool llc = std::getenv("FMX_STAGE_LLC") != nullptr;
-  if (llc) {
-    cpu_set_t near = llc_siblings(creator_cpu), pref;
-    CPU_AND(&pref, &near, &g_load_cpus);
-    if (creator_cpu >= 0) CPU_CLR(creator_cpu, &pref);
-    if (CPU_COUNT(&pref) > 0) {
-      out = pref;
-      return true;
-    }
-  }
   out = g_load_cpus;
   if (creator_cpu >= 0) CPU_CLR(creator_cpu, &out);
   return CPU_COUNT(&out) > 0;
@@ -210,7 +171,7 @@ struct StageReq {
 // the CPU of the thread that creates them (a registering thread is often pinned to one
 // CPU; threads inherit that mask): each helper runs on the CPUs the process was given at
 // load time (taskset / numactl / a per-rank binding, FMX_STAGE_CPUS) that share the
-// creator's last-level cache, never the creator's own (helper_cpus).
+// never the creator's own (helper_cpus).
 class Stager {
  public:
   ~Stager() { stop(); }

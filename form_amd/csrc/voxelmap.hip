@@ -576,18 +576,7 @@ struct MatchArgs {
   // (its pinned slot of the profiler's work ring: the byte model of THIS launch)
   uint32_t* prof_acc;
   uint32_t* prof_work;
-  // Heaviest-first dispatch (VERDICT r4 "next round" 4; 8-lane build only): workgroup b
-  // processes query block order[b] (null: b).  Every query block stores its duration
-  // to cost[] (null: not kept) and the launch's last block rewrites order[] for the next
-  // match on the same map and query set: query blocks by duration class, longest first
-  // (stable within a class).  The results are the same in any order — only which
-  // workgroup takes which query block changes.
-  uint32_t* order;
-  uint32_t* cost;
-  uint32_t* order_out;  // where the last block writes the next order (null: none; nb <= kOrderMaxBlocks) —
-                        // the same buffer as order when that is set: every block has read its entry by then
 };
-constexpr uint32_t kOrderMaxBlocks = 8 * 256;  // the last block's counting sort: <= 8 entries per thread
 
 // kGroup lanes cooperate on one query: lane g of the group visits shifts
 // g, g+kGroup, ... (3-4 of the 27 voxels), then the group min-reduces
@@ -1554,6 +1543,7 @@ __device__ __forceinline__ uint2 block_sum2(uint32_t x, uint32_t y) {
       t.x += s2[0][i];
       t.y += s2[1][i];
     }
+  __syncthreads();  // s2 is read before a following call may overwrite it
   return t;
 }
 __device__ inline uint2 match_tail(const MatchArgs& a, uint32_t* __restrict__ mcnt, uint32_t* __restrict__ host_counts,
@@ -1654,32 +1644,6 @@ __device__ inline uint2 match_tail(const MatchArgs& a, uint32_t* __restrict__ mc
   return cw;
 }
 
-// The last block: the next launch's query-block order, longest first.  Four duration
-// classes (>= 16, 8, 4 us, shorter; 100 MHz ticks), a stable counting sort: thread t
-// takes query blocks [R t, R t + R), one four-way block scan gives each its slot.  Every
-// block's cost was stored (agent scope) before its ticket.
-__device__ inline void write_order(const MatchArgs& a, uint32_t nb) {
-  constexpr int R = kOrderMaxBlocks / kMatchThreads;
-  __shared__ uint32_t ws4[kMatchThreads / kWave][4];
-  uint32_t cls[R], cnt[4] = {0, 0, 0, 0};
-  const uint32_t b0 = threadIdx.x * R;
-#pragma unroll
-  for (int u = 0; u < R; ++u) {
-    const uint32_t b = b0 + u;
-    const uint32_t t = b < nb ? __hip_atomic_load(a.cost + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    cls[u] = t >= 1600u ? 0u : t >= 800u ? 1u : t >= 400u ? 2u : 3u;
-    if (b < nb) ++cnt[cls[u]];
-  }
-  uint32_t ex[4], tot[4];
-  block_excl_scan4(cnt, ex, tot, ws4);
-  const uint32_t base[4] = {0u, tot[0], tot[0] + tot[1], tot[0] + tot[1] + tot[2]};
-#pragma unroll
-  for (int u = 0; u < R; ++u) {
-    const uint32_t b = b0 + u;
-    if (b < nb) a.order_out[base[cls[u]] + ex[cls[u]]++] = b;
-  }
-}
-
 template <bool DENSE, bool FUSED = false>
 __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArgs a, MapView mp, MapView mt,
                                                          const float4* __restrict__ q_pl,
@@ -1695,7 +1659,7 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
                                                          uint32_t* __restrict__ thist, SortOut so, FusedArgs fz) {
   extern __shared__ uint32_t s_hist[];  // [K]
   const double* Tj = a.Tj;
-  const uint32_t bq = a.order ? a.order[blockIdx.x] : blockIdx.x;  // this workgroup's query block
+  const uint32_t bq = blockIdx.x;  // this workgroup's query block
   const bool planar = bq < a.nb_pl;
   const uint32_t bt = planar ? bq : bq - a.nb_pl;  // the block's index in its type
   const uint32_t qi = bt * kQPB + threadIdx.x / kGroup;  // the block's first query + the group
@@ -1885,7 +1849,6 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
     const uint32_t t_end = (uint32_t)wall_clock64();
     w4[0] = make_uint4(tp, tc, mq, d0);
     w4[1] = make_uint4(t_begin, t_end, d1, d2);
-    if (a.cost) __hip_atomic_store(a.cost + bq, t_end - t_begin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // (a profiled launch's probe / candidate totals: the last block sums these words; the
     // fused launch, whose blocks have no tail, adds them up as it goes)
     if (FUSED && a.prof_work) {
@@ -2074,7 +2037,6 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
       host_store(a.prof_work + 3, cw.y);
     }
   }
-  if (a.order_out) write_order(a, gridDim.x);
   if (threadIdx.x == 0) __hip_atomic_store(mticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2523,26 +2485,6 @@ void run_pair_scatter(fmx_ctx* c) {
   FMX_HIP(hipGetLastError());
 }
 
-// FMX_LPT=1: heaviest-first query-block dispatch (opt-in; same results).  Measured
-// round 5 (profiles/r5_ab_envs.txt): the warm launches it applies to were already short
-// (certificate), the cold one has no order, and the order read + the last block's
-// counting sort cost more than the shorter tail gained — match 0.296 -> 0.311 ms per C4
-// scan with it, so index order is the default.
-static bool no_lpt() {
-  static const bool v = std::getenv("FMX_LPT") == nullptr || std::getenv("FMX_NO_LPT") != nullptr;
-  return v;
-}
-// FMX_NO_WARM: every match cold; FMX_NO_CELL_CACHE: warm matches probe their own cell
-// again (A/B switches; results are identical either way)
-static bool no_warm() {
-  static const bool v = std::getenv("FMX_NO_WARM") != nullptr;
-  return v;
-}
-static bool no_cell_cache() {
-  static const bool v = std::getenv("FMX_NO_CELL_CACHE") != nullptr;
-  return v;
-}
-
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
   hipStream_t st = c->match_stream ? c->match_stream : c->stream;
@@ -2564,12 +2506,12 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   {
     const uint32_t* before = c->m_rec.p;
     c->m_rec.ensure((size_t)c->n_qpl + c->n_qpt + 1);
-    const bool warm = c->warm_rec_gen == c->warm_gen && c->m_rec.p == before && !no_warm();
+    const bool warm = c->warm_rec_gen == c->warm_gen && c->m_rec.p == before;
     const uint4* cbefore = c->m_cell.p;
     c->m_cell.ensure((size_t)c->n_qpl + c->n_qpt + 1);
     a.warm = warm && c->m_cell.p == cbefore ? c->m_rec.p : nullptr;
     a.rec = c->m_rec.p;
-    a.cell = no_cell_cache() ? nullptr : c->m_cell.p;
+    a.cell = c->m_cell.p;
     c->warm_rec_gen = c->warm_gen;
 #if FMX_CERT_ANY
     const float* cb = c->cert_b2.p;
@@ -2617,18 +2559,6 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   c->work_blocks = nb;
   ensure_zeroed(c->mcnt, 2 * (size_t)K, st);
   ensure_zeroed(c->mticket, 1, st);
-  // heaviest-first dispatch: the order the last match on this map and query set wrote
-  {
-    const uint32_t nbq = (c->n_qpl + kQPB - 1) / kQPB + (c->n_qpt + kQPB - 1) / kQPB;
-    const bool on = kGroup > 1 && !no_lpt() && nbq > 0 && nbq <= kOrderMaxBlocks;
-    c->mcost.ensure(nbq + 1);
-    c->mord.ensure(nbq + 1);
-    a.order = on && c->ord_gen == c->warm_gen && c->ord_nb == nbq ? c->mord.p : nullptr;
-    a.cost = on ? c->mcost.p : nullptr;
-    a.order_out = on ? c->mord.p : nullptr;
-    c->ord_gen = on ? c->warm_gen : 0;
-    c->ord_nb = nbq;
-  }
   c->ins_blk.ensure(nb + 1);
   c->ins_off.ensure(nb + 1);
   ensure_zeroed(c->thist, (size_t)K * (a.ntl_pl + a.ntl_pt) + 1, st);
@@ -2744,9 +2674,6 @@ void run_match_linearize(fmx_ctx* c, const double* pose_j34, double max_dist, do
 #if FMX_CERT_ANY
   a.cert_b2 = nullptr;
 #endif
-  a.order = nullptr;
-  a.cost = nullptr;
-  a.order_out = nullptr;
   a.nq_pl = c->n_qpl;
   a.nq_pt = c->n_qpt;
   a.nb_pl = (c->n_qpl + kQPB - 1) / kQPB;

@@ -950,6 +950,7 @@ void win_moments_pairs(fmx_ctx* c, const double* poses_i, const double* poses_j,
 void win_linearize_pairs(fmx_ctx* c, const double* poses_i, const double* poses_j, double sigma, int mode,
                          double* G_out, double* err_out) {
   if (!c->have_corr) throw StatusError(FMX_E_STATE, "no correspondences (call fmx_match or fmx_corr_set)");
+  comm_check(c);
   run_pair_scatter(c);  // fmx_match deferred it
   const int K = (int)c->K;
   if (K == 0) return;

@@ -246,7 +246,10 @@ fmx_status fmx_register_points(fmx_ctx* ctx, const double pose_init34[12], doubl
  * equations over xGMI".  RCCL is loaded on first use (FMX_E_RCCL if absent).  A wait for
  * an all-reduce is bounded: it polls the stream and ncclCommGetAsyncError and, after
  * FMX_COMM_TIMEOUT_S seconds (environment, default 60), aborts the communicator and
- * returns FMX_E_RCCL; the context then continues without a communicator. */
+ * returns FMX_E_RCCL.  The communicator is gone then, and every later sharded call
+ * (fmx_linearize_matched, fmx_linearize / fmx_error, fmx_register_points) also returns
+ * FMX_E_RCCL until fmx_comm_init attaches a new one: this rank holds only a shard of the
+ * queries, so a rank-local system must never stand in for the global one. */
 fmx_status fmx_comm_unique_id(uint8_t id[128]);
 fmx_status fmx_comm_init(fmx_ctx* ctx, const uint8_t id[128], int nranks, int rank);
 

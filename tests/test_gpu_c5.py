@@ -409,9 +409,13 @@ try:
     print("RESULT ok", time.time() - t0)
 except fmx.FmxError as e:
     print("RESULT err", e.status, round(time.time() - t0, 3), str(e))
-# the context stays usable (no communicator any more): the plain system
-S, err = ctx.linearize_matched(I34, 0.1)
-print("AFTER", bool(np.isfinite(S).all() and err > 0))
+# ADVICE r5: a retry must not return this rank's shard as the global system
+t1 = time.time()
+try:
+    ctx.linearize_matched(I34, 0.1)
+    print("RETRY ok")
+except fmx.FmxError as e:
+    print("RETRY err", e.status, round(time.time() - t1, 3))
 ctx.close()
 '''
 
@@ -422,8 +426,9 @@ def test_withheld_allreduce_fails_within_bound(tmp_path):
     (FMX_TEST_WITHHOLD_FLAG) keeps the publish kernel behind ncclAllReduce on the stream
     without storing the completion word — a collective that never completes, on a 1-rank
     communicator.  With FMX_COMM_TIMEOUT_S=2 the call returns FMX_E_RCCL after ~2 s (the
-    communicator aborted, the held kernel released) and the context keeps working without
-    a communicator."""
+    communicator aborted, the held kernel released).  ADVICE r5: a second sharded call on
+    the same context fails at once with FMX_E_RCCL too (its queries are only this rank's
+    shard), instead of returning the rank-local system."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -436,4 +441,5 @@ def test_withheld_allreduce_fails_within_bound(tmp_path):
     res = [ln.split() for ln in r.stdout.splitlines() if ln.startswith("RESULT")][0]
     assert res[1] == "err" and int(res[2]) == 7, r.stdout  # FMX_E_RCCL
     assert 1.9 <= float(res[3]) < 10.0, r.stdout  # the bound, not a hang (the held kernel itself gives up at 20 s)
-    assert "AFTER True" in r.stdout
+    retry = [ln.split() for ln in r.stdout.splitlines() if ln.startswith("RETRY")][0]
+    assert retry[1] == "err" and int(retry[2]) == 7 and float(retry[3]) < 1.0, r.stdout
