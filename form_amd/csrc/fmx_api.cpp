@@ -113,7 +113,8 @@ static void sync_all(fmx_ctx* c) {
 static void prof_collect(fmx_ctx* c) {
   Prof& pr = c->prof;
   if (pr.pending.empty()) return;
-  sync_all(c);  // profiled launches run on all three streams
+  run_pair_scatter(c);  // a tiled match's work counts reach its ring slot from its scatter
+  sync_all(c);          // profiled launches run on all three streams
   for (ProfPending& e : pr.pending) {
     float ms = 0.f;
     FMX_HIP(hipEventElapsedTime(&ms, e.a, e.b));
@@ -816,6 +817,7 @@ void swap_match_set(fmx_ctx* c) {
   ++c->corr_gen;
   swap(c->m_pair, S.m_pair); swap(c->m_d2, S.m_d2); swap(c->m_pi, S.m_pi); swap(c->m_ni, S.m_ni);
   swap(c->m_ins, S.m_ins); swap(c->hist, S.hist); swap(c->hist_off, S.hist_off); swap(c->thist, S.thist);
+  swap(c->thist_par, S.thist_par);
   swap(c->c_pl, S.c_pl); swap(c->c_pt, S.c_pt); swap(c->pair_counts, S.pair_counts);
   swap(c->chunk_range, S.chunk_range); swap(c->chunks, S.chunks); swap(c->n_chunks, S.n_chunks);
   swap(c->pair_base, S.pair_base); swap(c->work, S.work); swap(c->mcnt, S.mcnt); swap(c->mticket, S.mticket);
@@ -1563,8 +1565,23 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     int prio_lo = 0, prio_hi = 0;
     FMX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     FMX_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
-    FMX_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_lo));
-    FMX_HIP(hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, prio_lo));
+    const char* cus = std::getenv("FMX_SIDE_CUS");  // EXPERIMENT (A/B): side streams on N CUs
+    if (cus && std::atoi(cus) > 0) {
+      hipDeviceProp_t pr;
+      FMX_HIP(hipGetDeviceProperties(&pr, device));
+      const int ncu = pr.multiProcessorCount, n = std::min(ncu, std::atoi(cus));
+      const bool spread = std::getenv("FMX_SIDE_CUS_SPREAD") != nullptr;
+      std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; ++i) {
+        const bool on = spread ? (int)((int64_t)i * n / ncu) != (int)((int64_t)(i + 1) * n / ncu) : i >= ncu - n;
+        if (on) m[i / 32] |= 1u << (i % 32);
+      }
+      FMX_HIP(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)m.size(), m.data()));
+      FMX_HIP(hipExtStreamCreateWithCUMask(&c->side2, (uint32_t)m.size(), m.data()));
+    } else {
+      FMX_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_lo));
+      FMX_HIP(hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, prio_lo));
+    }
     c->ev_fork.create();
     c->ev_join.create();
     c->ev_pf.create();

@@ -215,7 +215,9 @@ struct Seg {
 struct PairScatter {
   uint32_t nb_pl = 0, nb_pt = 0, ntl_pl = 0, ntl_pt = 0;
   int K = 0;
-  int tiles = 0;
+  int tiles = 0;              // 0 per-block histograms; 1 counts scanned by the match's last block; 2 by the scatter
+  uint32_t thist_off = 0;     // the count table half the match added into
+  uint32_t* prof_work = nullptr;  // the match's profiler slot (tiles == 2: filled by the scatter)
 };
 
 struct Chunk {
@@ -286,6 +288,7 @@ struct MatchSet {
   DBuf<double4> m_pi, m_ni;
   DBuf<uint8_t> m_ins;
   DBuf<uint32_t> hist, hist_off, thist;
+  uint32_t thist_par = 0;
   DBuf<double> c_pl, c_pt;
   DBuf<uint32_t> pair_counts, chunk_range;
   DBuf<Chunk> chunks;
@@ -422,7 +425,8 @@ struct fmx_ctx {
   fmx::DBuf<uint4> m_cell;    // per query: its own cell as the last match found it (same scheme)
   uint64_t warm_gen = 1;      // bumped by every map build and query-set change
   uint64_t warm_rec_gen = 0;  // warm_gen when m_rec was last written (0: never)
-  fmx::DBuf<uint32_t> thist;  // tiled pair sort: per-(type, pair, tile) counts, self-resetting
+  fmx::DBuf<uint32_t> thist;  // tiled pair sort: per-(type, pair, tile) counts, two halves
+  uint32_t thist_par = 0;     // the half the last tiled match added into
   fmx::DBuf<float> cert_b2;   // FMX_CERT_DIAG / FMX_WARM_CERT builds: per query the last match's second-best bound
   double cert_pose[12] = {};  // ... and that match's pose
   uint64_t cert_gen = 0;      // warm_gen when cert_b2 was last written by an 8-lane match (0: none)
@@ -493,7 +497,6 @@ struct fmx_ctx {
   // LM trial proposes, queued behind the trial's linearization while the host decides;
   // used by the next ICP iteration if it starts from exactly that pose
   fmx::MatchSet spec;
-  hipStream_t match_stream = nullptr;  // run_match / run_pair_scatter stream override
   bool spec_valid = false;
   bool spec_first = false;  // the speculative set holds the scan's first match (not a speculation)
   bool spec_mom = false;    // ... and its pair moments are pending in the window machinery (win_moments_current)

@@ -550,8 +550,11 @@ struct MatchArgs {
   uint32_t nq_pl, nq_pt, nb_pl, nb_pt;  // queries; planar / point blocks
   int K;
   int sorted;  // 1: pair histogram for the pair sort; 0: per-pair counts only
-  int tiles;   // sorted: 1 = per-(pair, tile) counts scanned by the last block (k_pair_scatter_t)
+  int tiles;   // sorted: per-(type, pair, tile) counts, scanned by the last block (kTilesTail,
+               // k_pair_scatter_t) or by the pair scatter itself (kTilesScatter, k_pair_scatter_s)
   uint32_t ntl_pl, ntl_pt;  // tiles (kTileBlocks match blocks each) per type
+  uint32_t* thist_clear;    // kTilesScatter: the count table's other half, cleared by block 0
+  uint32_t thist_clear_n;
   // warm start (fmx_ctx::m_rec): the NN record per query of an earlier match on the same
   // map and query set (null: cold), this launch's NN records (null: not kept), and the
   // largest warm distance^2 that may bound the search (a record that close to the query
@@ -602,6 +605,12 @@ constexpr int kTileBlocks = FMX_TILE_Q / kQPB > 0 ? FMX_TILE_Q / kQPB : 1;
 constexpr int kTileQ = kTileBlocks * kQPB;  // 1024
 constexpr int kTileMaxPairs = (int)kMatchTileMaxPairs;  // LDS bound of the tiled path (wider windows: per-block path)
 constexpr int kWorkWords = 8;               // per-block match work / diagnostic words
+// Who scans the (type, pair, tile) counts of a tiled match: the match's last block
+// (kTilesTail), or every pair-scatter block its own share plus one extra scatter block
+// for the per-pair tables and insert offsets (kTilesScatter: the match has no serial
+// tail; used while the whole count table fits the scatter's LDS, kScatterTab words).
+constexpr int kTilesTail = 1, kTilesScatter = 2;
+constexpr uint32_t kScatterTab = 6144;
 
 // Outputs of the tiled pair sort's last-block pass (consumed by later launches).
 struct SortOut {
@@ -1995,6 +2004,14 @@ __global__ __launch_bounds__(kMatchThreads) FMX_MATCH_ATTR void k_match(MatchArg
       if (s_hist[k])
         __hip_atomic_fetch_add(thist + hbase + (size_t)k * ntl + tile, s_hist[k], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+    // block 0 clears the other half of the count table for the next tiled match on this
+    // set (what read it — this set's previous scatter or last block — ran before this
+    // launch, in stream order)
+    if (blockIdx.x == 0)
+      for (uint32_t i = threadIdx.x; i < a.thist_clear_n; i += kMatchThreads) a.thist_clear[i] = 0u;
+    // kTilesScatter: no last block — the pair scatter scans the counts
+    // (k_pair_scatter_s), so the launch ends with its last query block
+    if (a.tiles == kTilesScatter) return;
   } else if (a.sorted) {
     // pair-major layout [type][pair][block]: one exclusive scan gives every block's
     // destination offset (k_pair_base / k_pair_scatter)
@@ -2252,6 +2269,282 @@ __global__ __launch_bounds__(kTileQ) void k_pair_scatter_t(uint32_t nq_pl, uint3
   }
 }
 
+// ---- the tiled pair sort without a match tail (kTilesScatter)
+// Exclusive scan of one value per thread over an NT-thread block; total returned.
+template <int NT>
+__device__ __forceinline__ uint32_t blk_excl_scan(uint32_t v, uint32_t* ws, uint32_t& total) {
+  const uint32_t incl = wave_incl_scan(v);
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == kWave - 1) ws[w] = incl;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / kWave; ++i) {
+    const uint32_t x = ws[i];
+    off += i < w ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return off + incl - v;
+}
+
+struct ScatterArgs {
+  uint32_t nq_pl, nq_pt, ntl_pl, ntl_pt;
+  int K;
+  const int32_t* m_pair;
+  const double4* m_pi;
+  const double4* m_ni;
+  const float4* q_pl;
+  const float4* q_pt;
+  const uint32_t* thist;  // [type][pair][tile] match counts: [0, K ntl_pl) planar, then point
+  double* c_pl;
+  size_t ld_pl;
+  double* c_pt;
+  size_t ld_pt;
+  // the meta block's outputs: per-pair counts / first rows [type][K], the window chunk
+  // table, the pinned host copy (pair counts, insert totals, certified / warm queries)
+  uint32_t* pair_counts;
+  uint32_t* pair_base;
+  uint32_t* chunk_range;
+  Chunk* chunks;
+  uint32_t* n_chunks;
+  uint32_t* host_counts;
+  const uint32_t* ins_blk;  // per match block: insert count | certified << 10 | warm << 20
+  uint32_t* ins_off;        // -> k_insert offsets (per type, from 0)
+  uint32_t nb_pl, nb_pt;
+  const uint32_t* work;  // profiled launches: per-match-block work words (probes, candidates) ...
+  uint32_t* prof_work;   // ... summed into the launch's profiler slot (null: not profiled)
+};
+
+// Sum over tiles of row k of a [pair][tile] count table in LDS (one wave; every lane
+// returns the totals): *pre = the tiles before `tile`.
+__device__ __forceinline__ uint32_t tile_row_sum(const uint32_t* tab, uint32_t ntl, uint32_t tile, uint32_t& pre) {
+  uint32_t t = 0, p = 0;
+  for (uint32_t t0 = 0; t0 < ntl; t0 += kWave) {
+    const uint32_t i = t0 + lane_id();
+    const uint32_t v = i < ntl ? tab[i] : 0u;
+    t += v;
+    p += i < tile ? v : 0u;
+  }
+  pre = wave_sum(p);
+  return wave_sum(t);
+}
+
+// The meta block of k_pair_scatter_s (the grid's last): what the match's last block did
+// for kTilesTail — per-pair counts and first rows, the window chunk table, insert
+// offsets — running beside the tile blocks instead of after every query block.
+__device__ void scatter_meta(const ScatterArgs& a, uint32_t* s_tab) {
+  constexpr int NT = kTileQ, NW = NT / kWave;
+  __shared__ uint32_t ws[NW];
+  __shared__ uint32_t s_tot[2][kTileMaxPairs];
+  __shared__ uint32_t s_cr[kTileMaxPairs + 1];
+  __shared__ uint32_t s_cw[NW][4];
+  const int K = a.K, w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t n0 = (uint32_t)K * a.ntl_pl, n = n0 + (uint32_t)K * a.ntl_pt;
+  for (uint32_t i = threadIdx.x; i < n; i += NT) s_tab[i] = a.thist[i];
+  // the launch's certified / warm queries and (profiled) probes / candidates, in the
+  // same round of loads
+  const uint32_t nb = a.nb_pl + a.nb_pt;
+  uint32_t cs = 0, wm = 0, tp = 0, tc = 0;
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) {
+    const uint32_t x = a.ins_blk[b];
+    cs += (x >> 10) & 0x3FFu;
+    wm += x >> 20;
+    if (a.prof_work) {
+      tp += a.work[kWorkWords * b];
+      tc += a.work[kWorkWords * b + 1];
+    }
+  }
+  cs = wave_sum(cs);
+  wm = wave_sum(wm);
+  tp = wave_sum(tp);
+  tc = wave_sum(tc);
+  if (lane == 0) {
+    s_cw[w][0] = cs;
+    s_cw[w][1] = wm;
+    s_cw[w][2] = tp;
+    s_cw[w][3] = tc;
+  }
+  __syncthreads();
+  for (int it = w; it < 2 * K; it += NW) {  // per (type, pair): its total over the tiles
+    const int t = it / K, k = it % K;
+    const uint32_t ntl = t ? a.ntl_pt : a.ntl_pl;
+    uint32_t pre;
+    const uint32_t tot = tile_row_sum(s_tab + (t ? n0 : 0u) + (uint32_t)k * ntl, ntl, 0u, pre);
+    if (lane == 0) s_tot[t][k] = tot;
+  }
+  __syncthreads();
+  // per pair: counts (device + host), first rows per type, chunks (plane then point)
+  uint32_t carry_pl = 0, carry_pt = 0, carry_ch = 0;
+  for (int k0 = 0; k0 < K; k0 += NT) {
+    const int k = k0 + threadIdx.x;
+    const uint32_t npl = k < K ? s_tot[0][k] : 0u, npt = k < K ? s_tot[1][k] : 0u;
+    const uint32_t nch = (npl + kPlaneChunk - 1) / kPlaneChunk + (npt + kPointChunk - 1) / kPointChunk;
+    uint32_t t0, t1, t2;
+    const uint32_t b_pl = carry_pl + blk_excl_scan<NT>(npl, ws, t0);
+    const uint32_t b_pt = carry_pt + blk_excl_scan<NT>(npt, ws, t1);
+    const uint32_t b_ch = carry_ch + blk_excl_scan<NT>(nch, ws, t2);
+    if (k < K) {
+      a.pair_counts[k] = npl;
+      a.pair_counts[K + k] = npt;
+      a.pair_base[k] = b_pl;
+      a.pair_base[K + k] = b_pt;
+      host_store(a.host_counts + k, npl);  // mapped host memory
+      host_store(a.host_counts + K + k, npt);
+      s_cr[k] = b_ch;
+      s_tot[0][k] = b_pl;  // (first rows, for the descriptors below)
+      s_tot[1][k] = b_pt;
+    }
+    carry_pl += t0;
+    carry_pt += t1;
+    carry_ch += t2;
+  }
+  if (threadIdx.x == 0) s_cr[K] = carry_ch;
+  __syncthreads();
+  for (int k = threadIdx.x; k <= K; k += NT) a.chunk_range[k] = s_cr[k];
+  for (uint32_t ci = threadIdx.x; ci < carry_ch; ci += NT) {  // chunk -> pair by binary search
+    int lo = 0, hi = K - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_cr[mid] <= ci) lo = mid;
+      else hi = mid - 1;
+    }
+    const int k = lo;
+    const uint32_t j = ci - s_cr[k];
+    const uint32_t b_pl = s_tot[0][k], b_pt = s_tot[1][k];
+    const uint32_t e_pl = k + 1 < K ? s_tot[0][k + 1] : carry_pl, e_pt = k + 1 < K ? s_tot[1][k + 1] : carry_pt;
+    const uint32_t cpl = e_pl - b_pl, cpt = e_pt - b_pt;
+    const uint32_t ncpl = (cpl + kPlaneChunk - 1) / kPlaneChunk;
+    if (j < ncpl) {
+      const uint32_t r = j * kPlaneChunk;
+      a.chunks[ci] = Chunk{0, (uint32_t)k, b_pl + r, b_pl + min(cpl, r + kPlaneChunk)};
+    } else {
+      const uint32_t r = (j - ncpl) * kPointChunk;
+      a.chunks[ci] = Chunk{1, (uint32_t)k, b_pt + r, b_pt + min(cpt, r + kPointChunk)};
+    }
+  }
+  if (threadIdx.x == 0) *a.n_chunks = carry_ch;
+  // insert offsets per type (k_insert), from each type's first block
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t b0 = t ? a.nb_pl : 0u, nbt = t ? a.nb_pt : a.nb_pl;
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < nbt; i0 += NT) {
+      const uint32_t i = i0 + threadIdx.x;
+      const uint32_t v = i < nbt ? a.ins_blk[b0 + i] & 0x3FFu : 0u;
+      uint32_t tot;
+      const uint32_t ex = carry + blk_excl_scan<NT>(v, ws, tot);
+      if (i < nbt) a.ins_off[b0 + i] = ex;
+      carry += tot;
+    }
+    if (threadIdx.x == 0) host_store(a.host_counts + 2 * K + t, carry);
+  }
+  if (threadIdx.x == 0) {
+    uint32_t c4[4] = {0, 0, 0, 0};
+    for (int i = 0; i < NW; ++i)
+      for (int q = 0; q < 4; ++q) c4[q] += s_cw[i][q];
+    host_store(a.host_counts + 2 * K + 2, c4[0]);
+    host_store(a.host_counts + 2 * K + 3, c4[1]);
+    if (a.prof_work) {  // the launch's probes / candidates / certified / warm -> its profiler slot
+      host_store(a.prof_work, c4[2]);
+      host_store(a.prof_work + 1, c4[3]);
+      host_store(a.prof_work + 2, c4[0]);
+      host_store(a.prof_work + 3, c4[1]);
+    }
+  }
+}
+
+// Tiled stable scatter for kTilesScatter: tile blocks as k_pair_scatter_t, each finding
+// its own (pair, tile) offsets from the match's count table (its type's table to LDS in
+// the same round of loads as its rows; a wave per pair sums the pair's tiles and those
+// before this one; the pairs' first rows by one exclusive scan of the totals), plus the
+// meta block (scatter_meta).  Query order within a pair, deterministic.
+__global__ __launch_bounds__(kTileQ) void k_pair_scatter_s(ScatterArgs a) {
+  constexpr int NW = kTileQ / kWave;
+  __shared__ uint32_t s_tab[kScatterTab];
+  __shared__ uint32_t s_cnt[NW][kTileMaxPairs];
+  __shared__ uint32_t s_pre[kTileMaxPairs], s_tot[kTileMaxPairs];
+  const uint32_t ntiles = a.ntl_pl + a.ntl_pt;
+  if (blockIdx.x == ntiles) {
+    scatter_meta(a, s_tab);
+    return;
+  }
+  const int K = a.K;
+  const bool planar = blockIdx.x < a.ntl_pl;
+  const uint32_t tile = planar ? blockIdx.x : blockIdx.x - a.ntl_pl;
+  const uint32_t ntl = planar ? a.ntl_pl : a.ntl_pt;
+  const uint32_t qi = tile * kTileQ + threadIdx.x;
+  const uint32_t nq = planar ? a.nq_pl : a.nq_pt;
+  const int w = threadIdx.x / kWave, lane = lane_id();
+  // every load up front, in one round: the type's count table, the row's fields
+  const uint32_t* tab = a.thist + (planar ? 0u : (uint32_t)K * a.ntl_pl);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)K * ntl; i += kTileQ) s_tab[i] = tab[i];
+  for (int i = threadIdx.x; i < NW * K; i += kTileQ) s_cnt[i / K][i % K] = 0;
+  const size_t gq = planar ? qi : a.nq_pl + qi;
+  const bool in = qi < nq;
+  const int32_t pair = in ? a.m_pair[gq] : -1;
+  const double4 pi = in ? a.m_pi[gq] : make_double4(0, 0, 0, 0);
+  const double4 ni = in && planar ? a.m_ni[qi] : make_double4(0, 0, 0, 0);
+  const float4 pj = in ? (planar ? a.q_pl[qi] : a.q_pt[qi]) : make_float4(0, 0, 0, 0);
+  __syncthreads();
+  // per pair: its total and its matches in earlier tiles
+  for (int k = w; k < K; k += NW) {
+    uint32_t pre;
+    const uint32_t tot = tile_row_sum(s_tab + (uint32_t)k * ntl, ntl, tile, pre);
+    if (lane == 0) {
+      s_tot[k] = tot;
+      s_pre[k] = pre;
+    }
+  }
+  uint32_t rank = 0;
+  bool todo = pair >= 0;
+  while (__ballot(todo)) {
+    const int lead = __ffsll((unsigned long long)__ballot(todo)) - 1;
+    const int v = __shfl(pair, lead, 64);
+    const uint64_t m = __ballot(todo && pair == v);
+    if (todo && pair == v) {
+      rank = __popcll(m & lanemask_lt());
+      todo = false;
+    }
+    if (lane == lead) s_cnt[w][v] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (w == 0) {  // the pairs' first rows (exclusive scan of the totals) + this tile's offsets
+    uint32_t carry = 0;
+    for (int k0 = 0; k0 < K; k0 += kWave) {
+      const int k = k0 + lane;
+      const uint32_t v = k < K ? s_tot[k] : 0u;
+      const uint32_t incl = wave_incl_scan(v);
+      if (k < K) s_pre[k] += carry + incl - v;
+      carry += __shfl(incl, kWave - 1, 64);
+    }
+  }
+  for (int k = threadIdx.x; k < K; k += kTileQ) {  // per pair: exclusive scan over the waves
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const uint32_t c = s_cnt[i][k];
+      s_cnt[i][k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  if (pair < 0) return;
+  const uint32_t dst = s_pre[pair] + s_cnt[w][pair] + rank;
+  if (planar) {
+    double* c = a.c_pl;
+    const size_t ld = a.ld_pl;
+    c[0 * ld + dst] = pi.x; c[1 * ld + dst] = pi.y; c[2 * ld + dst] = pi.z;
+    c[3 * ld + dst] = ni.x; c[4 * ld + dst] = ni.y; c[5 * ld + dst] = ni.z;
+    c[6 * ld + dst] = (double)pj.x; c[7 * ld + dst] = (double)pj.y; c[8 * ld + dst] = (double)pj.z;
+  } else {
+    double* c = a.c_pt;
+    const size_t ld = a.ld_pt;
+    c[0 * ld + dst] = pi.x; c[1 * ld + dst] = pi.y; c[2 * ld + dst] = pi.z;
+    c[3 * ld + dst] = (double)pj.x; c[4 * ld + dst] = (double)pj.y; c[5 * ld + dst] = (double)pj.z;
+  }
+}
+
 // KeypointMap::insert_matches (map.tpp:148-165) for both feature types in one
 // launch: wave b covers the 64 queries of match block b and appends those whose NN
 // distance exceeded min_dist_map (m_ins) to the type's keypoint store, in query
@@ -2469,8 +2762,42 @@ void run_pair_scatter(fmx_ctx* c) {
   c->scatter_pending = false;
   const PairScatter& s = c->ps;
   const uint32_t nb = s.nb_pl + s.nb_pt;
+  hipStream_t st = c->stream;
+  if (nb > 0 && s.tiles == kTilesScatter) {  // tile blocks (if any pair) + the meta block
+    ScatterArgs a;
+    a.nq_pl = c->n_qpl;
+    a.nq_pt = c->n_qpt;
+    a.ntl_pl = c->K ? s.ntl_pl : 0u;
+    a.ntl_pt = c->K ? s.ntl_pt : 0u;
+    a.K = (int)c->K;
+    a.m_pair = c->m_pair.p;
+    a.m_pi = c->m_pi.p;
+    a.m_ni = c->m_ni.p;
+    a.q_pl = c->q_pl_pos.p;
+    a.q_pt = c->q_pt_pos.p;
+    a.thist = c->thist.p + s.thist_off;
+    a.c_pl = c->c_pl.p;
+    a.ld_pl = c->ld_pl;
+    a.c_pt = c->c_pt.p;
+    a.ld_pt = c->ld_pt;
+    a.pair_counts = c->pair_counts.p;
+    a.pair_base = c->pair_base.p;
+    a.chunk_range = c->chunk_range.p;
+    a.chunks = c->chunks.p;
+    a.n_chunks = c->n_chunks.p;
+    a.host_counts = c->h_counts.d;
+    a.ins_blk = c->ins_blk.p;
+    a.ins_off = c->ins_off.p;
+    a.nb_pl = s.nb_pl;
+    a.nb_pt = s.nb_pt;
+    a.work = c->work.p;
+    a.prof_work = s.prof_work;
+    ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
+    hipLaunchKernelGGL(k_pair_scatter_s, dim3(a.ntl_pl + a.ntl_pt + 1), dim3(kTileQ), 0, st, a);
+    FMX_HIP(hipGetLastError());
+    return;
+  }
   if (nb == 0 || c->K == 0) return;
-  hipStream_t st = c->match_stream ? c->match_stream : c->stream;
   ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
   if (s.tiles)
     hipLaunchKernelGGL(k_pair_scatter_t, dim3(s.ntl_pl + s.ntl_pt), dim3(kTileQ), 0, st, c->n_qpl, c->n_qpt, s.ntl_pl,
@@ -2487,7 +2814,7 @@ void run_pair_scatter(fmx_ctx* c) {
 
 void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_dist_map, bool sorted,
                bool defer_scatter) {
-  hipStream_t st = c->match_stream ? c->match_stream : c->stream;
+  hipStream_t st = c->stream;
   const int K = std::max<int>((int)c->K, 1);
   MatchArgs a;
   if (pose_j34) std::memcpy(a.Tj, pose_j34, sizeof(a.Tj));
@@ -2531,9 +2858,12 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   a.nb_pt = nb_pt;
   a.K = (int)c->K;
   a.sorted = sorted ? 1 : 0;
-  a.tiles = sorted && c->K <= (uint32_t)kTileMaxPairs ? 1 : 0;  // wider windows: per-block histograms
   a.ntl_pl = (a.nb_pl + kTileBlocks - 1) / kTileBlocks;
   a.ntl_pt = (nb_pt + kTileBlocks - 1) / kTileBlocks;
+  // wider windows: per-block histograms; a count table that fits the scatter's LDS: no
+  // match tail (the scatter scans it)
+  const uint64_t tab = (uint64_t)c->K * (a.ntl_pl + a.ntl_pt);
+  a.tiles = !sorted || c->K > (uint32_t)kTileMaxPairs ? 0 : tab <= kScatterTab ? kTilesScatter : kTilesTail;
   const uint32_t nq = c->n_qpl + c->n_qpt;
   c->m_pair.ensure(nq + 1);
   c->m_d2.ensure(nq + 1);
@@ -2561,7 +2891,14 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   ensure_zeroed(c->mticket, 1, st);
   c->ins_blk.ensure(nb + 1);
   c->ins_off.ensure(nb + 1);
-  ensure_zeroed(c->thist, (size_t)K * (a.ntl_pl + a.ntl_pt) + 1, st);
+  // the count table in two halves: a tiled launch adds into one and clears the other
+  // (read by this set's previous tiled match or its scatter) for the next
+  ensure_zeroed(c->thist, 2 * ((size_t)K * (a.ntl_pl + a.ntl_pt) + 1), st);
+  const size_t half = c->thist.cap / 2;
+  if (a.tiles && nb > 0) c->thist_par ^= 1u;  // (no launch without queries: nothing added or cleared)
+  uint32_t* thist_cur = c->thist.p + c->thist_par * half;
+  a.thist_clear = c->thist.p + (1u - c->thist_par) * half;
+  a.thist_clear_n = a.tiles ? (uint32_t)half : 0u;
   c->hist_off.ensure((size_t)K * (a.ntl_pl + a.ntl_pt) + 1);
   const SortOut so{c->hist_off.p, c->pair_counts.p, c->pair_base.p, c->chunk_range.p, c->chunks.p, c->n_chunks.p};
   c->h_counts.ensure(2 * (size_t)K + 4);
@@ -2600,7 +2937,7 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
       hipLaunchKernelGGL(kern, dim3(nb), dim3(kMatchThreads), K * sizeof(uint32_t), st, a,
                          view(0), view(1), c->q_pl_pos.p, c->q_pt_pos.p, c->map_inv_p, c->m_pair.p, c->m_d2.p, c->m_pi.p,
                          c->m_ni.p, c->m_ins.p, c->hist.p, c->work.p, c->mcnt.p, c->mticket.p, c->h_counts.d,
-                         c->ins_blk.p, c->ins_off.p, c->thist.p, so, FusedArgs{});
+                         c->ins_blk.p, c->ins_off.p, thist_cur, so, FusedArgs{});
       FMX_HIP(hipGetLastError());
     }
   }
@@ -2613,7 +2950,8 @@ void run_match(fmx_ctx* c, const double* pose_j34, double max_dist, double min_d
   // kernel's last block (tiled) or from the scan + k_pair_base (wider windows) right
   // away; the row scatter itself may be deferred (defer_scatter: fmx_match, whose
   // caller may only read the query-order outputs) until run_pair_scatter.
-  c->ps = PairScatter{a.nb_pl, nb_pt, a.ntl_pl, a.ntl_pt, a.K, a.tiles};
+  c->ps = PairScatter{a.nb_pl, nb_pt, a.ntl_pl, a.ntl_pt, a.K, a.tiles, (uint32_t)(thist_cur - c->thist.p),
+                      a.prof_work};
   c->scatter_pending = false;
   if (sorted && !a.tiles) {
     ProfScope ps(c->prof, PROF_PAIR_SORT, 0.0, st);
@@ -2762,6 +3100,11 @@ void work_fetch(fmx_ctx* c) {
 // Consume the asynchronously copied match counts (caller has synchronized or will).
 void match_counts_fetch(fmx_ctx* c, bool wait) {
   if (!c->counts_pending) return;
+  // kTilesScatter: the counts come from the pair scatter's meta block
+  if (c->scatter_pending && c->ps.tiles == kTilesScatter) {
+    run_pair_scatter(c);
+    wait = true;
+  }
   if (wait) stream_wait(c);
   const int K = std::max<int>((int)c->K, 1);
   c->cnt_pl.assign(c->h_counts.p, c->h_counts.p + c->K);

@@ -19,6 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 _SCRIPT = r'''
 import sys
+import torch  # first, as in every GPU process here: libfmx then binds torch's HIP runtime
 root = sys.argv[1]
 for p in (root, root + "/oracle", root + "/tests"):
     sys.path.insert(0, p)
