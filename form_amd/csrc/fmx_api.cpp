@@ -1559,28 +1559,26 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
   c->P = *p;
   c->device = device;
   fmx_status st = guard(c, [&] {
-    // the context stream carries the registration's critical path: highest priority;
-    // the side stream (map build beside the extraction, speculative matches beside the
-    // LM) the lowest, so its blocks yield the CUs to the critical path's
+    // the context stream carries the registration's critical path: highest priority
     int prio_lo = 0, prio_hi = 0;
     FMX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     FMX_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
-    const char* cus = std::getenv("FMX_SIDE_CUS");  // EXPERIMENT (A/B): side streams on N CUs
-    if (cus && std::atoi(cus) > 0) {
+    // The side streams (pipelined extraction, speculative map build) run on half of the
+    // CUs: their 1024-thread blocks otherwise occupy every CU while the ICP loop's
+    // window linearizations and matches wait for CU room (a linearization overlapping
+    // k_normals took 39 instead of 10 us, profiles/r5_c4_trace_unprofiled.txt).  Measured
+    // (profiles/r6_ab_side_cus.txt): 128 of 256 CUs +3-8 % C4 scans/s; the extraction
+    // itself, off the critical path, takes ~2x as long.
+    {
       hipDeviceProp_t pr;
       FMX_HIP(hipGetDeviceProperties(&pr, device));
-      const int ncu = pr.multiProcessorCount, n = std::min(ncu, std::atoi(cus));
-      const bool spread = std::getenv("FMX_SIDE_CUS_SPREAD") != nullptr;
+      const char* cus = std::getenv("FMX_SIDE_CUS");  // EXPERIMENT (A/B): N CUs, 0 = unmasked
+      const int ncu = pr.multiProcessorCount, n = cus ? std::min(ncu, std::atoi(cus)) : std::max(1, ncu / 2);
       std::vector<uint32_t> m((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; ++i) {
-        const bool on = spread ? (int)((int64_t)i * n / ncu) != (int)((int64_t)(i + 1) * n / ncu) : i >= ncu - n;
-        if (on) m[i / 32] |= 1u << (i % 32);
-      }
+      for (int i = ncu - n; i < ncu; ++i) m[i / 32] |= 1u << (i % 32);
+      if (n <= 0) std::fill(m.begin(), m.end(), 0xFFFFFFFFu);
       FMX_HIP(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)m.size(), m.data()));
       FMX_HIP(hipExtStreamCreateWithCUMask(&c->side2, (uint32_t)m.size(), m.data()));
-    } else {
-      FMX_HIP(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_lo));
-      FMX_HIP(hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, prio_lo));
     }
     c->ev_fork.create();
     c->ev_join.create();

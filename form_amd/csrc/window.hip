@@ -145,8 +145,16 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
   WSTAMP(0);
   const uint32_t type = d.type & 0xFFu;
   const int slot = (int)d.pair;
-  // the pair's chunk range, in flight with the rows (used after the block sum)
+  // the pair's chunk range, in flight with the rows (used after the block sum); wave 0
+  // also counts the pairs with rows for the done ticket now, off the finisher's chain
   const uint32_t cb = a.chunk_range[slot], ce = a.chunk_range[slot + 1];
+  uint32_t n_ne = 0;
+  if (w == 0)
+    for (int k0 = 0; k0 < a.npairs; k0 += kWave) {
+      const int k = k0 + lane;
+      const bool ne = k < a.npairs && a.chunk_range[k + 1] > a.chunk_range[k];
+      n_ne += (uint32_t)__popcll(__ballot(ne));
+    }
   int pi, pj;
   if (a.implicit_j >= 0) {
     pi = slot;
@@ -276,13 +284,8 @@ __global__ __launch_bounds__(kWinWaves * kWave) void k_win_linearize(WinArgs a, 
   __syncthreads();
   WSTAMP(4);
   if (w != 0) return;
-  // pairs with rows (the others have no chunk and never finish; the host zeroes them)
-  uint32_t n_ne = 0;
-  for (int k0 = 0; k0 < a.npairs; k0 += kWave) {
-    const int k = k0 + lane;
-    const bool ne = k < a.npairs && a.chunk_range[k + 1] > a.chunk_range[k];
-    n_ne += (uint32_t)__popcll(__ballot(ne));
-  }
+  // n_ne: the pairs with rows (the others have no chunk and never finish; the host
+  // zeroes them)
   uint32_t t = 0;
   if (lane == 0) t = __hip_atomic_fetch_add(a.done_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   t = __shfl(t, 0, 64);
