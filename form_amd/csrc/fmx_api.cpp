@@ -1563,17 +1563,19 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     int prio_lo = 0, prio_hi = 0;
     FMX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     FMX_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
-    // The side streams (pipelined extraction, speculative map build) run on half of the
-    // CUs: their 1024-thread blocks otherwise occupy every CU while the ICP loop's
-    // window linearizations and matches wait for CU room (a linearization overlapping
-    // k_normals took 39 instead of 10 us, profiles/r5_c4_trace_unprofiled.txt).  Measured
-    // (profiles/r6_ab_side_cus.txt): 128 of 256 CUs +3-8 % C4 scans/s; the extraction
-    // itself, off the critical path, takes ~2x as long.
+    // The side streams (pipelined extraction, speculative map build) run on a quarter of
+    // the CUs: their 1024-thread blocks (k_normals: ~147 KB of LDS each) otherwise occupy
+    // every CU while the ICP loop's window linearizations and matches wait for CU room (a
+    // linearization overlapping k_normals took 39 instead of 10 us,
+    // profiles/r5_c4_trace_unprofiled.txt).  Measured (profiles/r6_ab_side_cus.txt, 3 reps
+    // x 120 scans): unmasked 1412, 32 CUs 1316, 64 CUs 1460, 128 CUs 1442 scans/s; the
+    // extraction itself, off the critical path, takes ~3.5x as long (and at 32 CUs no
+    // longer finishes before the next scan needs it).
     {
       hipDeviceProp_t pr;
       FMX_HIP(hipGetDeviceProperties(&pr, device));
       const char* cus = std::getenv("FMX_SIDE_CUS");  // EXPERIMENT (A/B): N CUs, 0 = unmasked
-      const int ncu = pr.multiProcessorCount, n = cus ? std::min(ncu, std::atoi(cus)) : std::max(1, ncu / 2);
+      const int ncu = pr.multiProcessorCount, n = cus ? std::min(ncu, std::atoi(cus)) : std::max(1, ncu / 4);
       std::vector<uint32_t> m((ncu + 31) / 32, 0u);
       for (int i = ncu - n; i < ncu; ++i) m[i / 32] |= 1u << (i % 32);
       if (n <= 0) std::fill(m.begin(), m.end(), 0xFFFFFFFFu);
