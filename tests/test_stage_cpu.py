@@ -30,3 +30,15 @@ def test_stage_helpers_respect_a_restricted_mask():
         r = subprocess.run([path], capture_output=True, text=True, timeout=300, env=env,
                            preexec_fn=lambda: os.sched_setaffinity(0, set(cpus)))
         assert r.returncode == 0 and "stage ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+def test_smoother_host():
+    """The window smoother's host LM (form_amd/csrc/smoother.cpp: dense LM with priors, a
+    linear container factor and callback-linearized pair factors, plain and split form;
+    Schur marginal; Cholesky up to D = 108) — tests/cpp/test_smoother.cpp, also run under
+    ASan + UBSan by tools/asan_check.sh."""
+    path = os.path.join(ROOT, "tests", "cpp", "test_smoother")
+    if not os.path.exists(path):
+        pytest.fail(f"{path} missing: run __graft_entry__.build() (make -C tests/cpp)")
+    r = subprocess.run([path], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "smoother ok" in r.stdout, r.stdout + r.stderr[-3000:]
