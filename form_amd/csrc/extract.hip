@@ -1057,11 +1057,8 @@ __global__ __launch_bounds__(kNrmThreads) void k_normals(const float4* __restric
   float4* s_hi = s_lo + 2 * nblk;                           // [2][nblk]
   int2* s_cl = reinterpret_cast<int2*>(s_hi + 2 * nblk);    // [cap_pl] closest columns in r-1 / r+1
   unsigned long long* s_best = reinterpret_cast<unsigned long long*>(s_cl + a.cap_pl);  // [cap_pl]
-  int* s_col = reinterpret_cast<int*>(s_best + a.cap_pl);                              // [cap_pl] selected columns
-  // phase-2 work items, (this block's slot - s_beg) << 6 | block: 16 bits, and only this
-  // block's half of the slots — ~10 KB instead of 39 KB of LDS at C4, so that a window
-  // linearization's 30-KB blocks fit beside a k_normals block on its CU (extract_launch)
-  uint16_t* s_items = reinterpret_cast<uint16_t*>(s_col + a.cap_pl);                   // [hs_max * nblk]
+  uint32_t* s_items = reinterpret_cast<uint32_t*>(s_best + a.cap_pl);                   // [cap_pl * nblk]
+  int* s_col = reinterpret_cast<int*>(s_items + (size_t)a.cap_pl * nblk);              // [cap_pl] selected columns
   const int tid = threadIdx.x;
   __shared__ int s_found;
   __shared__ int s_nitems;
@@ -1208,7 +1205,7 @@ __global__ __launch_bounds__(kNrmThreads) void k_normals(const float4* __restric
         int base = 0;
         if (lane_id() == 0 && m) base = atomicAdd(&s_nitems, __popcll(m));
         base = __shfl(base, 0, 64);
-        if (keep) s_items[base + __popcll(m & lanemask_lt())] = (uint16_t)((s - s_beg) << 6 | bk);  // nblk <= 64
+        if (keep) s_items[base + __popcll(m & lanemask_lt())] = (uint32_t)(s * 64 + bk);  // nblk <= 32
       }
     }
     __syncthreads();
@@ -1219,7 +1216,7 @@ __global__ __launch_bounds__(kNrmThreads) void k_normals(const float4* __restric
 
     for (int q = tl; q < nitems; q += 256) {
       const uint32_t it = s_items[q];
-      const int s = s_beg + (int)(it >> 6), bk = (int)(it & 63);
+      const int s = (int)(it >> 6), bk = (int)(it & 63);
       const float4 p = s_row[CP + px(s_col[s])];
       unsigned long long kb = ~0ull;
 #pragma unroll 4
@@ -1502,11 +1499,10 @@ ExLaunch extract_launch(fmx_ctx* c, const float4* d_scan, int R, int C, hipStrea
   const int nblk = (C + 63) / 64;
   // k_normals: one workgroup per line, rows r-1..r+1 in LDS (160 KB per CU, minus
   // the kernel's few static bytes)
-  const size_t hs_max = ((size_t)a.cap_pl + 1) / 2;  // a block's slots (two blocks per line)
   const size_t lds_n = (size_t)3 * (C + (C >> 6) + 1) * 16 + (size_t)4 * nblk * 16 + (size_t)a.cap_pl * 20 +
-                       hs_max * nblk * 2;
+                       (size_t)a.cap_pl * nblk * 4;
   constexpr size_t kNrmLdsMax = 160 * 1024 - 256;
-  if (C <= kNrmMaxC && lds_n <= kNrmLdsMax && hs_max <= 1024 && nblk <= 64) {
+  if (C <= kNrmMaxC && lds_n <= kNrmLdsMax) {
     if (!c->nrm_attr_set) {
       FMX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_normals<5>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNrmLdsMax));
