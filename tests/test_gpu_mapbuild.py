@@ -3,7 +3,8 @@ its edges, checked through bit-exact matches against the oracle's VoxelMap::find
 (map.tpp:70-91): 70 rebuilds of one context (the 6-bit build epoch wraps and the table is
 cleared once, claim slots / counts reused across builds of different sizes), and maps
 whose cells hold hundreds and more than 8192 records (the dense path: sub-cell sort, and
-a cell too large to sort, walked whole)."""
+a cell too large to sort, walked whole), and a 7.9M-record two-scan map of both
+feature types (the interleaved record layout of the C5 maps)."""
 import numpy as np
 import pytest
 
@@ -12,6 +13,7 @@ from scenario import perturb, stream_features
 pytestmark = pytest.mark.gpu
 
 W = 0.8
+I34_ = np.hstack([np.eye(3), np.zeros((3, 1))])
 
 
 def _check(ctx, omaps, Q, Tj, K):
@@ -87,3 +89,54 @@ def test_dense_and_oversized_cells(fmx_mod, oracle, n_big):
     Qpt = np.vstack([c0 + rng.uniform(-0.6, 0.6, size=(300, 3)), rng.uniform(-3, 3, size=(300, 3))]).astype(np.float32)
     ctx.set_queries(Qpl, Qpt, 1)
     _check(ctx, omaps, (Qpl, Qpt), I34, 1)
+
+
+def test_large_build_two_scans_both_types(fmx_mod, oracle):
+    """A C5-sized map shape (run_map_build's interleaved record layout, >= 4M records)
+    from two scans at different poses and both feature types: 5.3M planar + 2.6M point
+    records, every match of 24k queries bit-exact against the oracle's VoxelMap, and a
+    rebuild of the same context (new epoch, the cells' record order set by the atomics
+    again) giving the same matches."""
+    import torch
+    from form_amd import shard, synth
+    side = 2300
+    pos4, nrm4 = shard.terrain_map(side, W, synth.SEED + 5, "cuda:0")
+    n = pos4.shape[0]
+    h = n // 2
+    pt4 = pos4[::2].contiguous()  # the point features: every second terrain sample
+    hp = pt4.shape[0] // 2
+    T1 = shard.expmap(np.array([0.001, -0.002, 0.003, 0.4, -0.3, 0.05]))
+    poses = np.stack([I34_, T1])
+    T1inv = np.linalg.inv(np.vstack([T1, [0, 0, 0, 1]]))[:3]
+
+    def to_local(x4, T):  # scan 1's records are stored in its own frame
+        x = x4[:, :3].double() @ torch.tensor(T[:, :3].T, device=x4.device) + torch.tensor(T[:, 3], device=x4.device)
+        return torch.cat([x.float(), x4[:, 3:]], 1).contiguous()
+    T1inv_rot = np.hstack([T1inv[:, :3], np.zeros((3, 1))])
+    pl0, nl0 = pos4[:h].contiguous(), nrm4[:h].contiguous()
+    pl1, nl1 = to_local(pos4[h:], T1inv), to_local(nrm4[h:], T1inv_rot)
+    pp0, pp1 = pt4[:hp].contiguous(), to_local(pt4[hp:], T1inv)
+    torch.cuda.synchronize()
+    ctx = fmx_mod.Context(fmx_mod.EstimatorParams(keypoint_pool_capacity=n + 1024, voxel_subdivision=1))
+    ctx.keypoints_add_device(0, pl0, nl0, pp0)
+    ctx.keypoints_add_device(1, pl1, nl1, pp1)
+    omaps = [oracle.VoxelMap(W, 0), oracle.VoxelMap(W, 1)]
+    for k, (pl, nl, pp) in enumerate(((pl0, nl0, pp0), (pl1, nl1, pp1))):
+        omaps[0].add_scan(k, poses[k], torch.cat([pl[:, :3], nl[:, :3]], 1).cpu().numpy())
+        omaps[1].add_scan(k, poses[k], pp[:, :3].cpu().numpy())
+    rng = np.random.default_rng(3)
+    qi = rng.choice(n, 16000, replace=False)
+    qp = rng.choice(pt4.shape[0], 8000, replace=False)
+    Qpl = np.concatenate([pos4[qi, :3].cpu().numpy(), nrm4[qi, :3].cpu().numpy()], 1)
+    Qpl[:, :3] += rng.normal(0, 0.05, (len(qi), 3)).astype(np.float32)
+    Qpt = pt4[qp, :3].cpu().numpy() + rng.normal(0, 0.05, (len(qp), 3)).astype(np.float32)
+    ctx.set_queries(Qpl, Qpt, 2)
+    Tj = shard.expmap(np.array([0.0003, 0.0002, -0.0004, 0.01, -0.02, 0.005]))
+    got = []
+    for _ in range(2):
+        ctx.map_build([0, 1], poses, W)
+        _check(ctx, omaps, (Qpl, Qpt), Tj, 2)
+        got.append(ctx.match_download())
+    for k in ("pair", "d2", "pi", "ni"):
+        assert np.array_equal(got[0][k], got[1][k]), k
+    ctx.close()
