@@ -668,7 +668,7 @@ ALG_BYTES_MODEL = {
              "a query the warm certificate settles probes and tests nothing (round 4: 87-92 % of warm queries)",
     "match_linearize": "per query 16 B read (+32 B planar normal of the winner unless the map interleaves it "
                        "with the position); 64 B per brick probe; per candidate record its line: 32 B, or 64 B "
-                       "interleaved (>= FMX_INTERLEAVE_MIN records: C5); 256 B of block partials per block",
+                       "interleaved (maps of >= 4M records: C5); 256 B of block partials per block",
     "map_build": "SURVEY.md §8(d) B_build = 2 (32 M_pl + 16 M_pt) + 16 S: the local records read and the "
                  "world-sorted records written at the local size, 16 B per hash slot, S = 2 M (load 0.5)",
     "window": "72 B per plane row (p_i, n_i, p_j as fp64) + 48 B per point pair + 92 doubles of G per pair",

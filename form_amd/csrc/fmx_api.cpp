@@ -601,8 +601,8 @@ struct fmx_ctx::Est {
   // keyed (j, i): m_fast_linear and marginalize reuse it
   std::map<std::pair<uint64_t, uint64_t>, std::vector<double>> gcache;
   // pair moments (moments.hpp) of every stored pair, keyed (j, i): the rows of scan j's
-  // last match, taken at reference poses; the LMs linearize the pairs from them on the
-  // host (FMX_LIN_ROWS=1: the per-row device linearization over the window store instead)
+  // last match, taken at reference poses; under FMX_MOMENTS=1 the LMs linearize the pairs
+  // from them on the host
   struct Mom {
     Pose ref_i, ref_j;
     std::vector<double> phi;  // kMomPairD
