@@ -243,98 +243,127 @@ __attribute__((target("avx2,fma"))) void chol_back_fma(const double* a, int n, c
   }
 }
 
-// AVX-512 form (the GPU box's EPYC has it): panel of 8 rows, every trailing row
-// updated as whole 8-wide column vectors starting at the vector that holds its
-// diagonal — the few entries left of the diagonal are lower-triangle scratch the
-// factor never reads, so no scalar heads or tails (masked loads for n % 8).  Two
-// trailing rows per pass share each panel load.  Same update order per element as
-// the AVX2 form (k ascending), FMA rounding.
 __attribute__((target("avx512f,fma"))) inline __mmask8 tail_mask(int left) {
   return left >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << left) - 1u);
 }
 
-template <int NB>
-__attribute__((target("avx512f,fma"))) void chol_trail_512(double* a, int n, int kb, int ke, int nb) {
-  const int nt = NB > 0 ? NB : nb;
-  const double* U[8];
-  for (int t = 0; t < nt; ++t) U[t] = a + (size_t)(kb + t) * n;
-  int i = ke;
-  for (; i + 2 <= n; i += 2) {
-    double* __restrict A0 = a + (size_t)i * n;
-    double* __restrict A1 = A0 + n;
-    __m512d b0[8], b1[8];
-    for (int t = 0; t < nt; ++t) {
-      b0[t] = _mm512_set1_pd(U[t][i]);
-      b1[t] = _mm512_set1_pd(U[t][i + 1]);
-    }
-    int m = i & ~7;
-    for (; m + 16 <= n; m += 16) {  // two column vectors: four independent FMA chains
-      __m512d x0 = _mm512_loadu_pd(A0 + m), x1 = _mm512_loadu_pd(A1 + m);
-      __m512d y0 = _mm512_loadu_pd(A0 + m + 8), y1 = _mm512_loadu_pd(A1 + m + 8);
-      for (int t = 0; t < nt; ++t) {
-        const __m512d uu = _mm512_loadu_pd(U[t] + m), vv = _mm512_loadu_pd(U[t] + m + 8);
-        x0 = _mm512_fnmadd_pd(b0[t], uu, x0);
-        x1 = _mm512_fnmadd_pd(b1[t], uu, x1);
-        y0 = _mm512_fnmadd_pd(b0[t], vv, y0);
-        y1 = _mm512_fnmadd_pd(b1[t], vv, y1);
+// The trailing rows i0 .. i0 + R - 1 take the 8 updates of panel rows kb .. kb + 7 in a
+// register tile: R rows x 3 column vectors (24 columns) per pass, each panel row's
+// three vectors loaded once for the R rows (its entries in rows i0 .. as embedded
+// broadcasts), then 8-wide (masked) vectors to the row end.  Columns start at the
+// vector holding row i0's diagonal; rows below i0 write lower-triangle scratch there.
+template <int R>
+__attribute__((target("avx512f,fma"))) inline void chol_tile_512(double* a, int n, int kb, int i0) {
+  const double* U = a + (size_t)kb * n;
+  double* A = a + (size_t)i0 * n;
+  int m = i0 & ~7;
+  for (; m + 24 <= n; m += 24) {
+    __m512d x[R][3];
+#pragma GCC unroll 16
+    for (int r = 0; r < R; ++r)
+#pragma GCC unroll 16
+      for (int v = 0; v < 3; ++v) x[r][v] = _mm512_loadu_pd(A + (size_t)r * n + m + 8 * v);
+#pragma GCC unroll 16
+    for (int t = 0; t < 8; ++t) {
+      const double* Ut = U + (size_t)t * n;
+      const __m512d u0 = _mm512_loadu_pd(Ut + m), u1 = _mm512_loadu_pd(Ut + m + 8), u2 = _mm512_loadu_pd(Ut + m + 16);
+#pragma GCC unroll 16
+      for (int r = 0; r < R; ++r) {
+        const __m512d b = _mm512_set1_pd(Ut[i0 + r]);
+        x[r][0] = _mm512_fnmadd_pd(b, u0, x[r][0]);
+        x[r][1] = _mm512_fnmadd_pd(b, u1, x[r][1]);
+        x[r][2] = _mm512_fnmadd_pd(b, u2, x[r][2]);
       }
-      _mm512_storeu_pd(A0 + m, x0);
-      _mm512_storeu_pd(A1 + m, x1);
-      _mm512_storeu_pd(A0 + m + 8, y0);
-      _mm512_storeu_pd(A1 + m + 8, y1);
     }
-    for (; m < n; m += 8) {
-      const __mmask8 k = tail_mask(n - m);
-      __m512d x0 = _mm512_maskz_loadu_pd(k, A0 + m), x1 = _mm512_maskz_loadu_pd(k, A1 + m);
-      for (int t = 0; t < nt; ++t) {
-        const __m512d uu = _mm512_maskz_loadu_pd(k, U[t] + m);
-        x0 = _mm512_fnmadd_pd(b0[t], uu, x0);
-        x1 = _mm512_fnmadd_pd(b1[t], uu, x1);
-      }
-      _mm512_mask_storeu_pd(A0 + m, k, x0);
-      _mm512_mask_storeu_pd(A1 + m, k, x1);
-    }
+#pragma GCC unroll 16
+    for (int r = 0; r < R; ++r)
+#pragma GCC unroll 16
+      for (int v = 0; v < 3; ++v) _mm512_storeu_pd(A + (size_t)r * n + m + 8 * v, x[r][v]);
   }
-  for (; i < n; ++i) {
-    double* __restrict A0 = a + (size_t)i * n;
-    __m512d b0[8];
-    for (int t = 0; t < nt; ++t) b0[t] = _mm512_set1_pd(U[t][i]);
-    for (int m = i & ~7; m < n; m += 8) {
-      const __mmask8 k = tail_mask(n - m);
-      __m512d x0 = _mm512_maskz_loadu_pd(k, A0 + m);
-      for (int t = 0; t < nt; ++t) x0 = _mm512_fnmadd_pd(b0[t], _mm512_maskz_loadu_pd(k, U[t] + m), x0);
-      _mm512_mask_storeu_pd(A0 + m, k, x0);
+  for (; m < n; m += 8) {
+    const __mmask8 k = tail_mask(n - m);
+    __m512d x[R];
+#pragma GCC unroll 16
+    for (int r = 0; r < R; ++r) x[r] = _mm512_maskz_loadu_pd(k, A + (size_t)r * n + m);
+#pragma GCC unroll 16
+    for (int t = 0; t < 8; ++t) {
+      const double* Ut = U + (size_t)t * n;
+      const __m512d u = _mm512_maskz_loadu_pd(k, Ut + m);
+#pragma GCC unroll 16
+      for (int r = 0; r < R; ++r) x[r] = _mm512_fnmadd_pd(_mm512_set1_pd(Ut[i0 + r]), u, x[r]);
     }
+#pragma GCC unroll 16
+    for (int r = 0; r < R; ++r) _mm512_mask_storeu_pd(A + (size_t)r * n + m, k, x[r]);
   }
 }
 
+// AVX-512 form (the GPU box's EPYC has it), blocked by 8 rows: (1) the panel's diagonal
+// block factored in a local 8 x 8 copy; (2) the panel's strip (columns >= ke) solved in
+// registers, the 8 rows of two 8-column vectors at a time (x_k -= U[t][k] x_t for t < k,
+// then x_k *= 1 / u_kk); (3) the trailing rows updated in 4-row register tiles
+// (chol_tile_512).  Every element still takes its updates k = 0, 1, ... in order as
+// fused multiply-adds and each row is scaled by its pivot's reciprocal, so the factor is
+// bit for bit the scalar FMA recurrence's (tests/cpp/test_smoother.cpp checks it), as the
+// row-at-a-time form it replaces was; the panel no longer round-trips every strip row
+// through memory once per pivot.
 __attribute__((target("avx512f,fma"))) bool chol_solve_512(double* a, const double* g, double* x, int n) {
   for (int kb = 0; kb < n; kb += 8) {
-    const int ke = std::min(n, kb + 8);
-    for (int k = kb; k < ke; ++k) {  // panel
-      double* __restrict Uk = a + (size_t)k * n;
-      const double s = Uk[k];
+    const int ke = std::min(n, kb + 8), nb = ke - kb;
+    double B[8][8], rk[8];
+    for (int i = 0; i < nb; ++i)
+      for (int m = i; m < nb; ++m) B[i][m] = a[(size_t)(kb + i) * n + kb + m];
+    for (int k = 0; k < nb; ++k) {
+      const double s = B[k][k];
       if (!(s > 0)) return false;
-      const double ukk = std::sqrt(s);
-      const __m512d r = _mm512_set1_pd(1.0 / ukk);
-      for (int m = k & ~7; m < n; m += 8) {
-        const __mmask8 msk = tail_mask(n - m);
-        _mm512_mask_storeu_pd(Uk + m, msk, _mm512_mul_pd(_mm512_maskz_loadu_pd(msk, Uk + m), r));
-      }
-      Uk[k] = ukk;
-      for (int i = k + 1; i < ke; ++i) {
-        double* __restrict Ai = a + (size_t)i * n;
-        const __m512d u = _mm512_set1_pd(Uk[i]);
-        for (int m = i & ~7; m < n; m += 8) {
-          const __mmask8 msk = tail_mask(n - m);
-          _mm512_mask_storeu_pd(Ai + m, msk,
-                                _mm512_fnmadd_pd(u, _mm512_maskz_loadu_pd(msk, Uk + m), _mm512_maskz_loadu_pd(msk, Ai + m)));
+      const double ukk = std::sqrt(s), r = 1.0 / ukk;
+      for (int m = k + 1; m < nb; ++m) B[k][m] = B[k][m] * r;
+      B[k][k] = ukk;
+      rk[k] = r;
+      for (int i = k + 1; i < nb; ++i)
+        for (int m = i; m < nb; ++m) B[i][m] = __builtin_fma(-B[k][i], B[k][m], B[i][m]);
+    }
+    for (int i = 0; i < nb; ++i)
+      for (int m = i; m < nb; ++m) a[(size_t)(kb + i) * n + kb + m] = B[i][m];
+    if (ke == n) break;  // (nb == 8 below: only the last panel is short)
+    double* P = a + (size_t)kb * n;
+    int m = ke;
+    for (; m + 16 <= n; m += 16) {
+      __m512d x0[8], x1[8];
+#pragma GCC unroll 16
+      for (int k = 0; k < 8; ++k) {
+        __m512d v0 = _mm512_loadu_pd(P + (size_t)k * n + m), v1 = _mm512_loadu_pd(P + (size_t)k * n + m + 8);
+#pragma GCC unroll 16
+        for (int t = 0; t < k; ++t) {
+          const __m512d b = _mm512_set1_pd(B[t][k]);
+          v0 = _mm512_fnmadd_pd(b, x0[t], v0);
+          v1 = _mm512_fnmadd_pd(b, x1[t], v1);
         }
+        const __m512d r = _mm512_set1_pd(rk[k]);
+        x0[k] = _mm512_mul_pd(v0, r);
+        x1[k] = _mm512_mul_pd(v1, r);
+        _mm512_storeu_pd(P + (size_t)k * n + m, x0[k]);
+        _mm512_storeu_pd(P + (size_t)k * n + m + 8, x1[k]);
       }
     }
-    if (ke < n) {
-      if (ke - kb == 8) chol_trail_512<8>(a, n, kb, ke, 8);
-      else chol_trail_512<0>(a, n, kb, ke, ke - kb);
+    for (; m < n; m += 8) {
+      const __mmask8 msk = tail_mask(n - m);
+      __m512d x0[8];
+#pragma GCC unroll 16
+      for (int k = 0; k < 8; ++k) {
+        __m512d v0 = _mm512_maskz_loadu_pd(msk, P + (size_t)k * n + m);
+#pragma GCC unroll 16
+        for (int t = 0; t < k; ++t) v0 = _mm512_fnmadd_pd(_mm512_set1_pd(B[t][k]), x0[t], v0);
+        x0[k] = _mm512_mul_pd(v0, _mm512_set1_pd(rk[k]));
+        _mm512_mask_storeu_pd(P + (size_t)k * n + m, msk, x0[k]);
+      }
+    }
+    int i = ke;
+    for (; i + 4 <= n; i += 4) chol_tile_512<4>(a, n, kb, i);
+    switch (n - i) {
+      case 3: chol_tile_512<3>(a, n, kb, i); break;
+      case 2: chol_tile_512<2>(a, n, kb, i); break;
+      case 1: chol_tile_512<1>(a, n, kb, i); break;
+      default: break;
     }
   }
   // forward U^T y = g (y in x), then back U x = y

@@ -93,6 +93,38 @@ int main() {
     }
   printf("lm iters %d lins %d, max |x - truth| %.3e, split vs plain %.3e\n", R1.iters, R1.lins, err, diff);
   if (!(err < 1e-6) || diff != 0.0) return 1;
+  // Cholesky factor bit for bit against the scalar FMA recurrence (right-looking, k
+  // ascending per element, rows scaled by the reciprocal of the pivot): every FMA host
+  // path (AVX2, AVX-512, any blocking) must round exactly like it
+  if (__builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) {
+    for (int D : {6, 7, 13, 18, 61, 96, 108, 150, 157}) {
+      std::vector<double> M((size_t)D * D), H((size_t)D * D), g0(D), xs(D);
+      for (double& v : M) v = nd(rng);
+      for (int i = 0; i < D; ++i)
+        for (int j = 0; j < D; ++j) {
+          double s = i == j ? D : 0.0;
+          for (int k = 0; k < D; ++k) s += M[(size_t)i * D + k] * M[(size_t)j * D + k];
+          H[(size_t)i * D + j] = s;
+        }
+      for (double& v : g0) v = nd(rng);
+      std::vector<double> R = H;
+      for (int k = 0; k < D; ++k) {
+        double* Uk = &R[(size_t)k * D];
+        const double ukk = std::sqrt(Uk[k]), r = 1.0 / ukk;
+        for (int m = k + 1; m < D; ++m) Uk[m] = Uk[m] * r;
+        Uk[k] = ukk;
+        for (int i = k + 1; i < D; ++i)
+          for (int m = i; m < D; ++m) R[(size_t)i * D + m] = std::fma(-Uk[i], Uk[m], R[(size_t)i * D + m]);
+      }
+      std::vector<double> F = H;
+      if (!chol_solve(F, g0.data(), xs.data(), D)) return 5;
+      size_t diff = 0;
+      for (int i = 0; i < D; ++i)
+        for (int m = i; m < D; ++m) diff += F[(size_t)i * D + m] != R[(size_t)i * D + m];
+      printf("D %3d: factor entries differing from the FMA recurrence: %zu\n", D, diff);
+      if (diff) return 6;
+    }
+  }
   // Schur marginal and Cholesky on random SPD augmented systems
   for (int D : {6, 18, 61, 108}) {
     std::vector<double> M((size_t)D * D), A((size_t)(D + 1) * (D + 1), 0.0), g0(D), xs(D);

@@ -37,8 +37,8 @@ for k,v in d['kernels'].items(): print('$w', k, v.get('hbm_bytes_per_launch'), r
   fi
   for w in ${CPATH:-c4 c2}; do
     rm -rf $D/prof_$w
-    # default --steps 40 (+ a 40-scan profile pass after them: skip 40)
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof_$w -o run --output-format csv -- python bench.py --workload $w --no-cpu-baseline --no-c5 --no-ablation --sub-workloads= --no-host-input --streams= > $D/bench_prof_$w.json 2> $D/prof_$w.err || { tail -20 $D/prof_$w.err; exit 1; }
+    # --steps 40 (+ a 40-scan profile pass after them: skip 40)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof_$w -o run --output-format csv -- python bench.py --workload $w --steps 40 --warmup 10 --no-cpu-baseline --no-c5 --no-ablation --sub-workloads= --no-host-input --streams= > $D/bench_prof_$w.json 2> $D/prof_$w.err || { tail -20 $D/prof_$w.err; exit 1; }
     T=$(find $D/prof_$w -name "*kernel_trace.csv" | head -1)
     python tools/critical_path.py $T 40 $D/critical_path_$w.json 40 > /dev/null || exit 1
     python tools/trace_gaps.py $T > $D/trace_gaps_$w.txt 2>&1 || true
