@@ -3,6 +3,7 @@
 // device stages.  Host code only; built with hipcc -ffp-contract=off so the pose
 // algebra rounds like the reference's SSE2 Eigen/GTSAM code.
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -1570,15 +1571,25 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     // profiles/r5_c4_trace_unprofiled.txt).  Measured (profiles/r6_ab_side_cus.txt, 3 reps
     // x 120 scans): unmasked 1412, 32 CUs 1316, 64 CUs 1460, 128 CUs 1442 scans/s; the
     // extraction itself, off the critical path, takes ~3.5x as long (and at 32 CUs no
-    // longer finishes before the next scan needs it).
+    // longer finishes before the next scan needs it).  Mask bits come in groups of 8 = one
+    // CU of each XCD (tools/flagbench/cumaskmap.hip), so any aligned run of 64 bits is 8 CUs
+    // of every XCD.  Successive contexts of the process take successive quarters, so that
+    // contexts serving concurrent streams do not pile their side work onto the same CUs
+    // (4 streams on one GPU: 1421-1667 scans/s with one shared quarter, profiles/
+    // r6_end_bench_spread.txt).  FMX_SIDE_CUS: the side streams' CU count (0 = all CUs).
     {
+      static std::atomic<uint32_t> ctx_seq{0};
       hipDeviceProp_t pr;
       FMX_HIP(hipGetDeviceProperties(&pr, device));
-      const char* cus = std::getenv("FMX_SIDE_CUS");  // EXPERIMENT (A/B): N CUs, 0 = unmasked
+      const char* cus = std::getenv("FMX_SIDE_CUS");
       const int ncu = pr.multiProcessorCount, n = cus ? std::min(ncu, std::atoi(cus)) : std::max(1, ncu / 4);
       std::vector<uint32_t> m((ncu + 31) / 32, 0u);
-      for (int i = ncu - n; i < ncu; ++i) m[i / 32] |= 1u << (i % 32);
-      if (n <= 0) std::fill(m.begin(), m.end(), 0xFFFFFFFFu);
+      if (n <= 0) {
+        std::fill(m.begin(), m.end(), 0xFFFFFFFFu);
+      } else {
+        const int q = (int)(ctx_seq.fetch_add(1u) % (uint32_t)std::max(1, ncu / n));
+        for (int i = ncu - n * (q + 1); i < ncu - n * q; ++i) m[i / 32] |= 1u << (i % 32);
+      }
       FMX_HIP(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)m.size(), m.data()));
       FMX_HIP(hipExtStreamCreateWithCUMask(&c->side2, (uint32_t)m.size(), m.data()));
     }
