@@ -1576,7 +1576,9 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     // of every XCD.  Successive contexts of the process take successive quarters, so that
     // contexts serving concurrent streams do not pile their side work onto the same CUs
     // (4 streams on one GPU: 1421-1667 scans/s with one shared quarter, profiles/
-    // r6_end_bench_spread.txt).  FMX_SIDE_CUS: the side streams' CU count (0 = all CUs).
+    // r6_end_bench_spread.txt).  FMX_SIDE_CUS: the side streams' CU count (0 = all CUs;
+    // several contexts serving concurrent streams measured faster unmasked:
+    // profiles/r6_ab_side_cus_streams.txt).
     {
       static std::atomic<uint32_t> ctx_seq{0};
       hipDeviceProp_t pr;
