@@ -106,6 +106,7 @@ static void sync_all(fmx_ctx* c) {
   FMX_HIP(hipStreamSynchronize(c->stream));
   if (c->side) FMX_HIP(hipStreamSynchronize(c->side));
   if (c->side2) FMX_HIP(hipStreamSynchronize(c->side2));
+  if (c->lin) FMX_HIP(hipStreamSynchronize(c->lin));
 }
 // A match launch's algorithmic bytes: the per-launch part known at
 // launch time + 64 B per hash probe and per candidate record its line (32 B: position +
@@ -968,6 +969,7 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       }
     };
     bool launched = false, ready = false;  // (moments: captured by the LM's callbacks below)
+    int nlin = 0;                          // (rows: this LM's linearizations so far)
     if (mom) {
       // The pairs' moments at the LM's starting values: launched by the LM's first
       // linearization (split form: the host builds the base system and the non-pair
@@ -1030,13 +1032,17 @@ void smooth_register(fmx_ctx* c, fmx_ctx::Est& e, uint64_t j, uint32_t nfeat, co
       };
       set_lin(g, lin_begin, lin_end);
     } else {
-      // split form: launch, the host assembles the non-pair terms, then wait (smoother.hpp)
+      // split form: launch, the host assembles the non-pair terms, then wait (smoother.hpp).
+      // The LM's first linearization goes to the context stream (behind this iteration's
+      // match and scatter); its trials to the `lin` stream: their rows were final when the
+      // first one's word arrived, and a speculative match queued right after a trial
+      // (maybe_spec, on the context stream) then runs beside it instead of behind it.
       auto lin_begin = [&](const std::vector<Pose>& x) {
         table.resize(12 * ((size_t)K + 1));
         for (int k = 0; k < K; ++k) std::memcpy(&table[12 * k], x[slot.at(c->map_scans[k])].m, 12 * sizeof(double));
         std::memcpy(&table[12 * (size_t)K], x[slot.at(j)].m, 12 * sizeof(double));
         HostScope hs(10);
-        win_linearize_current(c, table.data(), sigma, nullptr);
+        win_linearize_current(c, table.data(), sigma, nullptr, nlin++ == 0 ? nullptr : c->lin);
         maybe_spec(x);
       };
       auto lin_end = [&](double* G) {
@@ -1564,6 +1570,7 @@ fmx_status fmx_create(const fmx_params* p, int device, fmx_ctx** out) {
     int prio_lo = 0, prio_hi = 0;
     FMX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     FMX_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
+    FMX_HIP(hipStreamCreateWithPriority(&c->lin, hipStreamNonBlocking, prio_hi));
     // The side streams (pipelined extraction, speculative map build) run on a quarter of
     // the CUs: their 1024-thread blocks (k_normals: ~147 KB of LDS each) otherwise occupy
     // every CU while the ICP loop's window linearizations and matches wait for CU room (a
@@ -1683,6 +1690,7 @@ void fmx_destroy(fmx_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->side2) (void)hipStreamDestroy(c->side2);
+  if (c->lin) (void)hipStreamDestroy(c->lin);
   c->ev_fork.destroy();
   c->ev_join.destroy();
   c->ev_pf.destroy();

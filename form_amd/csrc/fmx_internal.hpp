@@ -274,6 +274,7 @@ struct WinStore {
   bool pending = false;  // a k_win_linearize launched by win_start, not yet finished
   bool pending_mom = false;  // ... a k_win_moments (its results in hM)
   uint32_t pending_seq = 0, pending_grid = 0;
+  hipStream_t pending_st = nullptr;  // the stream the pending launch went to
   int pending_np = 0;
   HBuf<double> hG, hM, hposes;  // hM: per pair 2 x 136 moments (k_win_moments)
   HBuf<uint32_t> hmeta;
@@ -327,6 +328,7 @@ struct fmx_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;                    // map build, overlapped with extraction
   hipStream_t side2 = nullptr;                   // pipelined extraction of the announced next scan
+  hipStream_t lin = nullptr;                     // the ICP loop's LM trial linearizations (beside the speculative match)
   // stream -> side -> stream ordering.  Rings of events: each record takes the next one
   // and a wait uses the last recorded, so an event is never re-recorded while an earlier
   // cross-stream wait on it may still be pending in the runtime (a re-record right after
@@ -799,7 +801,7 @@ void win_remove(fmx_ctx* c, uint64_t s);
 std::vector<WinPair> win_pairs(fmx_ctx* c);
 void win_set_pairs(fmx_ctx* c, const std::vector<WinPair>& prs, const std::vector<uint64_t>& keys);
 void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double sigma, double* G_out);
-void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out);
+void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out, hipStream_t st = nullptr);
 void win_finish(fmx_ctx* c, double* G_out);  // completes a win_linearize_* / win_moments_* called with G_out = null
 // pair moments (k_win_moments): per pair 2 x 136 doubles (plane, point; packed upper 16 x 16)
 constexpr int kMomPair = 272;

@@ -595,10 +595,10 @@ void win_timing_collect(fmx_ctx* c, uint32_t grid_chunks) {
 // to a device scratch word; the caller all-reduces and copies (no win_finish).
 // mom: k_win_moments instead (per pair 2 x 136 doubles of moments, to W.hM)
 void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses, int nposes, double bytes,
-               double* out_dev = nullptr, bool mom = false) {
+               double* out_dev = nullptr, bool mom = false, hipStream_t st_launch = nullptr) {
   WinStore& W = c->win;
   if (W.pending) win_finish(c, nullptr);  // an abandoned one (error path): drain it first
-  hipStream_t st = c->stream;
+  hipStream_t st = st_launch ? st_launch : c->stream;
   WinPoses wp;
   WinPosesN<kWinSmallArgPoses> wps;
   if (nposes <= kWinSmallArgPoses) {
@@ -656,6 +656,7 @@ void win_start(fmx_ctx* c, WinArgs a, uint32_t grid_chunks, const double* poses,
     FMX_HIP(hipGetLastError());
   }
   W.pending = out_dev == nullptr;
+  W.pending_st = st;
   W.pending_seq = a.seq;
   W.pending_np = a.npairs;
   W.pending_mom = mom;
@@ -670,7 +671,7 @@ void win_finish(fmx_ctx* c, double* G_out) {
   W.pending = false;
   {
     HostScope hs(13);
-    wait_flag(c, c->h_flag.p, W.pending_seq);
+    wait_flag(c, c->h_flag.p, W.pending_seq, W.pending_st);
   }
   if (G_out) {
     if (W.pending_mom) std::memcpy(G_out, W.hM.p, (size_t)W.pending_np * 2 * kMomP * sizeof(double));
@@ -863,8 +864,12 @@ void win_linearize_stored(fmx_ctx* c, const double* poses, int nposes, double si
 
 // Same for the current scan's K pairs straight from the sorted match (device-built
 // chunk table): poses[k] = pose of map_scans[k], poses[K] = the current pose.
-void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out) {
+// st (null: the context stream): another stream, for a launch whose inputs the host has
+// already seen complete (the LM's trial linearizations, whose rows the LM's first
+// linearization on the context stream read before them).
+void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double* G_out, hipStream_t st) {
   if (!c->have_corr) throw StatusError(FMX_E_STATE, "win_linearize_current: no sorted match");
+  if (c->scatter_pending) st = nullptr;  // its rows are still to be written on the context stream
   run_pair_scatter(c);
   WinArgs a{};
   a.chunks = c->chunks.p;
@@ -878,7 +883,8 @@ void win_linearize_current(fmx_ctx* c, const double* poses, double sigma, double
   a.implicit_j = (int)c->K;
   a.inv = 1.0 / sigma;
   // exact row counts arrive with the match counts; the byte model uses the last known
-  win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K);
+  win_start(c, a, c->max_chunks, poses, (int)c->K + 1, 72.0 * c->rows_pl + 48.0 * c->rows_pt + 8.0 * kWinG * c->K,
+            nullptr, false, st);
   if (G_out) win_finish(c, G_out);
 }
 
